@@ -1,0 +1,232 @@
+"""ctypes wrapper around ``librtg_oracle.so`` -- TEST INFRASTRUCTURE ONLY.
+
+The oracle is the CPU restatement of the reference hot path (see
+``rtg_oracle.c`` header for the arithmetic contract).  Only ``tests/``,
+``__graft_entry__.smoke()`` and ``bench.py``'s ``cpu_baseline`` leg may use
+it, and only as the checker / CPU baseline -- never on the product path.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import subprocess
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "librtg_oracle.so")
+
+_f = ctypes.POINTER(ctypes.c_float)
+_d = ctypes.POINTER(ctypes.c_double)
+_i = ctypes.POINTER(ctypes.c_int32)
+_i64 = ctypes.c_int64
+
+_lib = None
+
+
+def build() -> None:
+    subprocess.run(["make", "-s", "-C", HERE], check=True)
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            build()
+        _lib = ctypes.CDLL(LIB_PATH)
+    return _lib
+
+
+def _fp(a: np.ndarray):
+    assert a.dtype == np.float32 and a.flags.c_contiguous
+    return a.ctypes.data_as(_f)
+
+
+def _c32(a) -> np.ndarray:
+    return np.ascontiguousarray(np.asarray(a, dtype=np.float32))
+
+
+def _i32(a) -> np.ndarray:
+    return np.ascontiguousarray(np.asarray(a, dtype=np.int32))
+
+
+def full_body_pos(zl, zg, body, lh, rh, precise_gripper=True, want_rot=True, kabsch_quats=None):
+    """``kabsch_quats`` (B,3,4): optional injected torso/left-wrist/right-wrist Kabsch results."""
+    zl, zg, body, lh, rh = map(_c32, (zl, zg, body, lh, rh))
+    kq = _c32(kabsch_quats) if kabsch_quats is not None else None
+    B = body.shape[0]
+    dof = np.empty((B, 30), np.float32)
+    lr = np.empty((B, 31, 4), np.float32) if want_rot else None
+    br = np.empty((B, 59, 4), np.float32) if want_rot else None
+    lib().oracle_full_body_pos_kq(_fp(zl), _fp(zg), int(precise_gripper), _fp(body), _fp(lh), _fp(rh), _i64(B),
+                                  _fp(dof), _fp(lr) if want_rot else None, _fp(br) if want_rot else None,
+                                  _fp(kq) if kq is not None else None)
+    return dof, lr, br
+
+
+def upper_body(zl, x):
+    zl, x = _c32(zl), _c32(x)
+    B = x.shape[0]
+    dof = np.empty((B, 30), np.float32)
+    lr = np.empty((B, 31, 4), np.float32)
+    lib().oracle_upper_body(_fp(zl), _fp(x), _i64(B), _fp(dof), _fp(lr))
+    return dof, lr
+
+
+def full_body_rot(zl, brot, bpos, lh, rh):
+    zl, brot, bpos, lh, rh = map(_c32, (zl, brot, bpos, lh, rh))
+    B = brot.shape[0]
+    dof = np.empty((B, 30), np.float32)
+    lr = np.empty((B, 31, 4), np.float32)
+    lib().oracle_full_body_rot(_fp(zl), _fp(brot), _fp(bpos), _fp(lh), _fp(rh), _i64(B), _fp(dof), _fp(lr))
+    return dof, lr
+
+
+def body_rot(parents, grot):
+    p, grot = _i32(parents), _c32(grot)
+    B = grot.shape[0]
+    dof = np.empty((B, 30), np.float32)
+    lr = np.empty((B, 31, 4), np.float32)
+    lib().oracle_body_rot(p.ctypes.data_as(_i), _fp(grot), _i64(B), _fp(dof), _fp(lr))
+    return dof, lr
+
+
+def fk(parents, zl, local_rot, root_t):
+    p, zl, lr, rt = _i32(parents), _c32(zl), _c32(local_rot), _c32(root_t)
+    B, J = lr.shape[:2]
+    gr = np.empty((B, J, 4), np.float32)
+    gp = np.empty((B, J, 3), np.float32)
+    lib().oracle_fk(p.ctypes.data_as(_i), _fp(zl), ctypes.c_int32(J), _fp(lr), _fp(rt), _i64(B), _fp(gr), _fp(gp))
+    return gr, gp
+
+
+def local_rotation(parents, g_rot):
+    p, g = _i32(parents), _c32(g_rot)
+    B, J = g.shape[:2]
+    out = np.empty_like(g)
+    lib().oracle_local_rotation(p.ctypes.data_as(_i), ctypes.c_int32(J), _fp(g), _i64(B), _fp(out))
+    return out
+
+
+def state_fk(parents, tree_quat, local_t, local_rot, root_t):
+    p, tq, lt, lr, rt = _i32(parents), _c32(tree_quat), _c32(local_t), _c32(local_rot), _c32(root_t)
+    B, J = lr.shape[:2]
+    gr = np.empty((B, J, 4), np.float32)
+    gp = np.empty((B, J, 3), np.float32)
+    lib().oracle_state_fk(p.ctypes.data_as(_i), _fp(tq), _fp(lt), ctypes.c_int32(J), _fp(lr), _fp(rt), _i64(B),
+                          _fp(gr), _fp(gp))
+    return gr, gp
+
+
+def state_local_rotation(parents, tree_quat, g_rot):
+    p, tq, g = _i32(parents), _c32(tree_quat), _c32(g_rot)
+    B, J = g.shape[:2]
+    out = np.empty_like(g)
+    lib().oracle_state_local_rotation(p.ctypes.data_as(_i), _fp(tq), ctypes.c_int32(J), _fp(g), _i64(B), _fp(out))
+    return out
+
+
+def _unary(name, a, out_shape):
+    a = _c32(a)
+    out = np.empty(out_shape, np.float32)
+    getattr(lib(), name)(_fp(a), _i64(a.shape[0]), _fp(out))
+    return out
+
+
+def _binary(name, a, b, out_shape):
+    a, b = _c32(a), _c32(b)
+    out = np.empty(out_shape, np.float32)
+    getattr(lib(), name)(_fp(a), _fp(b), _i64(a.shape[0]), _fp(out))
+    return out
+
+
+def quat_mul(a, b):
+    return _binary("oracle_quat_mul", a, b, (len(a), 4))
+
+
+def quat_mul_norm(a, b):
+    return _binary("oracle_quat_mul_norm", a, b, (len(a), 4))
+
+
+def quat_normalize(a):
+    return _unary("oracle_quat_normalize", a, (len(a), 4))
+
+
+def quat_rotate(q, v):
+    return _binary("oracle_quat_rotate", q, v, (len(q), 3))
+
+
+def quat_from_angle_axis(angle, axis):
+    return _binary("oracle_quat_from_angle_axis", angle, axis, (len(angle), 4))
+
+
+def quat_from_rotation_matrix(m):
+    return _unary("oracle_quat_from_rotmat", np.reshape(m, (-1, 9)), (len(m), 4))
+
+
+def quat_to_exp_map(q):
+    return _unary("oracle_quat_to_exp_map", q, (len(q), 3))
+
+
+def quat_to_dof_pos(q31):
+    q31 = _c32(q31)
+    out = np.empty((q31.shape[0], 30), np.float32)
+    lib().oracle_quat_to_dof_pos(_fp(q31), _i64(q31.shape[0]), _fp(out))
+    return out
+
+
+def radians_between(v1, v2, n):
+    v1, v2, n = map(_c32, (v1, v2, n))
+    out = np.empty(len(v1), np.float32)
+    lib().oracle_radians_between(_fp(v1), _fp(v2), _fp(n), _i64(len(v1)), _fp(out))
+    return out
+
+
+def cal_joint_quat(Z, M):
+    Z, M = _c32(Z), _c32(M)
+    n, npts = Z.shape[:2]
+    out = np.empty((n, 4), np.float32)
+    lib().oracle_cal_joint_quat(_fp(Z), _fp(M), ctypes.c_int32(npts), _i64(n), _fp(out))
+    return out
+
+
+def kabsch_rotmat(A):
+    A = _c32(np.reshape(A, (-1, 9)))
+    out = np.empty_like(A)
+    lib().oracle_kabsch_rotmat(_fp(A), _i64(len(A)), _fp(out))
+    return out.reshape(-1, 3, 3)
+
+
+def quat_in_xyz_axis(q, seq):
+    q = _c32(q)
+    out = np.empty((len(q), 3, 4), np.float32)
+    lib().oracle_quat_in_xyz_axis(_fp(q), seq.encode(), _i64(len(q)), _fp(out))
+    return out
+
+
+def as_euler(q, seq):
+    q = _c32(q)
+    out = np.empty((len(q), 3), np.float64)
+    lib().oracle_as_euler(_fp(q), seq.encode(), _i64(len(q)), out.ctypes.data_as(_d))
+    return out
+
+
+def shoulder_pr(v1, v0, parent):
+    v1, v0, parent = map(_c32, (v1, v0, parent))
+    out = np.empty((len(v1), 2, 4), np.float32)
+    lib().oracle_shoulder_pr(_fp(v1), _fp(v0), _fp(parent), _i64(len(v1)), _fp(out))
+    return out
+
+
+def elbow_py(v1, v0, parent):
+    v1, v0, parent = map(_c32, (v1, v0, parent))
+    out = np.empty((len(v1), 2, 4), np.float32)
+    lib().oracle_elbow_py(_fp(v1), _fp(v0), _fp(parent), _i64(len(v1)), _fp(out))
+    return out
+
+
+def atan2f(y, x):
+    y, x = _c32(y), _c32(x)
+    out = np.empty_like(y)
+    lib().oracle_atan2f_n(_fp(y), _fp(x), _i64(len(y)), _fp(out))
+    return out

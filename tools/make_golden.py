@@ -1,0 +1,302 @@
+"""Generate golden vectors by running the reference in the build container.
+
+Writes small ``.npz`` fixtures into ``tests/golden/``.  The reference code is
+imported from ``/root/reference`` (never copied); zero poses come from the
+``.npz`` assets (decoded without unpickling).  Inputs are the deterministic
+synthetic frames of ``rtg.synth`` (no recorded mocap ships with the reference).
+
+Fixtures (all float32 unless noted):
+  full_body_pos_precise.npz  VtrdynFullBodyPosRetargeter(precise_gripper=True)   512 frames
+  full_body_pos_binary.npz   VtrdynFullBodyPosRetargeter(precise_gripper=False)  128 frames
+  upper_body.npz             HuUpperBodyFromMocapRetarget                        512 frames
+  full_body_rot.npz          VtrdynFullBodyRetargeter                            256 frames
+  body_rot.npz               Mocap2HuBodyRetargeter                              256 frames
+  kinematics.npz             cal_forward_kinematics / cal_local_rotation /
+                             SkeletonState FK on hu_v5, vtrdyn, vtrdyn_full, noitom
+  primitives.npz             per-primitive vectors incl. edge cases
+  kat_rotation_test.npz      retarget/rotation_test.py known-answer test, restated
+  zero_pose.npz              zero-pose global translations as the reference computes them
+"""
+from __future__ import annotations
+
+import json
+import os
+import sys
+import warnings
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+REPO = os.path.dirname(HERE)
+sys.path.insert(0, HERE)
+sys.path.insert(0, os.path.join(REPO, "humanoid-real-time-retarget_amd"))
+
+import refharness as rh  # noqa: E402
+from rtg import synth  # noqa: E402
+
+OUT = os.path.join(REPO, "tests", "golden")
+warnings.filterwarnings("ignore")
+
+
+def t2n(t):
+    return t.detach().cpu().numpy().astype(np.float32).copy()
+
+
+def gen_full_body_pos(ref, torch, precise, n, seed):
+    full = rh.ref_zero_pose(ref, "vtrdyn_full")
+    hu = rh.ref_zero_pose(ref, "hu_v5")
+    s = ref.full_body_pos.VtrdynFullBodyPosRetargeter(full, hu, precise_gripper=precise)
+    body, lh, rhd = synth.synth_full_body_inputs(n, seed)
+    dof, lr, bg = [], [], []
+    for i in range(n):
+        a, b, c = s.retarget(torch.from_numpy(body[i]), torch.from_numpy(lh[i]), torch.from_numpy(rhd[i]))
+        lr.append(t2n(a)); dof.append(t2n(b)); bg.append(t2n(c))
+    bg = np.stack(bg)
+    return dict(body=body, lh=lh, rh=rhd, dof=np.stack(dof), local_rot=np.stack(lr),
+                body_rot_rows=bg[:, [10, 14, 39]], body_rot_untouched_identity=np.array(
+                    np.all(np.delete(bg, [10, 14, 39], axis=1) == np.array([0, 0, 0, 1], np.float32))),
+                precise_gripper=np.array(precise), seed=np.array(seed))
+
+
+def gen_upper_body(ref, torch, n, seed):
+    vz = rh.ref_zero_pose(ref, "vtrdyn")
+    hu = rh.ref_zero_pose(ref, "hu_v5")
+    s = ref.upper_body.HuUpperBodyFromMocapRetarget(vz, hu)
+    x = synth.synth_upper_body_inputs(n, seed)
+    dof, lr, kq = [], [], []
+    zl = vz.local_translation
+    for i in range(n):
+        xt = torch.from_numpy(x[i])
+        a, b = s.retarget_from_global_translation(xt)
+        lr.append(t2n(a)); dof.append(t2n(b))
+        st = ref.transform3d.coord_transform(xt, dir=torch.Tensor([-1, -1, 1]))
+        kq.append(t2n(ref.transform3d.cal_joint_quat(zl[[17, 13, 11]].unsqueeze(0),
+                                                     (st[[17, 13, 11]] - st[[10]]).unsqueeze(0))).reshape(4))
+    return dict(x=x, dof=np.stack(dof), local_rot=np.stack(lr), kabsch_q=np.stack(kq), seed=np.array(seed))
+
+
+def gen_full_body_rot(ref, torch, n, seed):
+    full = rh.ref_zero_pose(ref, "vtrdyn_full")
+    hu = rh.ref_zero_pose(ref, "hu_v5")
+    s = ref.full_body.VtrdynFullBodyRetargeter(full, hu)
+    brot, bpos, lh, rhd = synth.synth_full_body_rot_inputs(n, seed)
+    dof, lr = [], []
+    for i in range(n):
+        a, b = s.retarget(torch.from_numpy(brot[i]), torch.from_numpy(bpos[i]), None, torch.from_numpy(lh[i]),
+                          None, torch.from_numpy(rhd[i]))
+        lr.append(t2n(a)); dof.append(t2n(b))
+    return dict(body_rot=brot, body_pos=bpos, lh=lh, rh=rhd, dof=np.stack(dof), local_rot=np.stack(lr),
+                seed=np.array(seed))
+
+
+def gen_body_rot(ref, torch, n, seed):
+    br_mod = rh.load_body_retargeter_module(ref)
+    vz = rh.ref_zero_pose(ref, "vtrdyn")
+    hu = rh.ref_zero_pose(ref, "hu_v5")
+    s = br_mod.Mocap2HuBodyRetargeter(vz, hu)
+    _, grot = synth.synth_body21_pose(n, seed)
+    dof, lr = [], []
+    for i in range(n):
+        a, b = s.retarget_from_pose(torch.from_numpy(grot[i]))
+        lr.append(t2n(a)); dof.append(t2n(b))
+    return dict(global_rot=grot, dof=np.stack(dof), local_rot=np.stack(lr), seed=np.array(seed))
+
+
+def gen_kinematics(ref, torch, n):
+    out = {}
+    for k, name in enumerate(["hu_v5", "vtrdyn", "vtrdyn_full", "noitom"]):
+        st = rh.ref_skeleton_state(ref, name)
+        tree = st.skeleton_tree
+        J = tree.num_joints
+        lr = synth.random_local_quats(n, J, 100 + k)
+        rt = np.random.default_rng(200 + k).normal(0, 0.3, (n, 3)).astype(np.float32)
+        gr, gp = ref.rkm.cal_forward_kinematics(torch.from_numpy(lr), torch.from_numpy(rt),
+                                                tree.parent_indices, tree.local_translation)
+        loc = ref.rkm.cal_local_rotation(gr, tree.parent_indices)
+        sk = ref.skeleton3d.SkeletonState.from_rotation_and_root_translation(
+            tree, torch.from_numpy(lr), torch.from_numpy(rt), is_local=True)
+        out[f"{name}_local_rot"] = lr
+        out[f"{name}_root_t"] = rt
+        out[f"{name}_g_rot"] = t2n(gr)
+        out[f"{name}_g_pos"] = t2n(gp)
+        out[f"{name}_inv_local"] = t2n(loc)
+        out[f"{name}_state_g_rot"] = t2n(sk.global_rotation)
+        out[f"{name}_state_g_pos"] = t2n(sk.global_translation)
+        skg = ref.skeleton3d.SkeletonState.from_rotation_and_root_translation(
+            tree, torch.from_numpy(out[f"{name}_state_g_rot"]), torch.from_numpy(rt), is_local=False)
+        out[f"{name}_state_local_rot"] = t2n(skg.local_rotation)
+    return out
+
+
+def _rand_quats(rng, n):
+    q = rng.normal(size=(n, 4))
+    q /= np.linalg.norm(q, axis=-1, keepdims=True)
+    return q.astype(np.float32)
+
+
+def gen_primitives(ref, torch):
+    r3 = ref.rotation3d
+    tf = ref.transform3d
+    fb = ref.full_body_pos
+    rng = np.random.default_rng(7)
+    out = {}
+    n = 1024
+    a = _rand_quats(rng, n) * rng.uniform(0.5, 2.0, (n, 1)).astype(np.float32)
+    b = _rand_quats(rng, n)
+    out["qm_a"], out["qm_b"] = a, b
+    out["quat_mul"] = t2n(r3.quat_mul(torch.from_numpy(a), torch.from_numpy(b)))
+    out["quat_mul_norm"] = t2n(r3.quat_mul_norm(torch.from_numpy(a), torch.from_numpy(b)))
+    out["quat_normalize"] = t2n(r3.quat_normalize(torch.from_numpy(a)))
+    v = rng.normal(size=(n, 3)).astype(np.float32)
+    out["qr_v"] = v
+    out["quat_rotate"] = t2n(r3.quat_rotate(torch.from_numpy(b), torch.from_numpy(v)))
+    # quat_from_angle_axis: random + small / pi / >pi / deadzone angles
+    ang = np.concatenate([rng.uniform(-4, 4, n - 16),
+                          np.array([0, 1e-4, -1e-4, 3e-4, 4.9e-4, 6e-4, -6e-4, np.pi, -np.pi, 2 * np.pi,
+                                    3.5, -3.5, 1e-7, 0.5, -0.5, 1.0])]).astype(np.float32)
+    axs = rng.normal(size=(n, 3)).astype(np.float32)
+    axs[-16:] = np.eye(3, dtype=np.float32)[np.arange(16) % 3]
+    out["qaa_angle"], out["qaa_axis"] = ang, axs
+    out["quat_from_angle_axis"] = t2n(r3.quat_from_angle_axis(torch.from_numpy(ang), torch.from_numpy(axs)))
+    # quat_from_rotation_matrix: random rotations + 180deg + tie cases
+    from scipy.spatial.transform import Rotation as sRot
+    mats = sRot.from_quat(_rand_quats(rng, n - 8).astype(np.float64)).as_matrix()
+    special = [np.diag([1.0, -1, -1]), np.diag([-1.0, 1, -1]), np.diag([-1.0, -1, 1]), np.eye(3),
+               sRot.from_rotvec([np.pi / 2, 0, 0]).as_matrix(), sRot.from_rotvec([0, np.pi / 2, 0]).as_matrix(),
+               sRot.from_rotvec([0, 0, np.pi / 2]).as_matrix(), sRot.from_rotvec([np.pi / 2, np.pi / 2, 0]).as_matrix()]
+    mats = np.concatenate([mats, np.stack(special)]).astype(np.float32)
+    out["qrm_m"] = mats
+    out["quat_from_rotation_matrix"] = t2n(r3.quat_from_rotation_matrix(torch.from_numpy(mats)))
+    # quat_to_dof_pos on (30,4) chunks -- the hot-path shape (atan2 takes glibc's scalar path)
+    q31 = _rand_quats(rng, 64 * 31).reshape(64, 31, 4)
+    q31[..., 3] = np.abs(q31[..., 3])
+    small = np.array([0, 1e-4, 3e-4, 4.9e-4, 6e-4, 1e-3, 1e-2, 3.1], np.float32)
+    for i, s in enumerate(small):   # single-axis small rotations (exp-map deadzone)
+        q31[i, 1:, :] = 0
+        q31[i, 1:, 3] = np.cos(s / 2)
+        q31[i, 1:, 1] = np.sin(s / 2)
+    q31 = q31.astype(np.float32)
+    out["dof_q31"] = q31
+    out["quat_to_dof_pos"] = np.stack([t2n(tf.quat_to_dof_pos(torch.from_numpy(q31[i, 1:]), ref.Hu_v5.Hu_DOF_AXIS))
+                                       for i in range(len(q31))])
+    # radians_between_vecs / proj_in_plane (1-D only in the reference)
+    m = 512
+    v1 = rng.normal(size=(m, 3)).astype(np.float32)
+    v2 = rng.normal(size=(m, 3)).astype(np.float32)
+    v2[:8] = v1[:8] * np.float32(2.0)                       # parallel: sign(0) -> 0
+    v2[8:16] = v1[8:16] + rng.normal(0, 1e-4, (8, 3)).astype(np.float32)   # near parallel
+    nn = rng.normal(size=(m, 3)).astype(np.float32)
+    out["rbv_v1"], out["rbv_v2"], out["rbv_n"] = v1, v2, nn
+    out["radians_between_vecs"] = np.array([tf.radians_between_vecs(torch.from_numpy(v1[i]), torch.from_numpy(v2[i]),
+                                                                    torch.from_numpy(nn[i])).item()
+                                            for i in range(m)], np.float32)
+    eye = torch.eye(3)
+    out["proj_in_plane_y"] = np.stack([t2n(tf.proj_in_plane(torch.from_numpy(v1[i]), eye[1])) for i in range(m)])
+    out["proj_in_plane_z"] = np.stack([t2n(tf.proj_in_plane(torch.from_numpy(v1[i]), eye[2])) for i in range(m)])
+    # cal_joint_quat (Kabsch) with 3 and 5 points
+    for npts in (3, 5):
+        k = 256
+        Z = rng.normal(0, 0.1, (k, npts, 3)).astype(np.float32)
+        if npts == 3:
+            Z[:k // 2, :, 0] = 0.0          # rank-2 like the torso fit
+        R = sRot.from_quat(_rand_quats(rng, k).astype(np.float64)).as_matrix()
+        M = (np.einsum("kij,knj->kni", R, Z.astype(np.float64)) + rng.normal(0, 0.002, Z.shape)).astype(np.float32)
+        M[-4:] = -M[-4:]                     # reflection-only fits (det fix path)
+        out[f"cjq{npts}_Z"], out[f"cjq{npts}_M"] = Z, M
+        out[f"cal_joint_quat{npts}"] = np.stack([t2n(tf.cal_joint_quat(torch.from_numpy(Z[i:i + 1]),
+                                                                       torch.from_numpy(M[i:i + 1]))).reshape(4)
+                                                 for i in range(k)])
+    # quat_in_xyz_axis (scipy float64 Euler) incl. gimbal lock
+    qe = _rand_quats(rng, 512)
+    gl = sRot.from_euler("XYZ", [[0.3, np.pi / 2, 0.2], [0.1, -np.pi / 2, -0.4]]).as_quat().astype(np.float32)
+    qe[:2] = gl
+    out["qxyz_q"] = qe
+    for seq in ("XYZ", "YXZ", "ZYX"):
+        res = [tf.quat_in_xyz_axis(torch.from_numpy(qe[i:i + 1]), seq) for i in range(len(qe))]
+        out[f"quat_in_xyz_axis_{seq}"] = np.stack([np.stack([t2n(r[j]).reshape(4) for j in range(3)]) for r in res])
+    # cal_shoulderPR / cal_elbowP_and_shoulderY
+    k = 512
+    sv1 = rng.normal(0, 0.3, (k, 3)).astype(np.float32)
+    par = _rand_quats(rng, k)
+    par[:, 3] = np.abs(par[:, 3])
+    full = rh.ref_zero_pose(ref, "vtrdyn_full")
+    sv0 = np.broadcast_to(t2n(full.local_translation[13]), (k, 3)).copy()
+    ev0 = np.broadcast_to(t2n(full.local_translation[14]), (k, 3)).copy()
+    out["sh_v1"], out["sh_v0"], out["el_v0"], out["sh_parent"] = sv1, sv0, ev0, par
+    spr, epy = [], []
+    for i in range(k):
+        p_, r_ = fb.cal_shoulderPR(torch.from_numpy(sv1[i]), torch.from_numpy(sv0[i]), torch.from_numpy(par[i:i + 1]))
+        spr.append(np.stack([t2n(p_).reshape(4), t2n(r_).reshape(4)]))
+        y_, e_ = fb.cal_elbowP_and_shoulderY(torch.from_numpy(sv1[i]), torch.from_numpy(ev0[i]),
+                                             torch.from_numpy(par[i:i + 1]))
+        epy.append(np.stack([t2n(y_).reshape(4), t2n(e_).reshape(4)]))
+    out["cal_shoulderPR"] = np.stack(spr)
+    out["cal_elbowP_and_shoulderY"] = np.stack(epy)
+    return out
+
+
+def gen_kat(ref, torch):
+    """retarget/rotation_test.py:95-152 restated as data: arm segments from known joint angles."""
+    r3 = ref.rotation3d
+    fb = ref.full_body_pos
+    p = [torch.tensor([[0., 0., 0.]]), torch.tensor([[0., -1., 0.]]), torch.tensor([[0., -1., -1.]]),
+         torch.tensor([[1., -1., -1.]])]
+    vec0, vec1, vec2 = p[1] - p[0], p[2] - p[1], p[3] - p[2]
+    f = torch.float32
+    quat0 = r3.quat_from_angle_axis(torch.tensor([0.0], dtype=f), torch.tensor([0, 0, 1], dtype=f))
+    q11 = r3.quat_from_angle_axis(torch.tensor([0.0], dtype=f), torch.tensor([0, 1, 0], dtype=f))
+    q12 = r3.quat_from_angle_axis(torch.tensor([-0.0], dtype=f), torch.tensor([1, 0, 0], dtype=f))
+    q13 = r3.quat_from_angle_axis(torch.tensor([-torch.pi / 6], dtype=f), torch.tensor([0, 0, 1], dtype=f))
+    q2 = r3.quat_from_angle_axis(torch.tensor([torch.pi / 4], dtype=f), torch.tensor([0, 1, 0], dtype=f))
+    q1 = r3.quat_mul_three(q11, q12, q13)
+    v1t = r3.quat_rotate(r3.quat_mul_norm(quat0, q1), vec1)
+    v2t = r3.quat_rotate(r3.quat_mul_norm(r3.quat_mul_norm(quat0, q1), q2), vec2)
+    pitch, roll = fb.cal_shoulderPR(v1t[0], vec1[0], quat0)
+    comb = r3.quat_mul_three(quat0, pitch, roll)
+    v1cal = r3.quat_rotate(comb, vec1)
+    yaw, elbow = fb.cal_elbowP_and_shoulderY(v2t[0], vec2[0], comb)
+    v2cal = r3.quat_rotate(r3.quat_mul_three(comb, yaw, elbow), vec2)
+    assert torch.allclose(v1cal, v1t, rtol=1e-3, atol=1e-6)
+    assert torch.allclose(v2cal, v2t, rtol=1e-3, atol=1e-6)
+    return dict(vec1=t2n(vec1), vec2=t2n(vec2), quat0=t2n(quat0), v1t=t2n(v1t), v2t=t2n(v2t),
+                pitch=t2n(pitch), roll=t2n(roll), yaw=t2n(yaw), elbow=t2n(elbow), v1cal=t2n(v1cal), v2cal=t2n(v2cal))
+
+
+def main() -> None:
+    import torch
+    torch.set_num_threads(1)
+    ref = rh.load_reference()
+    os.makedirs(OUT, exist_ok=True)
+    zp = {}
+    for name in ["hu_v5", "vtrdyn", "vtrdyn_full", "noitom"]:
+        z = rh.ref_zero_pose(ref, name)
+        zp[f"{name}_local_t"] = t2n(z.local_translation)
+        zp[f"{name}_global_t"] = t2n(z.global_translation)
+    np.savez_compressed(os.path.join(OUT, "zero_pose.npz"), **zp)
+    jobs = {
+        "full_body_pos_precise": lambda: gen_full_body_pos(ref, torch, True, 512, 1234),
+        "full_body_pos_binary": lambda: gen_full_body_pos(ref, torch, False, 128, 4321),
+        "upper_body": lambda: gen_upper_body(ref, torch, 512, 2345),
+        "full_body_rot": lambda: gen_full_body_rot(ref, torch, 256, 3456),
+        "body_rot": lambda: gen_body_rot(ref, torch, 256, 5678),
+        "kinematics": lambda: gen_kinematics(ref, torch, 128),
+        "primitives": lambda: gen_primitives(ref, torch),
+        "kat_rotation_test": lambda: gen_kat(ref, torch),
+    }
+    only = set(sys.argv[1:])
+    for name, fn in jobs.items():
+        if only and name not in only:
+            continue
+        d = fn()
+        np.savez_compressed(os.path.join(OUT, f"{name}.npz"), **d)
+        print(f"wrote {name}.npz")
+    meta = {"torch": torch.__version__, "mkl": "2024.2", "generator": "tools/make_golden.py",
+            "reference": "shuoshuof/Humanoid-Real-Time-Retarget @ 2024-12-20 (read-only /root/reference)"}
+    import scipy
+    meta["scipy"] = scipy.__version__
+    with open(os.path.join(OUT, "META.json"), "w") as f:
+        json.dump(meta, f, indent=2)
+
+
+if __name__ == "__main__":
+    main()
