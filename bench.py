@@ -1,0 +1,204 @@
+"""Throughput bench of the batched retarget hot path (BASELINE.json metric).
+
+One step = one launch of VtrdynFullBodyPosRetargeter's batched solver over a
+batch of synthetic VTRDyn frames already resident in HBM (BASELINE config 3:
+262144 frames per GPU, fp32).  Inputs are generated on the device (seed
+1234 + rank) into a ring of buffer sets larger than the 256 MiB Infinity Cache
+so every timed step reads cold HBM.  Frames shard across ranks with no
+data-path collective ("scaling": "weak"); the RCCL broadcast of the solver
+constants happens at setup and the DOF gather after the timed region.
+
+  python bench.py [--gpus N] [--steps K] [--warmup W] [--batch B]
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import subprocess
+import sys
+import time
+
+import numpy as np
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+PKG = os.path.join(REPO, "humanoid-real-time-retarget_amd")
+sys.path.insert(0, PKG)
+sys.path.insert(0, os.path.join(REPO, "oracle"))
+
+METRIC = "retargeted frames/sec + max joint-angle err vs ref, Hu humanoid @1/2/4/8 GPU"
+BYTES_PER_FRAME = 504          # 32 used input points x 12 B + 30 DOF x 4 B
+HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md: 8.0 TB/s spec
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--batch", type=int, default=262144, help="frames per GPU per step")
+    ap.add_argument("--ring", type=int, default=0, help="input buffer sets (0 = enough to exceed 256 MiB x 2)")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-seconds", type=float, default=12.0)
+    return ap.parse_args()
+
+
+def dist_setup(args):
+    import torch
+    import torch.distributed as dist
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    else:
+        torch.cuda.set_device(0)
+    return world, rank, local
+
+
+def barrier(world):
+    import torch
+    if world > 1:
+        import torch.distributed as dist
+        dist.barrier()
+    torch.cuda.synchronize()
+
+
+def cpu_baseline(body, lh, rh, zl, zg, seconds):
+    """Oracle (the C port of the reference path) on the host cores, bounded sample."""
+    import oracle as orc
+    threads = int(os.environ.get("OMP_NUM_THREADS", str(min(16, os.cpu_count() or 1))))
+    n = body.shape[0]
+    orc.full_body_pos(zl, zg, body[:256], lh[:256], rh[:256], True, want_rot=False)   # warm
+    done, t0 = 0, time.perf_counter()
+    while time.perf_counter() - t0 < seconds:
+        orc.full_body_pos(zl, zg, body, lh, rh, True, want_rot=False)
+        done += n
+    dt = time.perf_counter() - t0
+    try:
+        model = [l.split(":", 1)[1].strip() for l in open("/proc/cpuinfo") if l.startswith("model name")][0]
+    except Exception:  # noqa: BLE001
+        model = "unknown"
+    return {"value": done / dt, "unit": "frames/s", "cores": threads, "kind": "port",
+            "sample": f"{done} synthetic frames ({n}-frame slices of the bench workload), oracle/rtg_oracle.c "
+                      f"OpenMP x{threads}, {dt:.1f} s", "cpu": model}
+
+
+def parity_vs_reference():
+    """max / p99 |dof_gpu - dof_ref| on the committed reference golden vectors."""
+    import torch
+    from rtg import _lib, assets
+    from rtg.runtime import Solver
+    g = np.load(os.path.join(REPO, "tests", "golden", "full_body_pos_precise.npz"))
+    zp = np.load(os.path.join(REPO, "tests", "golden", "zero_pose.npz"))
+    S = Solver(_lib.SOLVER_FULL_BODY_POS, zp["vtrdyn_full_local_t"], zp["vtrdyn_full_global_t"],
+               assets.parents("vtrdyn_full"), True)
+    dof, _, _ = S.retarget([torch.from_numpy(np.ascontiguousarray(g[k])).cuda() for k in ("body", "lh", "rh")])
+    e = np.abs(dof.cpu().numpy().astype(np.float64) - g["dof"])
+    fm = e.max(1)
+    return {"frames": int(len(fm)), "max_abs_err": float(e.max()), "p99_frame_err": float(np.quantile(fm, 0.99)),
+            "median_frame_err": float(np.median(fm)), "frac_frames_le_1e-5": float(np.mean(fm <= 1e-5)),
+            "unit": "rad (DOFs 18,19,27,28: m)"}
+
+
+def main():
+    args = parse()
+    import torch
+    world, rank, local = dist_setup(args)
+    from rtg import _lib, assets, ops
+    from rtg.runtime import Solver, Topology
+
+    B = args.batch
+    dev = torch.device("cuda", local)
+    # solver constants: rank 0 owns the zero pose; RCCL broadcast to the other ranks (setup, untimed)
+    zl = torch.from_numpy(assets.local_translation("vtrdyn_full")).to(dev)
+    topo_full = Topology(assets.parents("vtrdyn_full"), zl.cpu().numpy(), assets.tree_quat("vtrdyn_full"))
+    zg = ops.forward_kinematics(topo_full, torch.tensor([[0, 0, 0, 1.0]]).expand(1, 59, 4),
+                                torch.zeros(1, 3), state=True)[1][0]
+    if world > 1:
+        import torch.distributed as dist
+        blob = torch.cat([zl.reshape(-1), zg.reshape(-1)]).contiguous()
+        dist.broadcast(blob, src=0)
+        zl, zg = blob[:177].reshape(59, 3), blob[177:].reshape(59, 3)
+    solver = Solver(_lib.SOLVER_FULL_BODY_POS, zl.cpu().numpy(), zg.cpu().numpy(), assets.parents("vtrdyn_full"),
+                    precise_gripper=True)
+
+    bytes_per_set = B * (63 + 60 + 60 + 30) * 4
+    ring = args.ring or max(2, int(np.ceil(2 * 256 * 2**20 / bytes_per_set)))
+    sets = []
+    for r in range(ring):
+        body, lh, rh = ops.synth_full_body(topo_full, B, seed=1234 + rank, frame_offset=r * B)
+        dof = torch.empty((B, 30), device=dev, dtype=torch.float32)
+        sets.append((body, lh, rh, dof))
+    torch.cuda.synchronize()
+
+    stream = torch.cuda.current_stream()
+    for i in range(args.warmup):
+        b, l, r_, d = sets[i % ring]
+        solver.retarget([b, l, r_], out_dof=d)
+    barrier(world)
+    starts = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps)]
+    ends = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps)]
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        b, l, r_, d = sets[i % ring]
+        starts[i].record(stream)
+        solver.retarget([b, l, r_], out_dof=d)
+        ends[i].record(stream)
+    barrier(world)
+    wall = time.perf_counter() - t0
+    kern_ms = float(np.mean([s.elapsed_time(e) for s, e in zip(starts, ends)]))
+    if world > 1:
+        import torch.distributed as dist
+        tw = torch.tensor([wall], device=dev, dtype=torch.float64)
+        dist.all_reduce(tw, op=dist.ReduceOp.MAX)
+        wall = float(tw.item())
+    frames = world * B * args.steps
+    value = frames / wall
+    ms_per_step = wall * 1e3 / args.steps
+
+    gather_ms = None
+    if world > 1:   # final DOF gather to rank 0 over RCCL (untimed region, reported separately)
+        import torch.distributed as dist
+        d = sets[(args.steps - 1) % ring][3]
+        outs = [torch.empty_like(d) for _ in range(world)] if rank == 0 else None
+        torch.cuda.synchronize()
+        tg = time.perf_counter()
+        dist.gather(d, outs, dst=0)
+        torch.cuda.synchronize()
+        gather_ms = (time.perf_counter() - tg) * 1e3
+
+    if rank == 0:
+        achieved = BYTES_PER_FRAME * B / (kern_ms * 1e-3) / 1e9
+        line = {
+            "metric": METRIC, "value": value, "unit": "frames/s", "n_gpus": world, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": ms_per_step, "higher_is_better": True, "scaling": "weak",
+            "vs_baseline": None, "dtype": "f32", "data": "synthetic (device-generated VTRDyn frames, seed 1234+rank)",
+            "config": {"workload": "VtrdynFullBodyPosRetargeter batched solve, Hu v5 target (BASELINE config 3)",
+                       "frames_per_gpu_per_step": B, "global_batch": B * world, "parallelism": f"dp{world}",
+                       "input_ring_sets": ring, "precise_gripper": True},
+            "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": achieved / HBM_PEAK_GBS, "traffic": None,
+                         "kernel": "k_retarget<FULL_BODY_POS>", "kernel_ms": kern_ms,
+                         "bytes_per_frame": BYTES_PER_FRAME},
+        }
+        if gather_ms is not None:
+            line["gather_ms"] = gather_ms
+        try:
+            line["parity_vs_reference"] = parity_vs_reference()
+        except Exception as e:  # noqa: BLE001
+            line["parity_vs_reference"] = {"error": repr(e)}
+        if world == 1 and not args.no_cpu_baseline:
+            b, l, r_, _ = sets[0]
+            n = min(B, 65536)
+            line["cpu_baseline"] = cpu_baseline(b[:n].cpu().numpy(), l[:n].cpu().numpy(), r_[:n].cpu().numpy(),
+                                                zl.cpu().numpy(), zg.cpu().numpy(), args.cpu_seconds)
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        import torch.distributed as dist
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,358 @@
+// rtg_api.cpp -- C ABI (include/rtg.h) over the gfx950 kernels.
+//
+// Host-side only: argument validation (mirroring the reference's assertions),
+// handle lifetime, and stream-ordered launches.  Launch entry points never
+// allocate, copy or synchronise, so callers may capture them into hipGraphs.
+#include <hip/hip_runtime.h>
+
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <new>
+#include <string>
+
+#include "rtg_kernels.cuh"
+
+using namespace rtg;
+
+struct rtg_topology_s {
+    int32_t J = 0;
+    int32_t *d_parents = nullptr;
+    V *d_local_t = nullptr;
+    Q *d_tree_quat = nullptr;
+    TopoView view() const { return TopoView{d_parents, d_local_t, d_tree_quat, J}; }
+};
+
+struct rtg_solver_s {
+    int kind = 0;
+    int precise = 0;
+    SolverConsts consts{};
+};
+
+namespace {
+
+thread_local std::string g_err;
+
+int fail(int code, const char *fmt, ...) __attribute__((format(printf, 2, 3)));
+int fail(int code, const char *fmt, ...)
+{
+    char buf[512];
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(buf, sizeof buf, fmt, ap);
+    va_end(ap);
+    g_err = buf;
+    return code;
+}
+
+int hip_check(hipError_t e, const char *what)
+{
+    if (e == hipSuccess) return RTG_OK;
+    return fail(e == hipErrorOutOfMemory ? RTG_ERR_OUT_OF_MEMORY : RTG_ERR_DEVICE, "%s: %s", what,
+                hipGetErrorString(e));
+}
+
+#define RTG_TRY(expr, what)                          \
+    do {                                             \
+        int rc_ = hip_check((expr), (what));         \
+        if (rc_ != RTG_OK) return rc_;               \
+    } while (0)
+
+inline hipStream_t as_stream(rtg_stream_t s) { return reinterpret_cast<hipStream_t>(s); }
+inline V v3(const float *p, int j) { return V{p[3 * j], p[3 * j + 1], p[3 * j + 2]}; }
+
+int axis_of(char c, int *ax, int *lower)
+{
+    switch (c) {
+    case 'x': *ax = 0; *lower = 1; return 1;
+    case 'y': *ax = 1; *lower = 1; return 1;
+    case 'z': *ax = 2; *lower = 1; return 1;
+    case 'X': *ax = 0; *lower = 0; return 1;
+    case 'Y': *ax = 1; *lower = 0; return 1;
+    case 'Z': *ax = 2; *lower = 0; return 1;
+    default: return 0;
+    }
+}
+
+}  // namespace
+
+extern "C" {
+
+int rtg_abi_version(void) { return RTG_ABI_VERSION; }
+
+const char *rtg_last_error(void) { return g_err.c_str(); }
+
+int rtg_device_count(void)
+{
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess) return 0;
+    return n;
+}
+
+// ---------------------------------------------------------------- topology
+int rtg_topology_create(const int32_t *parents, const float *local_t, const float *tree_quat, int32_t J,
+                        rtg_topology_t *out)
+{
+    if (!out) return fail(RTG_ERR_INVALID_ARGUMENT, "rtg_topology_create: out is NULL");
+    *out = nullptr;
+    if (!parents || !local_t) return fail(RTG_ERR_INVALID_ARGUMENT, "rtg_topology_create: NULL parents/local_t");
+    if (J < 1 || J > 1024) return fail(RTG_ERR_INVALID_ARGUMENT, "rtg_topology_create: J=%d out of range", J);
+    // parent-indexed tree in topological order (skeleton3d.py:87-88 asserts equal lengths;
+    // the FK loop kinematics.py:27 requires parents before children)
+    if (parents[0] != -1) return fail(RTG_ERR_INVALID_ARGUMENT, "rtg_topology_create: joint 0 must be the root");
+    for (int j = 1; j < J; ++j)
+        if (parents[j] < 0 || parents[j] >= j)
+            return fail(RTG_ERR_INVALID_ARGUMENT, "rtg_topology_create: parents[%d]=%d is not < %d", j, parents[j], j);
+    rtg_topology_s *t = new (std::nothrow) rtg_topology_s();
+    if (!t) return fail(RTG_ERR_OUT_OF_MEMORY, "rtg_topology_create: host allocation failed");
+    t->J = J;
+    Q *tq = new (std::nothrow) Q[J];
+    if (!tq) {
+        delete t;
+        return fail(RTG_ERR_OUT_OF_MEMORY, "rtg_topology_create: host allocation failed");
+    }
+    for (int j = 0; j < J; ++j)
+        tq[j] = tree_quat ? Q{tree_quat[4 * j], tree_quat[4 * j + 1], tree_quat[4 * j + 2], tree_quat[4 * j + 3]}
+                          : Q{0.f, 0.f, 0.f, 1.f};
+    int rc = hip_check(hipMalloc(&t->d_parents, sizeof(int32_t) * J), "hipMalloc(parents)");
+    if (rc == RTG_OK) rc = hip_check(hipMalloc(&t->d_local_t, sizeof(V) * J), "hipMalloc(local_t)");
+    if (rc == RTG_OK) rc = hip_check(hipMalloc(&t->d_tree_quat, sizeof(Q) * J), "hipMalloc(tree_quat)");
+    if (rc == RTG_OK)
+        rc = hip_check(hipMemcpy(t->d_parents, parents, sizeof(int32_t) * J, hipMemcpyHostToDevice), "hipMemcpy");
+    if (rc == RTG_OK)
+        rc = hip_check(hipMemcpy(t->d_local_t, local_t, sizeof(V) * J, hipMemcpyHostToDevice), "hipMemcpy");
+    if (rc == RTG_OK) rc = hip_check(hipMemcpy(t->d_tree_quat, tq, sizeof(Q) * J, hipMemcpyHostToDevice), "hipMemcpy");
+    delete[] tq;
+    if (rc != RTG_OK) {
+        (void)hipFree(t->d_parents);
+        (void)hipFree(t->d_local_t);
+        (void)hipFree(t->d_tree_quat);
+        delete t;
+        return rc;
+    }
+    *out = t;
+    return RTG_OK;
+}
+
+int rtg_topology_destroy(rtg_topology_t t)
+{
+    if (!t) return RTG_OK;
+    (void)hipFree(t->d_parents);
+    (void)hipFree(t->d_local_t);
+    (void)hipFree(t->d_tree_quat);
+    delete t;
+    return RTG_OK;
+}
+
+int rtg_topology_num_joints(rtg_topology_t t) { return t ? t->J : -1; }
+
+// ---------------------------------------------------------------- kinematics
+static int check_fk(rtg_topology_t t, const void *a, const void *b, const void *c, const void *d, int64_t B,
+                    const char *fn)
+{
+    if (!t) return fail(RTG_ERR_INVALID_ARGUMENT, "%s: NULL topology", fn);
+    if (B < 0) return fail(RTG_ERR_INVALID_ARGUMENT, "%s: negative batch %lld", fn, (long long)B);
+    if (B > 0 && (!a || !b || !c || !d)) return fail(RTG_ERR_INVALID_ARGUMENT, "%s: NULL buffer", fn);
+    return RTG_OK;
+}
+
+int rtg_fk_f32(rtg_topology_t t, const float *local_rot, const float *root_t, int64_t B, float *g_rot, float *g_pos,
+               rtg_stream_t stream)
+{
+    int rc = check_fk(t, local_rot, root_t, g_rot, g_pos, B, "rtg_fk_f32");
+    if (rc != RTG_OK || B == 0) return rc;
+    RTG_TRY(launch_fk(t->view(), false, local_rot, root_t, B, g_rot, g_pos, as_stream(stream)), "k_fk");
+    return RTG_OK;
+}
+
+int rtg_state_fk_f32(rtg_topology_t t, const float *local_rot, const float *root_t, int64_t B, float *g_rot,
+                     float *g_pos, rtg_stream_t stream)
+{
+    int rc = check_fk(t, local_rot, root_t, g_rot, g_pos, B, "rtg_state_fk_f32");
+    if (rc != RTG_OK || B == 0) return rc;
+    RTG_TRY(launch_fk(t->view(), true, local_rot, root_t, B, g_rot, g_pos, as_stream(stream)), "k_fk<state>");
+    return RTG_OK;
+}
+
+int rtg_local_rotation_f32(rtg_topology_t t, const float *g_rot, int64_t B, float *local_rot, rtg_stream_t stream)
+{
+    int rc = check_fk(t, g_rot, local_rot, g_rot, local_rot, B, "rtg_local_rotation_f32");
+    if (rc != RTG_OK || B == 0) return rc;
+    RTG_TRY(launch_local_rotation(t->view(), false, g_rot, B, local_rot, as_stream(stream)), "k_local_rotation");
+    return RTG_OK;
+}
+
+int rtg_state_local_rotation_f32(rtg_topology_t t, const float *g_rot, int64_t B, float *local_rot,
+                                 rtg_stream_t stream)
+{
+    int rc = check_fk(t, g_rot, local_rot, g_rot, local_rot, B, "rtg_state_local_rotation_f32");
+    if (rc != RTG_OK || B == 0) return rc;
+    RTG_TRY(launch_local_rotation(t->view(), true, g_rot, B, local_rot, as_stream(stream)), "k_local_rotation<state>");
+    return RTG_OK;
+}
+
+int rtg_fk_multi_f32(const rtg_fk_segment *segs, int32_t n, rtg_stream_t stream)
+{
+    if (n < 0 || n > RTG_MAX_SEGMENTS)
+        return fail(RTG_ERR_INVALID_ARGUMENT, "rtg_fk_multi_f32: %d segments (max %d)", n, RTG_MAX_SEGMENTS);
+    if (n > 0 && !segs) return fail(RTG_ERR_INVALID_ARGUMENT, "rtg_fk_multi_f32: NULL segments");
+    FkMultiArgs A{};
+    A.n = n;
+    for (int i = 0; i < n; ++i) {
+        const rtg_fk_segment &s = segs[i];
+        int rc = check_fk(s.topo, s.local_rot, s.root_t, s.g_rot, s.g_pos, s.B, "rtg_fk_multi_f32");
+        if (rc != RTG_OK) return rc;
+        A.seg[i] = FkSeg{s.topo->view(), s.local_rot, s.root_t, s.g_rot, s.g_pos, s.B};
+    }
+    RTG_TRY(launch_fk_multi(A, as_stream(stream)), "k_fk_multi");
+    return RTG_OK;
+}
+
+// ---------------------------------------------------------------- solvers
+int rtg_solver_create(int kind, const float *zl, const float *zg, const int32_t *parents, int32_t Js,
+                      int precise_gripper, rtg_solver_t *out)
+{
+    if (!out) return fail(RTG_ERR_INVALID_ARGUMENT, "rtg_solver_create: out is NULL");
+    *out = nullptr;
+    if (!zl) return fail(RTG_ERR_INVALID_ARGUMENT, "rtg_solver_create: NULL zero-pose local translation");
+    SolverConsts C{};
+    switch (kind) {
+    case RTG_SOLVER_FULL_BODY_POS: {
+        if (Js != 59) return fail(RTG_ERR_INVALID_ARGUMENT, "FULL_BODY_POS expects the 59-joint VTRDYN_FULL zero pose, got %d", Js);
+        if (!zg) return fail(RTG_ERR_INVALID_ARGUMENT, "FULL_BODY_POS needs the zero-pose global translation");
+        // full_body_pos_retargeter.py:69, :139, :162, :78/:86/:99/:107, :184
+        C.Zt[0] = v3(zl, 11); C.Zt[1] = v3(zl, 36); C.Zt[2] = v3(zl, 34);
+        const int li[5] = {16, 20, 24, 28, 32}, ri[5] = {41, 45, 49, 53, 56}, gi[5] = {18, 22, 26, 30, 33};
+        for (int t = 0; t < 5; ++t) {
+            C.Zl[t] = v3(zl, li[t]);
+            C.Zr[t] = v3(zl, ri[t]);
+            C.grip_d[t] = zg[3 * gi[t]] - zg[3 * 14];
+        }
+        C.v0_lsh = v3(zl, 13); C.v0_lel = v3(zl, 14); C.v0_rsh = v3(zl, 38); C.v0_rel = v3(zl, 39);
+        break;
+    }
+    case RTG_SOLVER_UPPER_BODY:
+        if (Js != 21) return fail(RTG_ERR_INVALID_ARGUMENT, "UPPER_BODY expects the 21-joint VTRDYN zero pose, got %d", Js);
+        // retarget_solver.py:49-86
+        C.Zt[0] = v3(zl, 17); C.Zt[1] = v3(zl, 13); C.Zt[2] = v3(zl, 11);
+        C.v0_lsh = v3(zl, 19); C.v0_lel = v3(zl, 20); C.v0_rsh = v3(zl, 15); C.v0_rel = v3(zl, 16);
+        break;
+    case RTG_SOLVER_FULL_BODY_ROT: {
+        if (Js != 59) return fail(RTG_ERR_INVALID_ARGUMENT, "FULL_BODY_ROT expects the 59-joint VTRDYN_FULL zero pose, got %d", Js);
+        // full_body_retargeter.py:64,72,85,93,152 (gripper uses LOCAL translations, joint 24)
+        C.v0_lsh = v3(zl, 13); C.v0_lel = v3(zl, 14); C.v0_rsh = v3(zl, 38); C.v0_rel = v3(zl, 39);
+        const int gi[5] = {18, 22, 26, 30, 33};
+        for (int t = 0; t < 5; ++t) C.grip_d[t] = zl[3 * gi[t]] - zl[3 * 24];
+        break;
+    }
+    case RTG_SOLVER_BODY_ROT:
+        if (Js != 21) return fail(RTG_ERR_INVALID_ARGUMENT, "BODY_ROT expects the 21-joint VTRDYN zero pose, got %d", Js);
+        if (!parents) return fail(RTG_ERR_INVALID_ARGUMENT, "BODY_ROT needs the source parent indices");
+        C.par[0] = parents[18]; C.par[1] = parents[14]; C.par[2] = parents[19]; C.par[3] = parents[15];
+        for (int i = 0; i < 4; ++i)
+            if (C.par[i] < 0 || C.par[i] >= 21) return fail(RTG_ERR_INVALID_ARGUMENT, "BODY_ROT: bad parent index");
+        break;
+    default:
+        return fail(RTG_ERR_INVALID_ARGUMENT, "rtg_solver_create: unknown solver kind %d", kind);
+    }
+    SolverConsts *d = nullptr;
+    RTG_TRY(hipMalloc(&d, sizeof(SolverConsts)), "hipMalloc(solver consts)");
+    int rc = hip_check(hipMemcpy(d, &C, sizeof C, hipMemcpyHostToDevice), "hipMemcpy(consts)");
+    if (rc == RTG_OK && kind != RTG_SOLVER_BODY_ROT) rc = hip_check(launch_solver_prep(d, nullptr), "k_solver_prep");
+    if (rc == RTG_OK) rc = hip_check(hipMemcpy(&C, d, sizeof C, hipMemcpyDeviceToHost), "hipMemcpy(consts)");
+    (void)hipFree(d);
+    if (rc != RTG_OK) return rc;
+    rtg_solver_s *s = new (std::nothrow) rtg_solver_s();
+    if (!s) return fail(RTG_ERR_OUT_OF_MEMORY, "rtg_solver_create: host allocation failed");
+    s->kind = kind;
+    s->precise = precise_gripper ? 1 : 0;
+    s->consts = C;
+    *out = s;
+    return RTG_OK;
+}
+
+int rtg_solver_destroy(rtg_solver_t s)
+{
+    delete s;
+    return RTG_OK;
+}
+
+int rtg_retarget_f32(rtg_solver_t s, const float *in0, const float *in1, const float *in2, const float *in3,
+                     int64_t B, float *dof, float *local_rot, float *body_rot, rtg_stream_t stream)
+{
+    if (!s) return fail(RTG_ERR_INVALID_ARGUMENT, "rtg_retarget_f32: NULL solver");
+    if (B < 0) return fail(RTG_ERR_INVALID_ARGUMENT, "rtg_retarget_f32: negative batch");
+    if (B == 0) return RTG_OK;
+    if (B > (int64_t)0x7fffffff * 256) return fail(RTG_ERR_INVALID_ARGUMENT, "rtg_retarget_f32: batch too large");
+    if (!dof) return fail(RTG_ERR_INVALID_ARGUMENT, "rtg_retarget_f32: NULL dof");
+    const int need = s->kind == RTG_SOLVER_FULL_BODY_ROT ? 4 : (s->kind == RTG_SOLVER_FULL_BODY_POS ? 3 : 1);
+    const float *ins[4] = {in0, in1, in2, in3};
+    for (int i = 0; i < 4; ++i) {
+        if (i < need && !ins[i]) return fail(RTG_ERR_INVALID_ARGUMENT, "rtg_retarget_f32: input %d is NULL", i);
+        if (i >= need && ins[i]) return fail(RTG_ERR_INVALID_ARGUMENT, "rtg_retarget_f32: input %d must be NULL", i);
+    }
+    if (body_rot && s->kind != RTG_SOLVER_FULL_BODY_POS)
+        return fail(RTG_ERR_INVALID_ARGUMENT, "rtg_retarget_f32: body_rot is only produced by FULL_BODY_POS");
+    RTG_TRY(launch_retarget(s->kind, s->precise, s->consts, in0, in1, in2, in3, B, dof, local_rot, body_rot,
+                            as_stream(stream)),
+            "k_retarget");
+    return RTG_OK;
+}
+
+// ---------------------------------------------------------------- primitives
+int rtg_quat_op_f32(int op, const float *a, const float *b, const float *c, int64_t n, float *out,
+                    rtg_stream_t stream)
+{
+    if (op < RTG_OP_QUAT_MUL || op > RTG_OP_ELBOW_PY) return fail(RTG_ERR_INVALID_ARGUMENT, "rtg_quat_op_f32: bad op %d", op);
+    if (n < 0) return fail(RTG_ERR_INVALID_ARGUMENT, "rtg_quat_op_f32: negative n");
+    if (n == 0) return RTG_OK;
+    const bool needs_b = !(op == RTG_OP_QUAT_NORMALIZE || op == RTG_OP_QUAT_INVERSE || op == RTG_OP_QUAT_FROM_ROTMAT ||
+                           op == RTG_OP_QUAT_TO_EXP_MAP || op == RTG_OP_QUAT_TO_DOF_POS);
+    const bool needs_c = op == RTG_OP_RADIANS_BETWEEN || op == RTG_OP_SHOULDER_PR || op == RTG_OP_ELBOW_PY;
+    if (!a || !out || (needs_b && !b) || (needs_c && !c))
+        return fail(RTG_ERR_INVALID_ARGUMENT, "rtg_quat_op_f32: NULL operand for op %d", op);
+    RTG_TRY(launch_quat_op(op, a, b, c, n, out, as_stream(stream)), "k_quat_op");
+    return RTG_OK;
+}
+
+int rtg_cal_joint_quat_f32(const float *Z, const float *M, int32_t npts, int64_t n, float *out, rtg_stream_t stream)
+{
+    if (npts < 1 || npts > 8) return fail(RTG_ERR_UNSUPPORTED, "rtg_cal_joint_quat_f32: npts=%d (1..8)", npts);
+    if (n < 0) return fail(RTG_ERR_INVALID_ARGUMENT, "rtg_cal_joint_quat_f32: negative n");
+    if (n == 0) return RTG_OK;
+    if (!Z || !M || !out) return fail(RTG_ERR_INVALID_ARGUMENT, "rtg_cal_joint_quat_f32: NULL buffer");
+    RTG_TRY(launch_cal_joint_quat(Z, M, npts, n, out, as_stream(stream)), "k_cal_joint_quat");
+    return RTG_OK;
+}
+
+int rtg_quat_in_xyz_axis_f32(const float *q, const char *seq, int64_t n, float *out, rtg_stream_t stream)
+{
+    if (!seq || std::strlen(seq) != 3) return fail(RTG_ERR_INVALID_ARGUMENT, "rtg_quat_in_xyz_axis_f32: seq must have 3 axes");
+    int ax[3], lower[3];
+    for (int i = 0; i < 3; ++i)
+        if (!axis_of(seq[i], &ax[i], &lower[i]))
+            return fail(RTG_ERR_INVALID_ARGUMENT, "rtg_quat_in_xyz_axis_f32: bad axis '%c'", seq[i]);
+    if (lower[0] != lower[1] || lower[1] != lower[2])
+        return fail(RTG_ERR_INVALID_ARGUMENT, "rtg_quat_in_xyz_axis_f32: mixed intrinsic/extrinsic seq '%s'", seq);
+    if (ax[0] == ax[1] || ax[1] == ax[2])
+        return fail(RTG_ERR_INVALID_ARGUMENT, "rtg_quat_in_xyz_axis_f32: consecutive axes must differ ('%s')", seq);
+    if (n < 0) return fail(RTG_ERR_INVALID_ARGUMENT, "rtg_quat_in_xyz_axis_f32: negative n");
+    if (n == 0) return RTG_OK;
+    if (!q || !out) return fail(RTG_ERR_INVALID_ARGUMENT, "rtg_quat_in_xyz_axis_f32: NULL buffer");
+    RTG_TRY(launch_quat_in_xyz_axis(q, ax[0], ax[1], ax[2], lower[0], n, out, as_stream(stream)), "k_quat_in_xyz_axis");
+    return RTG_OK;
+}
+
+// ---------------------------------------------------------------- synthetic input
+int rtg_synth_full_body_f32(rtg_topology_t t, uint64_t seed, int64_t off, int64_t B, float *body, float *lh,
+                            float *rh, float *body_rot, rtg_stream_t stream)
+{
+    if (!t || t->J != 59) return fail(RTG_ERR_INVALID_ARGUMENT, "rtg_synth_full_body_f32: needs the 59-joint VTRDYN_FULL topology");
+    if (B < 0 || off < 0) return fail(RTG_ERR_INVALID_ARGUMENT, "rtg_synth_full_body_f32: negative batch/offset");
+    if (B == 0) return RTG_OK;
+    if (!body || !lh || !rh) return fail(RTG_ERR_INVALID_ARGUMENT, "rtg_synth_full_body_f32: NULL buffer");
+    RTG_TRY(launch_synth_full_body(t->view(), seed, off, B, body, lh, rh, body_rot, as_stream(stream)), "k_synth_full_body");
+    return RTG_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,57 @@
+// rtg_kernels.cuh -- types shared by the kernels and the C-ABI layer.
+#pragma once
+#include "rtg_math.cuh"
+#include "rtg.h"
+
+namespace rtg {
+
+// Device view of a topology (all pointers device memory, uniform per launch).
+struct TopoView {
+    const int32_t *parents;   // (J)   parents[j] < j, root -1
+    const V *local_t;         // (J)   zero-pose local translation
+    const Q *tree_quat;       // (J)   SkeletonTree pre-rotation
+    int32_t J;
+};
+
+// Per-solver constants, passed by value (kernel argument -> SGPRs).
+struct SolverConsts {
+    V Zt[3];          // torso Kabsch zero vectors
+    V Zl[5], Zr[5];   // wrist Kabsch zero vectors
+    V v0_lsh, v0_lel, v0_rsh, v0_rel;
+    ArmZero lsh, lel, rsh, rel;   // theta0 / phi0, filled by k_solver_prep
+    float grip_d[5];  // zero-pose x distances of the 5 finger tips to the wrist
+    float orig;       // their mean (gripper denominator), filled by k_solver_prep
+    int32_t par[4];   // BODY_ROT: parents of joints 18, 14, 19, 15
+};
+
+struct FkSeg {
+    TopoView T;
+    const float *local_rot;
+    const float *root_t;
+    float *g_rot;
+    float *g_pos;
+    int64_t B;
+};
+struct FkMultiArgs {
+    FkSeg seg[RTG_MAX_SEGMENTS];
+    int64_t block_start[RTG_MAX_SEGMENTS];
+    int32_t n;
+};
+
+hipError_t launch_solver_prep(SolverConsts *dev_consts, hipStream_t s);
+hipError_t launch_retarget(int kind, int precise, const SolverConsts &C, const float *in0, const float *in1,
+                           const float *in2, const float *in3, int64_t B, float *dof, float *local_rot,
+                           float *body_rot, hipStream_t s);
+hipError_t launch_fk(const TopoView &T, bool state, const float *lr, const float *rt, int64_t B, float *gr, float *gp,
+                     hipStream_t s);
+hipError_t launch_local_rotation(const TopoView &T, bool state, const float *g, int64_t B, float *l, hipStream_t s);
+hipError_t launch_fk_multi(FkMultiArgs &A, hipStream_t s);
+hipError_t launch_quat_op(int op, const float *a, const float *b, const float *c, int64_t n, float *out,
+                          hipStream_t s);
+hipError_t launch_cal_joint_quat(const float *Z, const float *M, int npts, int64_t n, float *out, hipStream_t s);
+hipError_t launch_quat_in_xyz_axis(const float *q, int s0, int s1, int s2, int extrinsic, int64_t n, float *out,
+                                   hipStream_t s);
+hipError_t launch_synth_full_body(const TopoView &T, uint64_t seed, int64_t off, int64_t B, float *body, float *lh,
+                                  float *rh, float *body_rot, hipStream_t s);
+
+}  // namespace rtg

@@ -1,0 +1,645 @@
+// rtg_kernels.hip -- CDNA4 (gfx950) kernels of the retargeting hot path.
+//
+// Work decomposition: one mocap frame per lane.  Frames are independent
+// (SURVEY.md §0), every solver step is a short dependent chain of scalar-sized
+// math, and a frame's working set (<= 32 input points) fits in VGPRs, so a
+// lane solves its frame end-to-end with no cross-lane traffic.  Zero-pose-only
+// terms are evaluated once per solver (k_solver_prep) and arrive as a by-value
+// kernel argument (SGPR-resident).  The 30-float DOF row of each frame is
+// staged through LDS so the block stores one contiguous, dwordx4-coalesced
+// tile instead of 64 lanes writing 120-byte-strided rows.
+#include "rtg_kernels.cuh"
+
+namespace rtg {
+
+// ----------------------------------------------------------------------------
+// loads / stores
+// ----------------------------------------------------------------------------
+RTG_DEV V ld3(const float *__restrict__ p) { return V{p[0], p[1], p[2]}; }
+RTG_DEV Q ld4(const float *__restrict__ p)
+{
+    const float4 v = *reinterpret_cast<const float4 *>(p);
+    return Q{v.x, v.y, v.z, v.w};
+}
+RTG_DEV void st4(float *__restrict__ p, Q q) { *reinterpret_cast<float4 *>(p) = make_float4(q.x, q.y, q.z, q.w); }
+RTG_DEV void st3(float *__restrict__ p, V v) { p[0] = v.x; p[1] = v.y; p[2] = v.z; }
+
+// ----------------------------------------------------------------------------
+// solver constants prep (1 thread): theta0 / phi0 of the four arm maps and the
+// gripper denominator, computed with exactly the per-frame device math.
+// ----------------------------------------------------------------------------
+__global__ void k_solver_prep(SolverConsts *c)
+{
+    if (threadIdx.x != 0 || blockIdx.x != 0) return;
+    c->lsh = shoulder_zero(c->v0_lsh);
+    c->rsh = shoulder_zero(c->v0_rsh);
+    c->lel = elbow_zero(c->v0_lel);
+    c->rel = elbow_zero(c->v0_rel);
+    c->orig = mean5(c->grip_d[0], c->grip_d[1], c->grip_d[2], c->grip_d[3], c->grip_d[4]);
+}
+
+// ----------------------------------------------------------------------------
+// solver bodies: each produces the 14 non-identity links (12..18, 21..27) and
+// the four gripper DOFs; everything else is the identity / 0 by construction.
+// ----------------------------------------------------------------------------
+struct FrameOut {
+    Q l[14];          // links 12..18 then 21..27
+    float grip[4];    // dof 18, 19, 27, 28
+    bool has_grip;
+    Q kab[3];         // FULL_BODY_POS: body_global_rotation rows 10, 14, 39
+};
+
+// VtrdynFullBodyPosRetargeter.retarget  full_body_pos_retargeter.py:25-217
+template <bool PRECISE>
+RTG_DEV void solve_full_body_pos(const SolverConsts &C, const float *__restrict__ b, const float *__restrict__ L,
+                                 const float *__restrict__ R, FrameOut &o)
+{
+    // _retarget_arm_from_global_translation :61-118
+    const V b10 = ld3(b + 30);
+    const V Mt[3] = {vsub(ld3(b + 51), b10), vsub(ld3(b + 39), b10), vsub(ld3(b + 33), b10)};
+    const Q R10 = cal_joint_quat<3>(C.Zt, Mt);
+    const V b14 = ld3(b + 42), b15 = ld3(b + 45), b16 = ld3(b + 48);
+    const V b18 = ld3(b + 54), b19 = ld3(b + 57), b20 = ld3(b + 60);
+    Q p, r, y, e;
+    shoulder_pr(vsub(b19, b18), C.lsh, R10, p, r);
+    elbow_py(vsub(b20, b19), C.lel, qmul(qmul(R10, p), r), y, e);
+    o.l[0] = p; o.l[1] = r; o.l[2] = y; o.l[3] = e;
+    shoulder_pr(vsub(b15, b14), C.rsh, R10, p, r);
+    elbow_py(vsub(b16, b15), C.rel, qmul(qmul(R10, p), r), y, e);
+    o.l[7] = p; o.l[8] = r; o.l[9] = y; o.l[10] = e;
+    // _retarget_wrist_from_global_translation :120-175
+    Q eul[3];
+    {
+        const Q par = qmul_norm(R10, qmul(qmul(qmul(o.l[0], o.l[1]), o.l[2]), o.l[3]));
+        const V l0 = ld3(L);
+        const V Ml[5] = {vsub(ld3(L + 6), l0), vsub(ld3(L + 18), l0), vsub(ld3(L + 30), l0), vsub(ld3(L + 42), l0),
+                         vsub(ld3(L + 51), l0)};
+        o.kab[1] = cal_joint_quat<5>(C.Zl, Ml);
+        quat_in_xyz_axis(qmul_norm(qconj(par), o.kab[1]), 0, 1, 2, false, eul);
+        o.l[4] = eul[0]; o.l[5] = eul[1]; o.l[6] = eul[2];
+    }
+    {
+        const Q par = qmul_norm(R10, qmul(qmul(qmul(o.l[7], o.l[8]), o.l[9]), o.l[10]));
+        const V r0 = ld3(R);
+        const V Mr[5] = {vsub(ld3(R + 6), r0), vsub(ld3(R + 18), r0), vsub(ld3(R + 30), r0), vsub(ld3(R + 42), r0),
+                         vsub(ld3(R + 51), r0)};
+        o.kab[2] = cal_joint_quat<5>(C.Zr, Mr);
+        quat_in_xyz_axis(qmul_norm(qconj(par), o.kab[2]), 0, 1, 2, false, eul);
+        o.l[11] = eul[0]; o.l[12] = eul[1]; o.l[13] = eul[2];
+    }
+    o.kab[0] = R10;
+    // _retarget_gripper :177-217 (hand points rotated into the wrist frame)
+    const Q cl = qconj(o.kab[1]), cr = qconj(o.kab[2]);
+    const float hl0 = qrotate(cl, ld3(L)).x, hr0 = qrotate(cr, ld3(R)).x;
+    const float la = mean5(qrotate(cl, ld3(L + 12)).x - hl0, qrotate(cl, ld3(L + 24)).x - hl0,
+                           qrotate(cl, ld3(L + 36)).x - hl0, qrotate(cl, ld3(L + 48)).x - hl0,
+                           qrotate(cl, ld3(L + 57)).x - hl0);
+    const float ra = mean5(qrotate(cr, ld3(R + 12)).x - hr0, qrotate(cr, ld3(R + 24)).x - hr0,
+                           qrotate(cr, ld3(R + 36)).x - hr0, qrotate(cr, ld3(R + 48)).x - hr0,
+                           qrotate(cr, ld3(R + 57)).x - hr0);
+    if (PRECISE) {
+        const float ls = clamp_lohi(la / C.orig - 0.5f, 0.0f, 0.5f) / 0.5f;
+        const float rs = clamp_lohi(ra / C.orig - 0.5f, 0.0f, 0.5f) / 0.5f;
+        o.grip[0] = ls * 0.044f; o.grip[1] = ls * -0.044f;
+        o.grip[2] = rs * 0.044f; o.grip[3] = rs * -0.044f;
+    } else {
+        const bool lc = la / C.orig < 0.7f, rc = ra / C.orig < 0.7f;
+        o.grip[0] = lc ? 0.0f : 0.044f; o.grip[1] = lc ? 0.0f : -0.044f;
+        o.grip[2] = rc ? 0.0f : 0.044f; o.grip[3] = rc ? 0.0f : -0.044f;
+    }
+    o.has_grip = true;
+}
+
+// HuUpperBodyFromMocapRetarget.retarget_from_global_translation  retarget_solver.py:40-99
+RTG_DEV void solve_upper_body(const SolverConsts &C, const float *__restrict__ x, FrameOut &o)
+{
+    auto pt = [&](int j) {   // coord_transform(dir=[-1,-1,1]) :41
+        const V v = ld3(x + 3 * j);
+        return V{v.x * -1.0f, v.y * -1.0f, v.z * 1.0f};
+    };
+    const V s10 = pt(10);
+    const V Mt[3] = {vsub(pt(17), s10), vsub(pt(13), s10), vsub(pt(11), s10)};
+    const Q R10 = cal_joint_quat<3>(C.Zt, Mt);
+    const V s14 = pt(14), s15 = pt(15), s16 = pt(16), s18 = pt(18), s19 = pt(19), s20 = pt(20);
+    Q pl, rl, pr, rr, y, e;
+    shoulder_pr(vsub(s19, s18), C.lsh, R10, pl, rl);
+    shoulder_pr(vsub(s15, s14), C.rsh, R10, pr, rr);
+    o.l[0] = pl; o.l[1] = rl; o.l[7] = pr; o.l[8] = rr;
+    elbow_py(vsub(s20, s19), C.lel, qmul(qmul(R10, pl), rl), y, e);
+    o.l[2] = y; o.l[3] = e;
+    elbow_py(vsub(s16, s15), C.rel, qmul(qmul(R10, pr), rr), y, e);
+    o.l[9] = y; o.l[10] = e;
+    o.l[4] = o.l[5] = o.l[6] = o.l[11] = o.l[12] = o.l[13] = qident();
+    o.has_grip = false;
+    o.kab[0] = R10;
+}
+
+// VtrdynFullBodyRetargeter.retarget  full_body_retargeter.py:19-177
+RTG_DEV void solve_full_body_rot(const SolverConsts &C, const float *__restrict__ q, const float *__restrict__ b,
+                                 const float *__restrict__ L, const float *__restrict__ R, FrameOut &o)
+{
+    const Q parL = ld4(q + 17 * 4), parR = ld4(q + 13 * 4);
+    const V b14 = ld3(b + 42), b15 = ld3(b + 45), b16 = ld3(b + 48);
+    const V b18 = ld3(b + 54), b19 = ld3(b + 57), b20 = ld3(b + 60);
+    Q p, r, y, e;
+    shoulder_pr(vsub(b19, b18), C.lsh, parL, p, r);
+    elbow_py(vsub(b20, b19), C.lel, qmul(qmul(parL, p), r), y, e);
+    o.l[0] = p; o.l[1] = r; o.l[2] = y; o.l[3] = e;
+    shoulder_pr(vsub(b15, b14), C.rsh, parR, p, r);
+    elbow_py(vsub(b16, b15), C.rel, qmul(qmul(parR, p), r), y, e);
+    o.l[7] = p; o.l[8] = r; o.l[9] = y; o.l[10] = e;
+    const Q wl = ld4(q + 20 * 4), wr = ld4(q + 16 * 4);
+    Q eul[3];
+    const Q pl = qmul_norm(parL, qmul(qmul(qmul(o.l[0], o.l[1]), o.l[2]), o.l[3]));
+    quat_in_xyz_axis(qmul_norm(qconj(pl), wl), 0, 1, 2, false, eul);
+    o.l[4] = eul[0]; o.l[5] = eul[1]; o.l[6] = eul[2];
+    const Q pr = qmul_norm(parR, qmul(qmul(qmul(o.l[7], o.l[8]), o.l[9]), o.l[10]));
+    quat_in_xyz_axis(qmul_norm(qconj(pr), wr), 0, 1, 2, false, eul);
+    o.l[11] = eul[0]; o.l[12] = eul[1]; o.l[13] = eul[2];
+    // _retarget_gripper :145-177 -- rotates by the wrist quaternion itself (not its inverse)
+    const float hl0 = qrotate(wl, ld3(L)).x, hr0 = qrotate(wr, ld3(R)).x;
+    const float la = mean5(qrotate(wl, ld3(L + 9)).x - hl0, qrotate(wl, ld3(L + 21)).x - hl0,
+                           qrotate(wl, ld3(L + 33)).x - hl0, qrotate(wl, ld3(L + 45)).x - hl0,
+                           qrotate(wl, ld3(L + 57)).x - hl0);
+    const float ra = mean5(qrotate(wr, ld3(R + 9)).x - hr0, qrotate(wr, ld3(R + 21)).x - hr0,
+                           qrotate(wr, ld3(R + 33)).x - hr0, qrotate(wr, ld3(R + 45)).x - hr0,
+                           qrotate(wr, ld3(R + 57)).x - hr0);
+    const bool lc = la / C.orig < 0.7f, rc = ra / C.orig < 0.7f;
+    o.grip[0] = lc ? 0.0f : 0.044f; o.grip[1] = lc ? 0.0f : -0.044f;
+    o.grip[2] = rc ? 0.0f : 0.044f; o.grip[3] = rc ? 0.0f : -0.044f;
+    o.has_grip = true;
+}
+
+// Mocap2HuBodyRetargeter.retarget_from_pose  body_retargeter.py:34-81
+RTG_DEV void solve_body_rot(const SolverConsts &C, const float *__restrict__ g, FrameOut &o)
+{
+    // cal_local_rotation (kinematics.py:41-63) for the four joints used
+    auto local = [&](int j, int p) { return qmul_norm(qconj(ld4(g + 4 * p)), ld4(g + 4 * j)); };
+    const Q l18 = local(18, C.par[0]), l14 = local(14, C.par[1]);
+    const Q l19 = local(19, C.par[2]), l15 = local(15, C.par[3]);
+    Q sl[3], sr[3], el[3], er[3];
+    quat_in_xyz_axis(l18, 1, 0, 2, false, sl);   // 'YXZ'
+    quat_in_xyz_axis(l14, 1, 0, 2, false, sr);
+    quat_in_xyz_axis(l19, 2, 1, 0, false, el);   // 'ZYX'
+    quat_in_xyz_axis(l15, 2, 1, 0, false, er);
+    o.l[0] = sl[0]; o.l[1] = sl[1]; o.l[2] = qmul_norm(el[0], sl[2]);
+    o.l[3] = el[1]; o.l[4] = el[2];
+    o.l[7] = sr[0]; o.l[8] = sr[1]; o.l[9] = qmul_norm(er[0], sr[2]);
+    o.l[10] = er[1]; o.l[11] = er[2];
+    o.l[5] = o.l[6] = o.l[12] = o.l[13] = qident();
+    o.has_grip = false;
+}
+
+// ----------------------------------------------------------------------------
+// solver kernel: body + epilogue (quat_to_dof_pos, outputs)
+// ----------------------------------------------------------------------------
+constexpr int kSolverBlock = 256;
+constexpr int kDofStride = 31;   // LDS row pitch (dwords): odd -> conflict-free ds_write_b32
+
+template <int KIND, bool PRECISE>
+__global__ __launch_bounds__(kSolverBlock) void k_retarget(SolverConsts C, const float *__restrict__ in0,
+                                                           const float *__restrict__ in1,
+                                                           const float *__restrict__ in2,
+                                                           const float *__restrict__ in3, int64_t B,
+                                                           float *__restrict__ dof, float *__restrict__ local_rot,
+                                                           float *__restrict__ body_rot)
+{
+    __shared__ float sdof[kSolverBlock * kDofStride];
+    const int64_t f0 = (int64_t)blockIdx.x * kSolverBlock;
+    const int64_t f = f0 + threadIdx.x;
+    float *row = sdof + threadIdx.x * kDofStride;
+    if (f < B) {
+        FrameOut o;
+        if (KIND == RTG_SOLVER_FULL_BODY_POS)
+            solve_full_body_pos<PRECISE>(C, in0 + f * 63, in1 + f * 60, in2 + f * 60, o);
+        else if (KIND == RTG_SOLVER_UPPER_BODY)
+            solve_upper_body(C, in0 + f * 63, o);
+        else if (KIND == RTG_SOLVER_FULL_BODY_ROT)
+            solve_full_body_rot(C, in0 + f * 84, in1 + f * 63, in2 + f * 60, in3 + f * 60, o);
+        else
+            solve_body_rot(C, in0 + f * 84, o);
+        // quat_to_dof_pos (transform3d.py:176-183): dof k <-> link k+1, component Hu_DOF_AXIS[k]
+#pragma unroll
+        for (int k = 0; k < 11; ++k) row[k] = 0.0f;
+#pragma unroll
+        for (int t = 0; t < 7; ++t) row[11 + t] = qexp_component(o.l[t], hu_dof_axis(11 + t));
+#pragma unroll
+        for (int t = 0; t < 7; ++t) row[20 + t] = qexp_component(o.l[7 + t], hu_dof_axis(20 + t));
+        row[18] = o.has_grip ? o.grip[0] : 0.0f;
+        row[19] = o.has_grip ? o.grip[1] : 0.0f;
+        row[27] = o.has_grip ? o.grip[2] : 0.0f;
+        row[28] = o.has_grip ? o.grip[3] : 0.0f;
+        row[29] = 0.0f;
+        if (local_rot) {
+            float *lr = local_rot + f * 124;
+#pragma unroll
+            for (int j = 0; j < 31; ++j) {
+                Q q = qident();
+                if (j >= 12 && j <= 18) q = o.l[j - 12];
+                if (j >= 21 && j <= 27) q = o.l[j - 14];
+                st4(lr + 4 * j, q);
+            }
+        }
+        if (KIND == RTG_SOLVER_FULL_BODY_POS && body_rot) {
+            float *br = body_rot + f * 236;
+            for (int j = 0; j < 59; ++j) {
+                Q q = qident();
+                if (j == 10) q = o.kab[0];
+                if (j == 14) q = o.kab[1];
+                if (j == 39) q = o.kab[2];
+                st4(br + 4 * j, q);
+            }
+        }
+    }
+    __syncthreads();
+    // coalesced store of the block's contiguous DOF tile: rows [f0, min(B, f0+256)) x 30.
+    // f0*120 B is 16-byte aligned, so the tile goes out as dwordx4 (full-line writes).
+    const int64_t nrows = (B - f0) < kSolverBlock ? (B - f0) : kSolverBlock;
+    const int nvals = (int)nrows * 30;
+    float *dst = dof + f0 * 30;
+    auto lds_at = [&](int i) {
+        const int r = i / 30;
+        return sdof[r * kDofStride + (i - r * 30)];
+    };
+    const int nvec = nvals >> 2;
+    for (int v = threadIdx.x; v < nvec; v += kSolverBlock) {
+        const int i = v << 2;
+        *reinterpret_cast<float4 *>(dst + i) = make_float4(lds_at(i), lds_at(i + 1), lds_at(i + 2), lds_at(i + 3));
+    }
+    for (int i = (nvec << 2) + threadIdx.x; i < nvals; i += kSolverBlock) dst[i] = lds_at(i);
+}
+
+// ----------------------------------------------------------------------------
+// forward kinematics -- one frame per lane, joints in topological (index) order.
+// The parent's global rotation / position is reused from registers when the
+// parent is the previous joint (chains), else re-read from the output rows this
+// lane has just written (branch points; L2-resident).  Topology is uniform
+// across the grid, so the loop body and all topology loads are scalar.
+// ----------------------------------------------------------------------------
+template <bool STATE>
+RTG_DEV void fk_frame(const TopoView &T, const float *__restrict__ lr, const float *__restrict__ rt,
+                      float *__restrict__ gr, float *__restrict__ gp)
+{
+    Q g = ld4(lr);            // root: global = local (not normalised) kinematics.py:27-29
+    V t = ld3(rt);
+    st4(gr, g);
+    st3(gp, t);
+    for (int j = 1; j < T.J; ++j) {
+        const int p = T.parents[j];
+        if (p != j - 1) {
+            g = ld4(gr + 4 * p);
+            t = ld3(gp + 3 * p);
+        }
+        Q lq = ld4(lr + 4 * j);
+        if (STATE) lq = qmul_norm(T.tree_quat[j], lq);   // skeleton3d.py:412-418
+        const V zl = T.local_t[j];
+        const V rot = qrotate(g, zl);
+        const Q ng = qmul_norm(g, lq);
+        const V nt = V{rot.x + t.x, rot.y + t.y, rot.z + t.z};
+        st4(gr + 4 * j, ng);
+        st3(gp + 3 * j, nt);
+        g = ng;
+        t = nt;
+    }
+}
+
+template <bool STATE>
+__global__ __launch_bounds__(256) void k_fk(TopoView T, const float *__restrict__ local_rot,
+                                            const float *__restrict__ root_t, int64_t B, float *__restrict__ g_rot,
+                                            float *__restrict__ g_pos)
+{
+    const int64_t f = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (f >= B) return;
+    fk_frame<STATE>(T, local_rot + f * T.J * 4, root_t + f * 3, g_rot + f * T.J * 4, g_pos + f * T.J * 3);
+}
+
+template <bool STATE>
+__global__ __launch_bounds__(256) void k_local_rotation(TopoView T, const float *__restrict__ g_rot, int64_t B,
+                                                        float *__restrict__ local_rot)
+{
+    const int64_t f = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (f >= B) return;
+    const float *g = g_rot + f * T.J * 4;
+    float *l = local_rot + f * T.J * 4;
+    st4(l, ld4(g));
+    for (int j = 1; j < T.J; ++j) {
+        const int p = T.parents[j];
+        Q q = qmul_norm(qconj(ld4(g + 4 * p)), ld4(g + 4 * j));
+        if (STATE) q = qmul_norm(qnormalize(qconj(T.tree_quat[j])), q);   // skeleton3d.py:477-481
+        st4(l + 4 * j, q);
+    }
+}
+
+__global__ __launch_bounds__(256) void k_fk_multi(FkMultiArgs A)
+{
+    int s = 0;
+#pragma unroll
+    for (int i = 1; i < RTG_MAX_SEGMENTS; ++i)
+        if (i < A.n && (int64_t)blockIdx.x >= A.block_start[i]) s = i;
+    const FkSeg &S = A.seg[s];
+    const int64_t f = ((int64_t)blockIdx.x - A.block_start[s]) * blockDim.x + threadIdx.x;
+    if (f >= S.B) return;
+    fk_frame<false>(S.T, S.local_rot + f * S.T.J * 4, S.root_t + f * 3, S.g_rot + f * S.T.J * 4,
+                    S.g_pos + f * S.T.J * 3);
+}
+
+// ----------------------------------------------------------------------------
+// elementwise primitives
+// ----------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void k_quat_op(int op, const float *__restrict__ a, const float *__restrict__ b,
+                                                 const float *__restrict__ c, int64_t n, float *__restrict__ out)
+{
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    switch (op) {
+    case RTG_OP_QUAT_MUL: st4(out + 4 * i, qmul(ld4(a + 4 * i), ld4(b + 4 * i))); break;
+    case RTG_OP_QUAT_MUL_NORM: st4(out + 4 * i, qmul_norm(ld4(a + 4 * i), ld4(b + 4 * i))); break;
+    case RTG_OP_QUAT_NORMALIZE: st4(out + 4 * i, qnormalize(ld4(a + 4 * i))); break;
+    case RTG_OP_QUAT_ROTATE: st3(out + 3 * i, qrotate(ld4(a + 4 * i), ld3(b + 3 * i))); break;
+    case RTG_OP_QUAT_INVERSE: st4(out + 4 * i, qconj(ld4(a + 4 * i))); break;
+    case RTG_OP_QUAT_FROM_ANGLE_AXIS: st4(out + 4 * i, qfrom_angle_axis(a[i], ld3(b + 3 * i))); break;
+    case RTG_OP_QUAT_FROM_ROTMAT: {
+        float m[9];
+#pragma unroll
+        for (int k = 0; k < 9; ++k) m[k] = a[9 * i + k];
+        st4(out + 4 * i, qfrom_rotmat(m));
+        break;
+    }
+    case RTG_OP_QUAT_TO_EXP_MAP: st3(out + 3 * i, qexp_map(ld4(a + 4 * i))); break;
+    case RTG_OP_RADIANS_BETWEEN: out[i] = radians_between(ld3(a + 3 * i), ld3(b + 3 * i), ld3(c + 3 * i)); break;
+    case RTG_OP_PROJ_IN_PLANE: st3(out + 3 * i, proj_in_plane(ld3(a + 3 * i), ld3(b + 3 * i))); break;
+    case RTG_OP_QUAT_TO_DOF_POS: {
+        const float *q = a + i * 124 + 4;   // local_rot[1:]
+#pragma unroll
+        for (int k = 0; k < 30; ++k) out[i * 30 + k] = qexp_component(ld4(q + 4 * k), hu_dof_axis(k));
+        break;
+    }
+    case RTG_OP_SHOULDER_PR: {
+        Q p, r;
+        const V v0 = ld3(b + 3 * i);
+        shoulder_pr(ld3(a + 3 * i), shoulder_zero(v0), ld4(c + 4 * i), p, r);
+        st4(out + 8 * i, p);
+        st4(out + 8 * i + 4, r);
+        break;
+    }
+    case RTG_OP_ELBOW_PY: {
+        Q y, e;
+        const V v0 = ld3(b + 3 * i);
+        elbow_py(ld3(a + 3 * i), elbow_zero(v0), ld4(c + 4 * i), y, e);
+        st4(out + 8 * i, y);
+        st4(out + 8 * i + 4, e);
+        break;
+    }
+    default: break;
+    }
+}
+
+template <int N>
+__global__ __launch_bounds__(256) void k_cal_joint_quat(const float *__restrict__ Z, const float *__restrict__ M,
+                                                        int64_t n, float *__restrict__ out)
+{
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    V z[N], m[N];
+#pragma unroll
+    for (int j = 0; j < N; ++j) {
+        z[j] = ld3(Z + (i * N + j) * 3);
+        m[j] = ld3(M + (i * N + j) * 3);
+    }
+    st4(out + 4 * i, cal_joint_quat<N>(z, m));
+}
+
+__global__ __launch_bounds__(256) void k_quat_in_xyz_axis(const float *__restrict__ q, int s0, int s1, int s2,
+                                                          int extrinsic, int64_t n, float *__restrict__ out)
+{
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    Q e[3];
+    quat_in_xyz_axis(ld4(q + 4 * i), s0, s1, s2, extrinsic != 0, e);
+#pragma unroll
+    for (int t = 0; t < 3; ++t) st4(out + (i * 3 + t) * 4, e[t]);
+}
+
+// ----------------------------------------------------------------------------
+// synthetic mocap on the device (bench / large-size tests)
+// counter-based hash RNG: frame f, draw k -> uniform in (0,1)
+// ----------------------------------------------------------------------------
+RTG_DEV uint64_t mix64(uint64_t z)
+{
+    z = (z ^ (z >> 30)) * 0xbf58476d1ce4e5b9ull;
+    z = (z ^ (z >> 27)) * 0x94d049bb133111ebull;
+    return z ^ (z >> 31);
+}
+RTG_DEV float urand(uint64_t seed, uint64_t f, uint32_t k)
+{
+    const uint64_t h = mix64(seed * 0x9e3779b97f4a7c15ull ^ mix64(f * 0x100000001b3ull + k));
+    return ((float)(h >> 40) + 0.5f) * (1.0f / 16777216.0f);
+}
+RTG_DEV float nrand(uint64_t seed, uint64_t f, uint32_t k)   // Box-Muller
+{
+    const float u1 = urand(seed, f, k), u2 = urand(seed, f, k + 0x8000u);
+    return sqrtf(-2.0f * logf(u1)) * cosf(6.28318530718f * u2);
+}
+RTG_DEV Q axis_angle_f(V ax, float ang)
+{
+    const float n = sqrtf(ax.x * ax.x + ax.y * ax.y + ax.z * ax.z);
+    const float s = sinf(0.5f * ang) / n, c = cosf(0.5f * ang);
+    return Q{ax.x * s, ax.y * s, ax.z * s, c};
+}
+RTG_DEV Q fast_qmul(Q a, Q b)
+{
+    return Q{a.w * b.x + a.x * b.w + a.y * b.z - a.z * b.y, a.w * b.y + a.y * b.w + a.z * b.x - a.x * b.z,
+             a.w * b.z + a.z * b.w + a.x * b.y - a.y * b.x, a.w * b.w - a.x * b.x - a.y * b.y - a.z * b.z};
+}
+RTG_DEV V fast_rot(Q q, V v)
+{
+    const V u{q.x, q.y, q.z};
+    const V t{2.0f * (u.y * v.z - u.z * v.y), 2.0f * (u.z * v.x - u.x * v.z), 2.0f * (u.x * v.y - u.y * v.x)};
+    return V{v.x + q.w * t.x + (u.y * t.z - u.z * t.y), v.y + q.w * t.y + (u.z * t.x - u.x * t.z),
+             v.z + q.w * t.z + (u.x * t.y - u.y * t.x)};
+}
+
+// joint group of VTRDYN_FULL (retarget/robot_config/VTRDYN_FULL.py:9-69): 0 root, 1 spine/arm, 2 leg, 3 finger
+RTG_DEV int full_group(int j)
+{
+    if (j == 0) return 0;
+    if (j <= 6) return 2;
+    if ((j >= 15 && j <= 33) || j >= 40) return 3;
+    return 1;
+}
+
+__constant__ int kFullToBody[21] = {0, 4, 5, 6, 1, 2, 3, 7, 8, 9, 10, 34, 35, 36, 37, 38, 39, 11, 12, 13, 14};
+
+__global__ __launch_bounds__(64) void k_synth_full_body(TopoView T, uint64_t seed, int64_t off, int64_t B,
+                                                        float *__restrict__ body, float *__restrict__ lh,
+                                                        float *__restrict__ rh, float *__restrict__ body_rot)
+{
+    __shared__ float sp[64][59 * 3 + 1];
+    __shared__ float sq[64][59 * 4];
+    const int64_t f = (int64_t)blockIdx.x * 64 + threadIdx.x;
+    if (f >= B) return;
+    const uint64_t fr = (uint64_t)(off + f);
+    float *P = sp[threadIdx.x];
+    float *G = sq[threadIdx.x];
+    for (int j = 0; j < T.J; ++j) {
+        const int grp = full_group(j);
+        const uint32_t k = 16u * (uint32_t)j;
+        Q lq;
+        if (grp == 0) {
+            lq = axis_angle_f(V{0.f, 0.f, 1.f}, (urand(seed, fr, k) * 2.0f - 1.0f) * 3.14159265f);
+        } else if (grp == 3) {
+            const bool yax = urand(seed, fr, k + 1) < 0.5f;
+            lq = axis_angle_f(yax ? V{0.f, 1.f, 0.f} : V{0.f, 0.f, 1.f}, 1.2f * urand(seed, fr, k + 2));
+        } else {
+            const V ax{nrand(seed, fr, k + 3), nrand(seed, fr, k + 4), nrand(seed, fr, k + 5)};
+            lq = axis_angle_f(ax, (grp == 1 ? 1.0f : 0.5f) * urand(seed, fr, k + 6));
+        }
+        Q g;
+        V t;
+        const int p = T.parents[j];
+        if (p < 0) {
+            g = lq;
+            t = V{0.1f * nrand(seed, fr, 2000), 0.1f * nrand(seed, fr, 2001), 0.1f * nrand(seed, fr, 2002)};
+        } else {
+            const Q gp{G[4 * p], G[4 * p + 1], G[4 * p + 2], G[4 * p + 3]};
+            const V r = fast_rot(gp, T.local_t[j]);
+            g = fast_qmul(gp, lq);
+            t = V{r.x + P[3 * p], r.y + P[3 * p + 1], r.z + P[3 * p + 2]};
+        }
+        G[4 * j] = g.x; G[4 * j + 1] = g.y; G[4 * j + 2] = g.z; G[4 * j + 3] = g.w;
+        P[3 * j] = t.x; P[3 * j + 1] = t.y; P[3 * j + 2] = t.z;
+    }
+    auto jit = [&](int j, int c) { return P[3 * j + c] + 0.002f * nrand(seed, fr, 3000u + 3u * j + c); };
+    for (int i = 0; i < 21; ++i) {
+        const int j = kFullToBody[i];
+#pragma unroll
+        for (int c = 0; c < 3; ++c) body[f * 63 + 3 * i + c] = jit(j, c);
+        if (body_rot) {
+            float n = sqrtf(G[4 * j] * G[4 * j] + G[4 * j + 1] * G[4 * j + 1] + G[4 * j + 2] * G[4 * j + 2] +
+                            G[4 * j + 3] * G[4 * j + 3]);
+            if (G[4 * j + 3] < 0.0f) n = -n;
+#pragma unroll
+            for (int c = 0; c < 4; ++c) body_rot[f * 84 + 4 * i + c] = G[4 * j + c] / n;
+        }
+    }
+    for (int i = 0; i < 20; ++i) {
+#pragma unroll
+        for (int c = 0; c < 3; ++c) {
+            lh[f * 60 + 3 * i + c] = jit(14 + i, c);
+            rh[f * 60 + 3 * i + c] = jit(39 + i, c);
+        }
+    }
+}
+
+// ----------------------------------------------------------------------------
+// launchers (host side, called from rtg_api.cpp)
+// ----------------------------------------------------------------------------
+static inline unsigned grid_for(int64_t n, int block) { return (unsigned)((n + block - 1) / block); }
+
+hipError_t launch_solver_prep(SolverConsts *dev_consts, hipStream_t s)
+{
+    hipLaunchKernelGGL(k_solver_prep, dim3(1), dim3(64), 0, s, dev_consts);
+    return hipGetLastError();
+}
+
+hipError_t launch_retarget(int kind, int precise, const SolverConsts &C, const float *in0, const float *in1,
+                           const float *in2, const float *in3, int64_t B, float *dof, float *local_rot,
+                           float *body_rot, hipStream_t s)
+{
+    const dim3 grid(grid_for(B, kSolverBlock)), block(kSolverBlock);
+    switch (kind) {
+    case RTG_SOLVER_FULL_BODY_POS:
+        if (precise)
+            hipLaunchKernelGGL((k_retarget<RTG_SOLVER_FULL_BODY_POS, true>), grid, block, 0, s, C, in0, in1, in2,
+                               in3, B, dof, local_rot, body_rot);
+        else
+            hipLaunchKernelGGL((k_retarget<RTG_SOLVER_FULL_BODY_POS, false>), grid, block, 0, s, C, in0, in1, in2,
+                               in3, B, dof, local_rot, body_rot);
+        break;
+    case RTG_SOLVER_UPPER_BODY:
+        hipLaunchKernelGGL((k_retarget<RTG_SOLVER_UPPER_BODY, false>), grid, block, 0, s, C, in0, in1, in2, in3, B,
+                           dof, local_rot, body_rot);
+        break;
+    case RTG_SOLVER_FULL_BODY_ROT:
+        hipLaunchKernelGGL((k_retarget<RTG_SOLVER_FULL_BODY_ROT, false>), grid, block, 0, s, C, in0, in1, in2, in3,
+                           B, dof, local_rot, body_rot);
+        break;
+    default:
+        hipLaunchKernelGGL((k_retarget<RTG_SOLVER_BODY_ROT, false>), grid, block, 0, s, C, in0, in1, in2, in3, B,
+                           dof, local_rot, body_rot);
+        break;
+    }
+    return hipGetLastError();
+}
+
+hipError_t launch_fk(const TopoView &T, bool state, const float *lr, const float *rt, int64_t B, float *gr, float *gp,
+                     hipStream_t s)
+{
+    if (state)
+        hipLaunchKernelGGL(k_fk<true>, dim3(grid_for(B, 256)), dim3(256), 0, s, T, lr, rt, B, gr, gp);
+    else
+        hipLaunchKernelGGL(k_fk<false>, dim3(grid_for(B, 256)), dim3(256), 0, s, T, lr, rt, B, gr, gp);
+    return hipGetLastError();
+}
+
+hipError_t launch_local_rotation(const TopoView &T, bool state, const float *g, int64_t B, float *l, hipStream_t s)
+{
+    if (state)
+        hipLaunchKernelGGL(k_local_rotation<true>, dim3(grid_for(B, 256)), dim3(256), 0, s, T, g, B, l);
+    else
+        hipLaunchKernelGGL(k_local_rotation<false>, dim3(grid_for(B, 256)), dim3(256), 0, s, T, g, B, l);
+    return hipGetLastError();
+}
+
+hipError_t launch_fk_multi(FkMultiArgs &A, hipStream_t s)
+{
+    int64_t blocks = 0;
+    for (int i = 0; i < A.n; ++i) {
+        A.block_start[i] = blocks;
+        blocks += grid_for(A.seg[i].B, 256);
+    }
+    for (int i = A.n; i < RTG_MAX_SEGMENTS; ++i) A.block_start[i] = blocks;
+    if (blocks == 0) return hipSuccess;
+    hipLaunchKernelGGL(k_fk_multi, dim3((unsigned)blocks), dim3(256), 0, s, A);
+    return hipGetLastError();
+}
+
+hipError_t launch_quat_op(int op, const float *a, const float *b, const float *c, int64_t n, float *out,
+                          hipStream_t s)
+{
+    hipLaunchKernelGGL(k_quat_op, dim3(grid_for(n, 256)), dim3(256), 0, s, op, a, b, c, n, out);
+    return hipGetLastError();
+}
+
+hipError_t launch_cal_joint_quat(const float *Z, const float *M, int npts, int64_t n, float *out, hipStream_t s)
+{
+    const dim3 g(grid_for(n, 256)), b(256);
+    switch (npts) {
+    case 1: hipLaunchKernelGGL(k_cal_joint_quat<1>, g, b, 0, s, Z, M, n, out); break;
+    case 2: hipLaunchKernelGGL(k_cal_joint_quat<2>, g, b, 0, s, Z, M, n, out); break;
+    case 3: hipLaunchKernelGGL(k_cal_joint_quat<3>, g, b, 0, s, Z, M, n, out); break;
+    case 4: hipLaunchKernelGGL(k_cal_joint_quat<4>, g, b, 0, s, Z, M, n, out); break;
+    case 5: hipLaunchKernelGGL(k_cal_joint_quat<5>, g, b, 0, s, Z, M, n, out); break;
+    case 6: hipLaunchKernelGGL(k_cal_joint_quat<6>, g, b, 0, s, Z, M, n, out); break;
+    case 7: hipLaunchKernelGGL(k_cal_joint_quat<7>, g, b, 0, s, Z, M, n, out); break;
+    default: hipLaunchKernelGGL(k_cal_joint_quat<8>, g, b, 0, s, Z, M, n, out); break;
+    }
+    return hipGetLastError();
+}
+
+hipError_t launch_quat_in_xyz_axis(const float *q, int s0, int s1, int s2, int extrinsic, int64_t n, float *out,
+                                   hipStream_t s)
+{
+    hipLaunchKernelGGL(k_quat_in_xyz_axis, dim3(grid_for(n, 256)), dim3(256), 0, s, q, s0, s1, s2, extrinsic, n, out);
+    return hipGetLastError();
+}
+
+hipError_t launch_synth_full_body(const TopoView &T, uint64_t seed, int64_t off, int64_t B, float *body, float *lh,
+                                  float *rh, float *body_rot, hipStream_t s)
+{
+    hipLaunchKernelGGL(k_synth_full_body, dim3(grid_for(B, 64)), dim3(64), 0, s, T, seed, off, B, body, lh, rh,
+                       body_rot);
+    return hipGetLastError();
+}
+
+}  // namespace rtg

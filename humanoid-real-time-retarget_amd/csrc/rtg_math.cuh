@@ -1,0 +1,477 @@
+// rtg_math.cuh -- device math for the retargeting hot path (gfx950).
+//
+// Every float32 operation is rounded on its own, in the association order the
+// reference's torch CPU ops use (build flag -ffp-contract=off plus the pragma
+// below); the two places torch itself fuses (torch.linalg.norm of a 3-vector
+// and torch.cross) use explicit __builtin_fmaf.  Measured op orders: DESIGN.md §3.
+//
+//  * torch.sqrt/acos/sin/cos run through MKL VML on the CPU (closed source):
+//    here they are correctly rounded (evaluated in float64, rounded once).
+//  * atan2 on the 30-element DOF tensor runs glibc's scalar atan2f: restated
+//    exactly (fdlibm s_atanf/e_atan2f).
+//  * torch.linalg.svd (MKL sgesdd) in the Kabsch fit: the proper-rotation polar
+//    factor is computed in float64 (cyclic Jacobi on A^T A) and rounded.
+//  * scipy Rotation.as_euler / from_euler: float64 restatement.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#pragma clang fp contract(off)
+
+namespace rtg {
+
+struct Q { float x, y, z, w; };
+struct V { float x, y, z; };
+
+#define RTG_DEV __device__ __forceinline__
+
+// ---------------------------------------------------------------- helpers
+RTG_DEV float cr_sqrt(float x) { return __builtin_sqrtf(x); }   // IEEE sqrt (correctly rounded build)
+RTG_DEV float cr_acos(float x) { return (float)::acos((double)x); }
+RTG_DEV float cr_sin(float x) { return (float)::sin((double)x); }
+RTG_DEV float cr_cos(float x) { return (float)::cos((double)x); }
+RTG_DEV float tsign(float v) { return v > 0.0f ? 1.0f : (v < 0.0f ? -1.0f : 0.0f); }
+RTG_DEV float clamp_lo(float v, float lo) { return v < lo ? lo : v; }          // NaN passes through
+RTG_DEV float clamp_lohi(float v, float lo, float hi) { return v < lo ? lo : (v > hi ? hi : v); }
+
+// glibc 2.35 float atanf (fdlibm s_atanf.c algorithm, decimal constants)
+RTG_DEV float g_atanf(float x)
+{
+    const float atanhi0 = 4.6364760399e-01f, atanhi1 = 7.8539812565e-01f, atanhi2 = 9.8279368877e-01f,
+                atanhi3 = 1.5707962513e+00f;
+    const float atanlo0 = 5.0121582440e-09f, atanlo1 = 3.7748947079e-08f, atanlo2 = 3.4473217170e-08f,
+                atanlo3 = 7.5497894159e-08f;
+    const int32_t hx = __float_as_int(x);
+    const int32_t ix = hx & 0x7fffffff;
+    if (ix >= 0x4c000000) {
+        if (ix > 0x7f800000) return x + x;
+        return hx > 0 ? atanhi3 + atanlo3 : -atanhi3 - atanlo3;
+    }
+    int id;
+    float hi = 0.0f, lo = 0.0f;
+    if (ix < 0x3ee00000) {
+        if (ix < 0x31000000) return x;
+        id = -1;
+    } else {
+        x = fabsf(x);
+        if (ix < 0x3f980000) {
+            if (ix < 0x3f300000) { id = 0; x = (2.0f * x - 1.0f) / (2.0f + x); hi = atanhi0; lo = atanlo0; }
+            else { id = 1; x = (x - 1.0f) / (x + 1.0f); hi = atanhi1; lo = atanlo1; }
+        } else {
+            if (ix < 0x401c0000) { id = 2; x = (x - 1.5f) / (1.0f + 1.5f * x); hi = atanhi2; lo = atanlo2; }
+            else { id = 3; x = -1.0f / x; hi = atanhi3; lo = atanlo3; }
+        }
+    }
+    const float z = x * x;
+    const float w = z * z;
+    const float s1 = z * (3.3333334327e-01f + w * (1.4285714924e-01f + w * (9.0908870101e-02f +
+                     w * (6.6610731184e-02f + w * (4.9768779427e-02f + w * 1.6285819933e-02f)))));
+    const float s2 = w * (-2.0000000298e-01f + w * (-1.1111110449e-01f + w * (-7.6918758452e-02f +
+                     w * (-5.8335702866e-02f + w * -3.6531571299e-02f))));
+    if (id < 0) return x - x * (s1 + s2);
+    const float r = hi - ((x * (s1 + s2) - lo) - x);
+    return hx < 0 ? -r : r;
+}
+
+// glibc 2.35 e_atan2f.c (torch.atan2 on <32-element tensors takes the scalar std::atan2 path)
+RTG_DEV float g_atan2f(float y, float x)
+{
+    const float tiny = 1.0e-30f, pi_o_4 = 7.8539818525e-01f, pi_o_2 = 1.5707963705e+00f,
+                pi = 3.1415927410e+00f, pi_lo = -8.7422776573e-08f;
+    const int32_t hx = __float_as_int(x), hy = __float_as_int(y);
+    const int32_t ix = hx & 0x7fffffff, iy = hy & 0x7fffffff;
+    if (ix > 0x7f800000 || iy > 0x7f800000) return x + y;
+    if (hx == 0x3f800000) return g_atanf(y);
+    const int m = ((hy >> 31) & 1) | ((hx >> 30) & 2);
+    if (iy == 0) {
+        if (m <= 1) return y;
+        return m == 2 ? pi + tiny : -pi - tiny;
+    }
+    if (ix == 0) return hy < 0 ? -pi_o_2 - tiny : pi_o_2 + tiny;
+    if (ix == 0x7f800000) {
+        if (iy == 0x7f800000) {
+            if (m == 0) return pi_o_4 + tiny;
+            if (m == 1) return -pi_o_4 - tiny;
+            if (m == 2) return 3.0f * pi_o_4 + tiny;
+            return -3.0f * pi_o_4 - tiny;
+        }
+        if (m == 0) return 0.0f;
+        if (m == 1) return -0.0f;
+        return m == 2 ? pi + tiny : -pi - tiny;
+    }
+    if (iy == 0x7f800000) return hy < 0 ? -pi_o_2 - tiny : pi_o_2 + tiny;
+    const int32_t k = (iy - ix) >> 23;
+    float z;
+    if (k > 60) z = pi_o_2 + 0.5f * pi_lo;
+    else if (hx < 0 && k < -60) z = 0.0f;
+    else z = g_atanf(fabsf(y / x));
+    if (m == 0) return z;
+    if (m == 1) return -z;
+    if (m == 2) return pi - (z - pi_lo);
+    return (z - pi_lo) - pi;
+}
+
+// ------------------------------------------------ quaternion algebra (rotation3d.py)
+RTG_DEV Q qmul(Q a, Q b)   // :14-27, each component a left fold of four products
+{
+    Q r;
+    r.w = ((a.w * b.w - a.x * b.x) - a.y * b.y) - a.z * b.z;
+    r.x = ((a.w * b.x + a.x * b.w) + a.y * b.z) - a.z * b.y;
+    r.y = ((a.w * b.y + a.y * b.w) + a.z * b.x) - a.x * b.z;
+    r.z = ((a.w * b.z + a.z * b.w) + a.x * b.y) - a.y * b.x;
+    return r;
+}
+RTG_DEV Q qconj(Q a) { return Q{-a.x, -a.y, -a.z, a.w}; }
+RTG_DEV Q qident() { return Q{0.0f, 0.0f, 0.0f, 1.0f}; }
+
+RTG_DEV Q qnormalize(Q q)  // quat_unit(quat_pos(q)) :30-56,92-98
+{
+    const float f = 1.0f - 2.0f * (q.w < 0.0f ? 1.0f : 0.0f);
+    q.x = f * q.x; q.y = f * q.y; q.z = f * q.z; q.w = f * q.w;
+    float n = cr_sqrt(((q.x * q.x + q.y * q.y) + q.z * q.z) + q.w * q.w);
+    n = clamp_lo(n, 1e-9f);
+    return Q{q.x / n, q.y / n, q.z / n, q.w / n};
+}
+RTG_DEV Q qmul_norm(Q a, Q b) { return qnormalize(qmul(a, b)); }
+
+RTG_DEV V qrotate(Q q, V v)  // :205-211, two Hamilton products
+{
+    const Q r = qmul(qmul(q, Q{v.x, v.y, v.z, 0.0f}), qconj(q));
+    return V{r.x, r.y, r.z};
+}
+
+RTG_DEV Q qfrom_angle_axis(float angle, V axis)  // :122-143
+{
+    const float theta = angle / 2.0f;
+    float n = cr_sqrt((axis.x * axis.x + axis.y * axis.y) + axis.z * axis.z);
+    n = clamp_lo(n, 1e-9f);
+    const float ax = axis.x / n, ay = axis.y / n, az = axis.z / n;
+    const float s = cr_sin(theta), c = cr_cos(theta);
+    return qnormalize(Q{ax * s, ay * s, az * s, c});
+}
+
+RTG_DEV Q qfrom_rotmat(const float m[9])  // :146-193 (the four overlapping branches, in order)
+{
+    const float d0 = m[0], d1 = m[4], d2 = m[8];
+    float w = cr_sqrt(clamp_lo((((d0 + d1) + d2) + 1.0f) / 4.0f, 0.0f));
+    float x = cr_sqrt(clamp_lo((((d0 - d1) - d2) + 1.0f) / 4.0f, 0.0f));
+    float y = cr_sqrt(clamp_lo((((-d0 + d1) - d2) + 1.0f) / 4.0f, 0.0f));
+    float z = cr_sqrt(clamp_lo((((-d0 - d1) + d2) + 1.0f) / 4.0f, 0.0f));
+    if (w >= x && w >= y && w >= z) {
+        x *= tsign(m[7] - m[5]);
+        y *= tsign(m[2] - m[6]);
+        z *= tsign(m[3] - m[1]);
+    }
+    if (x >= w && x >= y && x >= z) {
+        w *= tsign(m[7] - m[5]);
+        y *= tsign(m[3] + m[1]);
+        z *= tsign(m[2] + m[6]);
+    }
+    if (y >= w && y >= x && y >= z) {
+        w *= tsign(m[2] - m[6]);
+        x *= tsign(m[3] + m[1]);
+        z *= tsign(m[7] + m[5]);
+    }
+    if (z >= w && z >= x && z >= y) {
+        w *= tsign(m[3] - m[1]);
+        x *= tsign(m[6] + m[2]);
+        y *= tsign(m[7] + m[5]);
+    }
+    return qnormalize(Q{x, y, z, w});
+}
+
+// quat_to_angle_axis + angle_axis_to_exp_map (:587-627), returns the 3 exp-map components
+RTG_DEV V qexp_map(Q q)
+{
+    const float sin_theta = cr_sqrt(1.0f - q.w * q.w);
+    float angle = 2.0f * cr_acos(q.w);
+    angle = g_atan2f(cr_sin(angle), cr_cos(angle));   // normalize_angle :582-584
+    const bool mask = fabsf(sin_theta) > 1e-5f;
+    const float a = mask ? angle : 0.0f;
+    const float ax = mask ? q.x / sin_theta : 0.0f;
+    const float ay = mask ? q.y / sin_theta : 0.0f;
+    const float az = mask ? q.z / sin_theta : 1.0f;
+    return V{a * ax, a * ay, a * az};
+}
+RTG_DEV float qexp_component(Q q, int k)
+{
+    const V e = qexp_map(q);
+    return k == 0 ? e.x : (k == 1 ? e.y : e.z);
+}
+
+// ------------------------------------------------ vectors (transform3d.py)
+RTG_DEV float dot3(V a, V b) { return (a.x * b.x + a.y * b.y) + a.z * b.z; }          // torch.dot
+RTG_DEV float lnorm3(V a)                                                              // torch.linalg.norm
+{
+    return cr_sqrt(__builtin_fmaf(a.z, a.z, __builtin_fmaf(a.y, a.y, a.x * a.x)));
+}
+RTG_DEV V cross3(V a, V b)                                                             // torch.cross
+{
+    return V{__builtin_fmaf(a.y, b.z, -(a.z * b.y)), __builtin_fmaf(a.z, b.x, -(a.x * b.z)),
+             __builtin_fmaf(a.x, b.y, -(a.y * b.x))};
+}
+RTG_DEV V vsub(V a, V b) { return V{a.x - b.x, a.y - b.y, a.z - b.z}; }
+RTG_DEV V vdiv(V a, float s) { return V{a.x / s, a.y / s, a.z / s}; }
+RTG_DEV V vmul(V a, float s) { return V{s * a.x, s * a.y, s * a.z}; }
+
+RTG_DEV V proj_in_plane(V v, V n)  // :61-75
+{
+    const float nn = lnorm3(n);
+    return vsub(v, vmul(n, dot3(v, n) / (nn * nn)));
+}
+
+RTG_DEV float radians_between(V v1, V v2, V n)  // :77-100
+{
+    v1 = vdiv(v1, lnorm3(v1));
+    v2 = vdiv(v2, lnorm3(v2));
+    const V nrm = vdiv(n, lnorm3(n));
+    const float c = clamp_lohi(dot3(v1, v2), -1.0f, 1.0f);
+    return cr_acos(c) * tsign(dot3(nrm, cross3(v1, v2)));
+}
+
+// ------------------------------------------------ Kabsch (float64)
+// Proper-rotation polar factor of A: R = u1 v1^T + u2 v2^T + (u1 x u2)(v1 x v2)^T
+// where (v_i) are eigenvectors of A^T A for the two largest eigenvalues and
+// u_i = A v_i / |A v_i| (u2 re-orthogonalised).  Equals U diag(1,1,det(UV^T)) V^T,
+// the reference's det-fixed SVD solution (transform3d.py:40-45).
+RTG_DEV void jacobi_eig3(double S[3][3], double Vm[3][3])
+{
+#pragma unroll
+    for (int i = 0; i < 3; ++i)
+#pragma unroll
+        for (int j = 0; j < 3; ++j) Vm[i][j] = i == j ? 1.0 : 0.0;
+    for (int sweep = 0; sweep < 8; ++sweep) {
+#pragma unroll
+        for (int r = 0; r < 3; ++r) {
+            const int p = r == 2 ? 1 : 0;
+            const int qq = r == 0 ? 1 : 2;
+            const double apq = S[p][qq];
+            if (apq == 0.0) continue;
+            const double theta = (S[qq][qq] - S[p][p]) / (2.0 * apq);
+            double t = 1.0 / (fabs(theta) + sqrt(theta * theta + 1.0));
+            if (theta < 0.0) t = -t;
+            const double c = 1.0 / sqrt(t * t + 1.0);
+            const double s = t * c;
+#pragma unroll
+            for (int k = 0; k < 3; ++k) {
+                const double skp = S[k][p], skq = S[k][qq];
+                S[k][p] = c * skp - s * skq;
+                S[k][qq] = s * skp + c * skq;
+            }
+#pragma unroll
+            for (int k = 0; k < 3; ++k) {
+                const double spk = S[p][k], sqk = S[qq][k];
+                S[p][k] = c * spk - s * sqk;
+                S[qq][k] = s * spk + c * sqk;
+            }
+            S[p][qq] = 0.0;
+            S[qq][p] = 0.0;
+#pragma unroll
+            for (int k = 0; k < 3; ++k) {
+                const double vkp = Vm[k][p], vkq = Vm[k][qq];
+                Vm[k][p] = c * vkp - s * vkq;
+                Vm[k][qq] = s * vkp + c * vkq;
+            }
+        }
+    }
+}
+
+RTG_DEV void kabsch_rot(const float A[9], float R[9])
+{
+    double a[3][3], S[3][3], Vm[3][3];
+#pragma unroll
+    for (int i = 0; i < 3; ++i)
+#pragma unroll
+        for (int j = 0; j < 3; ++j) a[i][j] = (double)A[i * 3 + j];
+#pragma unroll
+    for (int i = 0; i < 3; ++i)
+#pragma unroll
+        for (int j = 0; j < 3; ++j) S[i][j] = a[0][i] * a[0][j] + a[1][i] * a[1][j] + a[2][i] * a[2][j];
+    jacobi_eig3(S, Vm);
+    // descending order of the eigenvalues (same selection as the oracle's sort),
+    // done on values so no array is indexed at run time
+    int o0 = 0, o1 = 1, o2 = 2, ti;
+    double a0 = S[0][0], a1 = S[1][1], a2 = S[2][2], td;
+    if (a1 > a0) { ti = o0; o0 = o1; o1 = ti; td = a0; a0 = a1; a1 = td; }
+    if (a2 > a0) { ti = o0; o0 = o2; o2 = ti; td = a0; a0 = a2; a2 = td; }
+    if (a2 > a1) { ti = o1; o1 = o2; o2 = ti; td = a1; a1 = a2; a2 = td; }
+    double v1[3], v2[3], u1[3], u2[3];
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+        v1[i] = o0 == 0 ? Vm[i][0] : (o0 == 1 ? Vm[i][1] : Vm[i][2]);
+        v2[i] = o1 == 0 ? Vm[i][0] : (o1 == 1 ? Vm[i][1] : Vm[i][2]);
+    }
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+        u1[i] = a[i][0] * v1[0] + a[i][1] * v1[1] + a[i][2] * v1[2];
+        u2[i] = a[i][0] * v2[0] + a[i][1] * v2[1] + a[i][2] * v2[2];
+    }
+    const double n1 = sqrt(u1[0] * u1[0] + u1[1] * u1[1] + u1[2] * u1[2]);
+#pragma unroll
+    for (int i = 0; i < 3; ++i) u1[i] /= n1;
+    const double d = u1[0] * u2[0] + u1[1] * u2[1] + u1[2] * u2[2];
+#pragma unroll
+    for (int i = 0; i < 3; ++i) u2[i] -= d * u1[i];
+    const double n2 = sqrt(u2[0] * u2[0] + u2[1] * u2[1] + u2[2] * u2[2]);
+#pragma unroll
+    for (int i = 0; i < 3; ++i) u2[i] /= n2;
+    const double u3[3] = {u1[1] * u2[2] - u1[2] * u2[1], u1[2] * u2[0] - u1[0] * u2[2],
+                          u1[0] * u2[1] - u1[1] * u2[0]};
+    const double v3[3] = {v1[1] * v2[2] - v1[2] * v2[1], v1[2] * v2[0] - v1[0] * v2[2],
+                          v1[0] * v2[1] - v1[1] * v2[0]};
+#pragma unroll
+    for (int i = 0; i < 3; ++i)
+#pragma unroll
+        for (int j = 0; j < 3; ++j) R[i * 3 + j] = (float)(u1[i] * v1[j] + u2[i] * v2[j] + u3[i] * v3[j]);
+}
+
+// cal_joint_quat (transform3d.py:31-50): A = M^T Z by einsum (sequential in j, no FMA)
+template <int N>
+RTG_DEV Q cal_joint_quat(const V (&Z)[N], const V (&M)[N])
+{
+    float A[9];
+#pragma unroll
+    for (int i = 0; i < 3; ++i)
+#pragma unroll
+        for (int k = 0; k < 3; ++k) {
+            float acc = 0.0f;
+#pragma unroll
+            for (int j = 0; j < N; ++j) {
+                const float mi = i == 0 ? M[j].x : (i == 1 ? M[j].y : M[j].z);
+                const float zk = k == 0 ? Z[j].x : (k == 1 ? Z[j].y : Z[j].z);
+                const float pr = mi * zk;
+                acc = j == 0 ? pr : acc + pr;
+            }
+            A[i * 3 + k] = acc;
+        }
+    float R[9];
+    kabsch_rot(A, R);
+    return qfrom_rotmat(R);
+}
+
+// ------------------------------------------------ scipy Rotation (float64)
+// from_quat(q).as_euler(seq): quaternion method of Bernardes & Viollet (2022),
+// as scipy 1.15 implements it; seq given as axis indices + intrinsic flag.
+RTG_DEV void scipy_as_euler(Q qf, int s0, int s1, int s2, bool extrinsic, double ang[3])
+{
+    double q[4] = {(double)qf.x, (double)qf.y, (double)qf.z, (double)qf.w};
+    const double nrm = sqrt(q[0] * q[0] + q[1] * q[1] + q[2] * q[2] + q[3] * q[3]);
+    q[0] /= nrm; q[1] /= nrm; q[2] /= nrm; q[3] /= nrm;
+    int i = extrinsic ? s0 : s2, j = s1, k = extrinsic ? s2 : s0;
+    const bool symmetric = i == k;
+    if (symmetric) k = 3 - i - j;
+    const int sign = (i - j) * (j - k) * (k - i) / 2;
+    const double qi = i == 0 ? q[0] : (i == 1 ? q[1] : q[2]);
+    const double qj = j == 0 ? q[0] : (j == 1 ? q[1] : q[2]);
+    const double qk = k == 0 ? q[0] : (k == 1 ? q[1] : q[2]);
+    double a, b, c, d;
+    if (symmetric) {
+        a = q[3]; b = qi; c = qj; d = qk * sign;
+    } else {
+        a = q[3] - qj; b = qi + qk * sign; c = qj + q[3]; d = qk * sign - qi;
+    }
+    ang[1] = 2.0 * ::atan2(::hypot(c, d), ::hypot(a, b));
+    int kase = 0;
+    if (fabs(ang[1]) <= 1e-7) kase = 1;
+    else if (fabs(ang[1] - M_PI) <= 1e-7) kase = 2;
+    const double half_sum = ::atan2(b, a), half_diff = ::atan2(d, c);
+    if (kase == 0) {
+        ang[0] = half_sum - half_diff;
+        ang[2] = half_sum + half_diff;
+    } else if (extrinsic) {
+        ang[2] = 0.0;
+        ang[0] = kase == 1 ? 2.0 * half_sum : -2.0 * half_diff;
+    } else {
+        ang[0] = 0.0;
+        ang[2] = kase == 1 ? 2.0 * half_sum : 2.0 * half_diff;
+    }
+    if (!symmetric) {
+        ang[2] *= sign;
+        ang[1] -= M_PI / 2.0;
+    }
+    if (!extrinsic) { const double tt = ang[0]; ang[0] = ang[2]; ang[2] = tt; }
+#pragma unroll
+    for (int t = 0; t < 3; ++t) {
+        if (ang[t] < -M_PI) ang[t] += 2.0 * M_PI;
+        else if (ang[t] > M_PI) ang[t] -= 2.0 * M_PI;
+    }
+}
+
+// from_euler(axis, angle).as_quat() for one elementary rotation, cast to float32
+RTG_DEV Q elementary_quat(int axis, double angle)
+{
+    const double h = angle / 2.0;
+    const float s = (float)::sin(h), c = (float)::cos(h);
+    return Q{axis == 0 ? s : 0.0f, axis == 1 ? s : 0.0f, axis == 2 ? s : 0.0f, c};
+}
+
+// quat_in_xyz_axis (transform3d.py:52-59)
+RTG_DEV void quat_in_xyz_axis(Q q, int s0, int s1, int s2, bool extrinsic, Q out[3])
+{
+    double ang[3];
+    scipy_as_euler(q, s0, s1, s2, extrinsic, ang);
+    out[0] = elementary_quat(s0, ang[0]);
+    out[1] = elementary_quat(s1, ang[1]);
+    out[2] = elementary_quat(s2, ang[2]);
+}
+
+// ------------------------------------------------ arm joint maps
+// Frame-independent halves of cal_shoulderPR / cal_elbowP_and_shoulderY:
+// theta0 / phi0 depend only on the zero-pose vector v0 and are evaluated once.
+struct ArmZero { float th0, ph0; };
+
+RTG_DEV ArmZero shoulder_zero(V v0)
+{
+    const V ex{1.f, 0.f, 0.f}, ey{0.f, 1.f, 0.f};
+    const V v0p = proj_in_plane(v0, ey);
+    return ArmZero{radians_between(ex, v0p, ey), radians_between(v0p, v0, cross3(v0p, ey))};
+}
+RTG_DEV ArmZero elbow_zero(V v0)
+{
+    const V ex{1.f, 0.f, 0.f}, ez{0.f, 0.f, 1.f};
+    const V v0p = proj_in_plane(v0, ez);
+    return ArmZero{radians_between(ex, v0p, ez), radians_between(v0p, v0, cross3(ez, v0p))};
+}
+
+// cal_shoulderPR (full_body_pos_retargeter.py:246-278)
+RTG_DEV void shoulder_pr(V v1, ArmZero z0, Q parent, Q &pitch, Q &roll)
+{
+    const V ex{1.f, 0.f, 0.f}, ey{0.f, 1.f, 0.f};
+    const V v1r = qrotate(qconj(parent), v1);
+    const V v1p = proj_in_plane(v1r, ey);
+    const float th1 = radians_between(ex, v1p, ey);
+    pitch = qfrom_angle_axis(th1 - z0.th0, ey);
+    const float ph1 = radians_between(v1p, v1r, cross3(v1p, ey));
+    roll = qfrom_angle_axis(ph1 - z0.ph0, ex);
+}
+
+// cal_elbowP_and_shoulderY (full_body_pos_retargeter.py:220-243)
+RTG_DEV void elbow_py(V v1, ArmZero z0, Q parent, Q &yaw, Q &elbow)
+{
+    const V ex{1.f, 0.f, 0.f}, ey{0.f, 1.f, 0.f}, ez{0.f, 0.f, 1.f};
+    const V v1r = qrotate(qconj(parent), v1);
+    const V v1p = proj_in_plane(v1r, ez);
+    const float th1 = radians_between(ex, v1p, ez);
+    yaw = qfrom_angle_axis(th1 - z0.th0, ez);
+    const float ph1 = radians_between(v1p, v1r, cross3(ez, v1p));
+    elbow = qfrom_angle_axis(ph1 - z0.ph0, ey);
+}
+
+// torch sum of 5 elements (cascade reduce order, measured) / 5
+RTG_DEV float mean5(float v0, float v1, float v2, float v3, float v4)
+{
+    return ((((v0 + v4) + v1) + v2) + v3) / 5.0f;
+}
+
+// Hu_v5.Hu_DOF_AXIS (retarget/robot_config/Hu_v5.py:12-18), dof k <-> link k+1
+__constant__ static const int8_t kHuDofAxis[30] = {2, 0, 1, 1, 1, 2, 0, 1, 1, 1, 2, 1, 0, 2, 1,
+                                                   0, 1, 2, 1, 1, 1, 0, 2, 1, 0, 1, 2, 1, 1, 2};
+RTG_DEV int hu_dof_axis(int k)
+{
+    // compile-time table for unrolled uses; avoids a constant-memory load
+    constexpr int8_t t[30] = {2, 0, 1, 1, 1, 2, 0, 1, 1, 1, 2, 1, 0, 2, 1,
+                              0, 1, 2, 1, 1, 1, 0, 2, 1, 0, 1, 2, 1, 1, 2};
+    return t[k];
+}
+
+}  // namespace rtg

@@ -1,0 +1,106 @@
+"""ctypes binding of ``librtg_hip.so`` (the C ABI declared in ``include/rtg.h``).
+
+The library is built in-tree by ``__graft_entry__.build()`` (``csrc/Makefile``)
+and is the only compute path: there is no CPU fallback.  Loading fails loudly
+when the shared object is missing.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+from ctypes import POINTER, c_char_p, c_float, c_int, c_int32, c_int64, c_uint64, c_void_p
+
+PKG_ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+LIB_PATH = os.environ.get("RTG_LIB", os.path.join(PKG_ROOT, "librtg_hip.so"))
+
+RTG_OK = 0
+ABI_VERSION = 1
+
+# rtg_solver_kind
+SOLVER_FULL_BODY_POS = 0
+SOLVER_UPPER_BODY = 1
+SOLVER_FULL_BODY_ROT = 2
+SOLVER_BODY_ROT = 3
+
+# rtg_quat_op
+OP_QUAT_MUL = 0
+OP_QUAT_MUL_NORM = 1
+OP_QUAT_NORMALIZE = 2
+OP_QUAT_ROTATE = 3
+OP_QUAT_INVERSE = 4
+OP_QUAT_FROM_ANGLE_AXIS = 5
+OP_QUAT_FROM_ROTMAT = 6
+OP_QUAT_TO_EXP_MAP = 7
+OP_RADIANS_BETWEEN = 8
+OP_PROJ_IN_PLANE = 9
+OP_QUAT_TO_DOF_POS = 10
+OP_SHOULDER_PR = 11
+OP_ELBOW_PY = 12
+
+MAX_SEGMENTS = 8
+
+
+class RtgError(RuntimeError):
+    """A librtg_hip call returned a non-zero rtg_status."""
+
+    def __init__(self, status: int, message: str):
+        super().__init__(f"rtg status {status}: {message}")
+        self.status = status
+
+
+class FkSegment(ctypes.Structure):
+    _fields_ = [("topo", c_void_p), ("local_rot", c_void_p), ("root_t", c_void_p), ("g_rot", c_void_p),
+                ("g_pos", c_void_p), ("B", c_int64)]
+
+
+# name -> (restype, argtypes); every symbol rtg.h declares
+SIGNATURES = {
+    "rtg_abi_version": (c_int, []),
+    "rtg_last_error": (c_char_p, []),
+    "rtg_device_count": (c_int, []),
+    "rtg_topology_create": (c_int, [POINTER(c_int32), POINTER(c_float), POINTER(c_float), c_int32, POINTER(c_void_p)]),
+    "rtg_topology_destroy": (c_int, [c_void_p]),
+    "rtg_topology_num_joints": (c_int, [c_void_p]),
+    "rtg_fk_f32": (c_int, [c_void_p, c_void_p, c_void_p, c_int64, c_void_p, c_void_p, c_void_p]),
+    "rtg_local_rotation_f32": (c_int, [c_void_p, c_void_p, c_int64, c_void_p, c_void_p]),
+    "rtg_state_fk_f32": (c_int, [c_void_p, c_void_p, c_void_p, c_int64, c_void_p, c_void_p, c_void_p]),
+    "rtg_state_local_rotation_f32": (c_int, [c_void_p, c_void_p, c_int64, c_void_p, c_void_p]),
+    "rtg_fk_multi_f32": (c_int, [POINTER(FkSegment), c_int32, c_void_p]),
+    "rtg_solver_create": (c_int, [c_int, POINTER(c_float), POINTER(c_float), POINTER(c_int32), c_int32, c_int,
+                                  POINTER(c_void_p)]),
+    "rtg_solver_destroy": (c_int, [c_void_p]),
+    "rtg_retarget_f32": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int64, c_void_p, c_void_p,
+                                 c_void_p, c_void_p]),
+    "rtg_quat_op_f32": (c_int, [c_int, c_void_p, c_void_p, c_void_p, c_int64, c_void_p, c_void_p]),
+    "rtg_cal_joint_quat_f32": (c_int, [c_void_p, c_void_p, c_int32, c_int64, c_void_p, c_void_p]),
+    "rtg_quat_in_xyz_axis_f32": (c_int, [c_void_p, c_char_p, c_int64, c_void_p, c_void_p]),
+    "rtg_synth_full_body_f32": (c_int, [c_void_p, c_uint64, c_int64, c_int64, c_void_p, c_void_p, c_void_p, c_void_p,
+                                        c_void_p]),
+}
+
+_lib = None
+
+
+def lib() -> ctypes.CDLL:
+    """Load librtg_hip.so (raises if it was not built)."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise ImportError(
+                f"librtg_hip.so not found at {LIB_PATH}; build it with `python -c 'import __graft_entry__ as g; "
+                f"g.build()'` (make -C humanoid-real-time-retarget_amd/csrc)")
+        handle = ctypes.CDLL(LIB_PATH)
+        for name, (res, args) in SIGNATURES.items():
+            fn = getattr(handle, name)
+            fn.restype = res
+            fn.argtypes = args
+        if handle.rtg_abi_version() != ABI_VERSION:
+            raise ImportError(f"librtg_hip ABI {handle.rtg_abi_version()} != expected {ABI_VERSION}")
+        _lib = handle
+    return _lib
+
+
+def check(status: int) -> None:
+    if status != RTG_OK:
+        msg = lib().rtg_last_error()
+        raise RtgError(status, msg.decode() if msg else "")

@@ -1,0 +1,238 @@
+"""Functional device ops over the C ABI (batched forms of the reference's functions).
+
+Each function takes tensors (host or device; moved to the current HIP device as
+contiguous float32) and returns device tensors.  Reference semantics are cited
+per op; all arithmetic happens in librtg_hip.so.
+"""
+from __future__ import annotations
+
+import ctypes
+from typing import Sequence
+
+import torch
+
+from . import _lib
+from ._lib import check, lib
+from .runtime import Topology, dev_f32, ptr, require_gpu, stream_handle
+
+
+def _flat(t: torch.Tensor, tail: int) -> torch.Tensor:
+    return t.reshape(-1, tail) if tail else t.reshape(-1)
+
+
+def _quat_op(op, a, b=None, c=None, a_tail=4, b_tail=4, c_tail=3, out_tail=4):
+    a = dev_f32(a)
+    lead = a.shape[:-1] if a_tail else a.shape
+    n = int(torch.Size(lead).numel())
+    af = _flat(a, a_tail)
+    bf = None if b is None else _flat(dev_f32(b).expand(*lead, *( (b_tail,) if b_tail else ())).contiguous(), b_tail)
+    cf = None if c is None else _flat(dev_f32(c).expand(*lead, *((c_tail,) if c_tail else ())).contiguous(), c_tail)
+    out_shape = tuple(lead) + ((out_tail,) if isinstance(out_tail, int) and out_tail else tuple(out_tail or ()))
+    out = torch.empty(out_shape, device=a.device, dtype=torch.float32)
+    check(lib().rtg_quat_op_f32(op, ptr(af), ptr(bf), ptr(cf), n, ptr(out), stream_handle()))
+    return out
+
+
+def _bcast(a, b, ta, tb):
+    a, b = dev_f32(a), dev_f32(b)
+    lead = torch.broadcast_shapes(a.shape[:-1], b.shape[:-1])
+    return a.expand(*lead, ta).contiguous(), b.expand(*lead, tb).contiguous()
+
+
+def quat_mul(a, b):
+    """rotation3d.py:14-27"""
+    a, b = _bcast(a, b, 4, 4)
+    return _quat_op(_lib.OP_QUAT_MUL, a, b)
+
+
+def quat_mul_norm(a, b):
+    """rotation3d.py:196-202"""
+    a, b = _bcast(a, b, 4, 4)
+    return _quat_op(_lib.OP_QUAT_MUL_NORM, a, b)
+
+
+def quat_normalize(q):
+    """rotation3d.py:92-98"""
+    return _quat_op(_lib.OP_QUAT_NORMALIZE, q)
+
+
+def quat_inverse(q):
+    """rotation3d.py:214-219"""
+    return _quat_op(_lib.OP_QUAT_INVERSE, q)
+
+
+def quat_rotate(q, v):
+    """rotation3d.py:205-211"""
+    q, v = _bcast(q, v, 4, 3)
+    return _quat_op(_lib.OP_QUAT_ROTATE, q, v, b_tail=3, out_tail=3)
+
+
+def quat_from_angle_axis(angle, axis):
+    """rotation3d.py:122-143 (angle (...), axis (...,3))"""
+    angle = dev_f32(angle)
+    axis = dev_f32(axis)
+    lead = torch.broadcast_shapes(angle.shape, axis.shape[:-1])
+    angle = angle.expand(lead).contiguous()
+    axis = axis.expand(*lead, 3).contiguous()
+    n = int(torch.Size(lead).numel())
+    out = torch.empty(tuple(lead) + (4,), device=angle.device, dtype=torch.float32)
+    check(lib().rtg_quat_op_f32(_lib.OP_QUAT_FROM_ANGLE_AXIS, ptr(angle), ptr(axis), None, n, ptr(out),
+                                stream_handle()))
+    return out
+
+
+def quat_from_rotation_matrix(m):
+    """rotation3d.py:146-193 (m (...,3,3))"""
+    m = dev_f32(m, (3, 3), "m")
+    lead = m.shape[:-2]
+    n = int(torch.Size(lead).numel())
+    out = torch.empty(tuple(lead) + (4,), device=m.device, dtype=torch.float32)
+    check(lib().rtg_quat_op_f32(_lib.OP_QUAT_FROM_ROTMAT, ptr(m), None, None, n, ptr(out), stream_handle()))
+    return out
+
+
+def quat_to_exp_map(q):
+    """rotation3d.py:620-627"""
+    return _quat_op(_lib.OP_QUAT_TO_EXP_MAP, q, out_tail=3)
+
+
+def radians_between_vecs(v1, v2, n):
+    """transform3d.py:77-100, batched over leading dims"""
+    v1, v2, n = dev_f32(v1), dev_f32(v2), dev_f32(n)
+    lead = torch.broadcast_shapes(v1.shape[:-1], v2.shape[:-1], n.shape[:-1])
+    v1, v2, n = (t.expand(*lead, 3).contiguous() for t in (v1, v2, n))
+    cnt = int(torch.Size(lead).numel())
+    out = torch.empty(tuple(lead), device=v1.device, dtype=torch.float32)
+    check(lib().rtg_quat_op_f32(_lib.OP_RADIANS_BETWEEN, ptr(v1), ptr(v2), ptr(n), cnt, ptr(out), stream_handle()))
+    return out
+
+
+def proj_in_plane(v, n):
+    """transform3d.py:61-75, batched"""
+    nn = dev_f32(n)
+    if bool((torch.linalg.norm(nn, dim=-1) <= 1e-6).any()):
+        raise AssertionError("proj_in_plane: plane normal has (near) zero length")   # transform3d.py:70
+    v, nn = _bcast(v, nn, 3, 3)
+    return _quat_op(_lib.OP_PROJ_IN_PLANE, v, nn, b_tail=3, out_tail=3)
+
+
+def quat_to_dof_pos_hu(local_rot):
+    """transform3d.py:176-183 with Hu_DOF_AXIS over local_rot[..., 1:, :] (local_rot (...,31,4))"""
+    lr = dev_f32(local_rot, (31, 4), "local_rot")
+    lead = lr.shape[:-2]
+    n = int(torch.Size(lead).numel())
+    out = torch.empty(tuple(lead) + (30,), device=lr.device, dtype=torch.float32)
+    check(lib().rtg_quat_op_f32(_lib.OP_QUAT_TO_DOF_POS, ptr(lr), None, None, n, ptr(out), stream_handle()))
+    return out
+
+
+def cal_shoulder_pr(v1, v0, parent):
+    """full_body_pos_retargeter.py:246-278, batched: returns (pitch (...,4), roll (...,4))"""
+    v1, v0, parent = dev_f32(v1), dev_f32(v0), dev_f32(parent)
+    lead = torch.broadcast_shapes(v1.shape[:-1], v0.shape[:-1], parent.shape[:-1])
+    v1, v0, parent = v1.expand(*lead, 3).contiguous(), v0.expand(*lead, 3).contiguous(), parent.expand(*lead, 4).contiguous()
+    n = int(torch.Size(lead).numel())
+    out = torch.empty(tuple(lead) + (2, 4), device=v1.device, dtype=torch.float32)
+    check(lib().rtg_quat_op_f32(_lib.OP_SHOULDER_PR, ptr(v1), ptr(v0), ptr(parent), n, ptr(out), stream_handle()))
+    return out[..., 0, :], out[..., 1, :]
+
+
+def cal_elbow_py(v1, v0, parent):
+    """full_body_pos_retargeter.py:220-243, batched: returns (shoulder_yaw, elbow_pitch)"""
+    v1, v0, parent = dev_f32(v1), dev_f32(v0), dev_f32(parent)
+    lead = torch.broadcast_shapes(v1.shape[:-1], v0.shape[:-1], parent.shape[:-1])
+    v1, v0, parent = v1.expand(*lead, 3).contiguous(), v0.expand(*lead, 3).contiguous(), parent.expand(*lead, 4).contiguous()
+    n = int(torch.Size(lead).numel())
+    out = torch.empty(tuple(lead) + (2, 4), device=v1.device, dtype=torch.float32)
+    check(lib().rtg_quat_op_f32(_lib.OP_ELBOW_PY, ptr(v1), ptr(v0), ptr(parent), n, ptr(out), stream_handle()))
+    return out[..., 0, :], out[..., 1, :]
+
+
+def cal_joint_quat(zero_vectors, motion_vectors):
+    """transform3d.py:31-50 (Kabsch).  (..., n, 3) x (..., n, 3) -> (..., 4)"""
+    Z, M = dev_f32(zero_vectors), dev_f32(motion_vectors)
+    lead = torch.broadcast_shapes(Z.shape[:-2], M.shape[:-2])
+    npts = int(Z.shape[-2])
+    if M.shape[-2] != npts:
+        raise ValueError("cal_joint_quat: point counts differ")
+    Z = Z.expand(*lead, npts, 3).contiguous()
+    M = M.expand(*lead, npts, 3).contiguous()
+    n = int(torch.Size(lead).numel())
+    out = torch.empty(tuple(lead) + (4,), device=Z.device, dtype=torch.float32)
+    check(lib().rtg_cal_joint_quat_f32(ptr(Z), ptr(M), npts, n, ptr(out), stream_handle()))
+    return out
+
+
+def quat_in_xyz_axis(q, seq: str = "xyz"):
+    """transform3d.py:52-59: three single-axis quaternions (each (...,4))."""
+    q = dev_f32(q, (4,), "q")
+    lead = q.shape[:-1]
+    n = int(torch.Size(lead).numel())
+    out = torch.empty(tuple(lead) + (3, 4), device=q.device, dtype=torch.float32)
+    check(lib().rtg_quat_in_xyz_axis_f32(ptr(q), seq.encode(), n, ptr(out), stream_handle()))
+    return out[..., 0, :], out[..., 1, :], out[..., 2, :]
+
+
+def forward_kinematics(topo: Topology, local_rot, root_t, state: bool = False):
+    """kinematics.py:13-39 (state=False) / SkeletonState FK skeleton3d.py:402-425 (state=True)."""
+    J = topo.num_joints
+    lr = dev_f32(local_rot, (J, 4), "local_rot")
+    lead = lr.shape[:-2]
+    rt = dev_f32(root_t, (3,), "root_t").expand(*lead, 3).contiguous()
+    B = int(torch.Size(lead).numel())
+    g_rot = torch.empty(tuple(lead) + (J, 4), device=lr.device, dtype=torch.float32)
+    g_pos = torch.empty(tuple(lead) + (J, 3), device=lr.device, dtype=torch.float32)
+    fn = lib().rtg_state_fk_f32 if state else lib().rtg_fk_f32
+    check(fn(topo.handle, ptr(lr), ptr(rt), B, ptr(g_rot), ptr(g_pos), stream_handle()))
+    return g_rot, g_pos
+
+
+def local_rotation(topo: Topology, g_rot, state: bool = False):
+    """kinematics.py:41-63 (state=False) / SkeletonState.local_rotation skeleton3d.py:460-484."""
+    J = topo.num_joints
+    g = dev_f32(g_rot, (J, 4), "g_rot")
+    B = int(torch.Size(g.shape[:-2]).numel())
+    out = torch.empty_like(g)
+    fn = lib().rtg_state_local_rotation_f32 if state else lib().rtg_local_rotation_f32
+    check(fn(topo.handle, ptr(g), B, ptr(out), stream_handle()))
+    return out
+
+
+def forward_kinematics_multi(segments: Sequence[tuple]):
+    """One launch over several (topology, local_rot (B,J,4), root_t (B,3)) segments.
+
+    Returns a list of (g_rot, g_pos) per segment.
+    """
+    require_gpu()
+    if len(segments) > _lib.MAX_SEGMENTS:
+        raise ValueError(f"at most {_lib.MAX_SEGMENTS} segments per launch")
+    segs = (_lib.FkSegment * max(1, len(segments)))()
+    keep, outs = [], []
+    for i, (topo, lr, rt) in enumerate(segments):
+        J = topo.num_joints
+        lr = dev_f32(lr, (J, 4), "local_rot")
+        B = int(lr.shape[0])
+        rt = dev_f32(rt, (3,), "root_t")
+        g_rot = torch.empty((B, J, 4), device=lr.device, dtype=torch.float32)
+        g_pos = torch.empty((B, J, 3), device=lr.device, dtype=torch.float32)
+        segs[i] = _lib.FkSegment(topo.handle.value, lr.data_ptr(), rt.data_ptr(), g_rot.data_ptr(), g_pos.data_ptr(), B)
+        keep += [lr, rt]
+        outs.append((g_rot, g_pos))
+    check(lib().rtg_fk_multi_f32(segs, len(segments), stream_handle()))
+    return outs
+
+
+def synth_full_body(topo_full: Topology, B: int, seed: int = 1234, frame_offset: int = 0, want_rot: bool = False,
+                    out=None):
+    """Synthetic VTRDyn frames generated on the device (rtg_synth_full_body_f32)."""
+    dev = require_gpu()
+    if out is None:
+        body = torch.empty((B, 21, 3), device=dev, dtype=torch.float32)
+        lh = torch.empty((B, 20, 3), device=dev, dtype=torch.float32)
+        rh = torch.empty((B, 20, 3), device=dev, dtype=torch.float32)
+    else:
+        body, lh, rh = out
+    rot = torch.empty((B, 21, 4), device=dev, dtype=torch.float32) if want_rot else None
+    check(lib().rtg_synth_full_body_f32(topo_full.handle, ctypes.c_uint64(seed), frame_offset, B, ptr(body), ptr(lh),
+                                        ptr(rh), ptr(rot), stream_handle()))
+    return (body, lh, rh, rot) if want_rot else (body, lh, rh)

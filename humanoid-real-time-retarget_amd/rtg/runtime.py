@@ -1,0 +1,139 @@
+"""Device runtime: tensor plumbing, topology and solver handles.
+
+PyTorch is used only for device memory and streams: tensors are handed to the
+C ABI as raw device pointers plus the current HIP stream (``torch.cuda`` is HIP
+on ROCm).  Every compute call goes to ``librtg_hip.so``; there is no CPU path.
+"""
+from __future__ import annotations
+
+import ctypes
+from typing import Optional, Sequence
+
+import numpy as np
+import torch
+
+from . import _lib
+from ._lib import check, lib
+
+
+def require_gpu() -> torch.device:
+    if not torch.cuda.is_available():
+        raise RuntimeError("humanoid-real-time-retarget_amd: no HIP device visible; the retarget path runs only on "
+                           "MI355X (gfx950) -- there is no CPU fallback")
+    lib()
+    return torch.device("cuda", torch.cuda.current_device())
+
+
+def stream_handle(stream: Optional[torch.cuda.Stream] = None) -> ctypes.c_void_p:
+    s = stream if stream is not None else torch.cuda.current_stream()
+    return ctypes.c_void_p(s.cuda_stream)
+
+
+def dev_f32(x, shape_tail: Sequence[int] = (), name: str = "tensor") -> torch.Tensor:
+    """Contiguous float32 device tensor (copies host data / other dtypes)."""
+    dev = require_gpu()
+    t = x if isinstance(x, torch.Tensor) else torch.as_tensor(np.asarray(x))
+    if t.device != dev or t.dtype != torch.float32:
+        t = t.to(device=dev, dtype=torch.float32)
+    t = t.contiguous()
+    tail = tuple(shape_tail)
+    if tail and tuple(t.shape[-len(tail):]) != tail:
+        raise ValueError(f"{name}: expected trailing shape {tail}, got {tuple(t.shape)}")
+    return t
+
+
+def ptr(t: Optional[torch.Tensor]) -> Optional[ctypes.c_void_p]:
+    return None if t is None else ctypes.c_void_p(t.data_ptr())
+
+
+def _host_f32(a) -> np.ndarray:
+    if isinstance(a, torch.Tensor):
+        a = a.detach().cpu().numpy()
+    return np.ascontiguousarray(np.asarray(a, dtype=np.float32))
+
+
+def _host_i32(a) -> np.ndarray:
+    if isinstance(a, torch.Tensor):
+        a = a.detach().cpu().numpy()
+    return np.ascontiguousarray(np.asarray(a, dtype=np.int32))
+
+
+class Topology:
+    """A parent-indexed skeleton resident on the device (``rtg_topology_t``)."""
+
+    def __init__(self, parent_indices, local_translation, tree_quat=None):
+        require_gpu()
+        p = _host_i32(parent_indices)
+        lt = _host_f32(local_translation).reshape(-1, 3)
+        tq = None if tree_quat is None else _host_f32(tree_quat).reshape(-1, 4)
+        J = int(p.shape[0])
+        if lt.shape[0] != J or (tq is not None and tq.shape[0] != J):
+            raise ValueError("parent_indices / local_translation / quat lengths differ")   # skeleton3d.py:87-88
+        h = ctypes.c_void_p()
+        check(lib().rtg_topology_create(p.ctypes.data_as(ctypes.POINTER(ctypes.c_int32)),
+                                        lt.ctypes.data_as(ctypes.POINTER(ctypes.c_float)),
+                                        None if tq is None else tq.ctypes.data_as(ctypes.POINTER(ctypes.c_float)),
+                                        J, ctypes.byref(h)))
+        self._h = h
+        self.num_joints = J
+        self.parents = p
+        self.local_translation = lt
+
+    @property
+    def handle(self) -> ctypes.c_void_p:
+        return self._h
+
+    def __del__(self):
+        h = getattr(self, "_h", None)
+        if h is not None and h.value and _lib._lib is not None:
+            _lib._lib.rtg_topology_destroy(h)
+            self._h = None
+
+
+class Solver:
+    """A retarget solver (``rtg_solver_t``) of one of the four reference kinds."""
+
+    N_INPUTS = {_lib.SOLVER_FULL_BODY_POS: 3, _lib.SOLVER_UPPER_BODY: 1, _lib.SOLVER_FULL_BODY_ROT: 4,
+                _lib.SOLVER_BODY_ROT: 1}
+
+    def __init__(self, kind: int, src_local_t, src_global_t=None, src_parents=None, precise_gripper=False):
+        require_gpu()
+        lt = _host_f32(src_local_t).reshape(-1, 3)
+        gt = None if src_global_t is None else _host_f32(src_global_t).reshape(-1, 3)
+        par = None if src_parents is None else _host_i32(src_parents)
+        h = ctypes.c_void_p()
+        fp = ctypes.POINTER(ctypes.c_float)
+        check(lib().rtg_solver_create(int(kind), lt.ctypes.data_as(fp), None if gt is None else gt.ctypes.data_as(fp),
+                                      None if par is None else par.ctypes.data_as(ctypes.POINTER(ctypes.c_int32)),
+                                      int(lt.shape[0]), int(bool(precise_gripper)), ctypes.byref(h)))
+        self._h = h
+        self.kind = int(kind)
+        self.precise_gripper = bool(precise_gripper)
+
+    def retarget(self, inputs: Sequence[torch.Tensor], want_local_rot=False, want_body_rot=False,
+                 out_dof: Optional[torch.Tensor] = None, stream=None):
+        """Batched solve.  ``inputs``: device float32 tensors in the order of rtg.h.
+
+        Returns (dof (B,30), local_rot (B,31,4) | None, body_rot (B,59,4) | None).
+        """
+        n = self.N_INPUTS[self.kind]
+        if len(inputs) != n:
+            raise ValueError(f"solver kind {self.kind} takes {n} inputs, got {len(inputs)}")
+        B = int(inputs[0].shape[0])
+        for t in inputs:
+            if not (t.is_cuda and t.dtype == torch.float32 and t.is_contiguous()) or int(t.shape[0]) != B:
+                raise ValueError("inputs must be contiguous float32 device tensors with one batch size")
+        dev = inputs[0].device
+        dof = out_dof if out_dof is not None else torch.empty((B, 30), device=dev, dtype=torch.float32)
+        lr = torch.empty((B, 31, 4), device=dev, dtype=torch.float32) if want_local_rot else None
+        br = torch.empty((B, 59, 4), device=dev, dtype=torch.float32) if want_body_rot else None
+        ins = [ptr(t) for t in inputs] + [None] * (4 - n)
+        check(lib().rtg_retarget_f32(self._h, ins[0], ins[1], ins[2], ins[3], B, ptr(dof), ptr(lr), ptr(br),
+                                     stream_handle(stream)))
+        return dof, lr, br
+
+    def __del__(self):
+        h = getattr(self, "_h", None)
+        if h is not None and h.value and _lib._lib is not None:
+            _lib._lib.rtg_solver_destroy(h)
+            self._h = None

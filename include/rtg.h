@@ -1,0 +1,174 @@
+/*
+ * rtg.h -- C ABI of the MI355X-native retargeting hot path (librtg_hip.so).
+ *
+ * The reference (shuoshuof/Humanoid-Real-Time-Retarget) has no native
+ * boundary: its operator API is the set of Python classes / TorchScript
+ * functions called in-process on CPU float32 tensors.  Each entry point below
+ * replaces one of those (cited per function); the Python drop-in modules in
+ * humanoid-real-time-retarget_amd/{retarget,robot_kinematics_model,poselib}
+ * bind them with ctypes.
+ *
+ * Conventions
+ *  - quaternions are [x, y, z, w] float32 (poselib/poselib/core/rotation3d.py:14-27);
+ *  - every pointer argument is a caller-owned DEVICE pointer (hipMalloc / torch
+ *    device tensor), C-contiguous, float32 unless stated; the library never
+ *    frees caller memory and never allocates in a launch call;
+ *  - launches are stream-ordered on `stream` (a hipStream_t; NULL = default
+ *    stream) and thread-safe across distinct streams; nothing synchronises;
+ *  - every call returns an rtg_status; on failure rtg_last_error() returns a
+ *    thread-local message.  Argument errors mirror the reference's Python
+ *    assertions (e.g. proj_in_plane's |n| > 1e-6, transform3d.py:70).
+ */
+#ifndef RTG_H
+#define RTG_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define RTG_ABI_VERSION 1
+
+typedef enum rtg_status {
+    RTG_OK = 0,
+    RTG_ERR_INVALID_ARGUMENT = 1,
+    RTG_ERR_DEVICE = 2,          /* a HIP runtime call failed */
+    RTG_ERR_OUT_OF_MEMORY = 3,
+    RTG_ERR_UNSUPPORTED = 4
+} rtg_status;
+
+typedef struct rtg_topology_s *rtg_topology_t;
+typedef struct rtg_solver_s *rtg_solver_t;
+typedef void *rtg_stream_t; /* hipStream_t */
+
+/* Library / error handling. */
+int rtg_abi_version(void);
+const char *rtg_last_error(void);
+/* Number of visible devices (0 when no GPU / driver). */
+int rtg_device_count(void);
+
+/* ------------------------------------------------------------------------
+ * Topology: a parent-indexed skeleton (SkeletonTree, skeleton3d.py:83-96;
+ * RobotZeroPose, robot_kinematics_model/base_robot.py:24-58).
+ * parents[J] (root = -1, parents[j] < j), local_t[J*3] zero-pose local
+ * translation, tree_quat[J*4] the SkeletonTree pre-rotation (NULL = identity).
+ * Host pointers; the data is copied to device memory owned by the handle.
+ * ---------------------------------------------------------------------- */
+int rtg_topology_create(const int32_t *parents, const float *local_t, const float *tree_quat, int32_t J,
+                        rtg_topology_t *out);
+int rtg_topology_destroy(rtg_topology_t topo);
+int rtg_topology_num_joints(rtg_topology_t topo);
+
+/* ------------------------------------------------------------------------
+ * Kinematics
+ * ---------------------------------------------------------------------- */
+/* cal_forward_kinematics (robot_kinematics_model/kinematics.py:13-39).
+ * local_rot (B,J,4), root_t (B,3) -> g_rot (B,J,4), g_pos (B,J,3). */
+int rtg_fk_f32(rtg_topology_t topo, const float *local_rot, const float *root_t, int64_t B, float *g_rot,
+               float *g_pos, rtg_stream_t stream);
+/* cal_local_rotation (kinematics.py:41-63). g_rot (B,J,4) -> local_rot (B,J,4). */
+int rtg_local_rotation_f32(rtg_topology_t topo, const float *g_rot, int64_t B, float *local_rot,
+                           rtg_stream_t stream);
+/* SkeletonState.global_transformation (poselib skeleton3d.py:402-425): FK with the
+ * tree pre-rotation; local_rot must hold the state's (normalised) rotations. */
+int rtg_state_fk_f32(rtg_topology_t topo, const float *local_rot, const float *root_t, int64_t B, float *g_rot,
+                     float *g_pos, rtg_stream_t stream);
+/* SkeletonState.local_rotation (skeleton3d.py:460-484): inverse FK incl. tree-quat fix-up. */
+int rtg_state_local_rotation_f32(rtg_topology_t topo, const float *g_rot, int64_t B, float *local_rot,
+                                 rtg_stream_t stream);
+
+/* Mixed-target FK: up to RTG_MAX_SEGMENTS independent (topology, frame batch)
+ * segments in ONE launch (BASELINE config 5). */
+#define RTG_MAX_SEGMENTS 8
+typedef struct rtg_fk_segment {
+    rtg_topology_t topo;
+    const float *local_rot; /* (B,J,4) */
+    const float *root_t;    /* (B,3)   */
+    float *g_rot;           /* (B,J,4) */
+    float *g_pos;           /* (B,J,3) */
+    int64_t B;
+} rtg_fk_segment;
+int rtg_fk_multi_f32(const rtg_fk_segment *segments, int32_t n_segments, rtg_stream_t stream);
+
+/* ------------------------------------------------------------------------
+ * Retarget solvers (retarget/retarget_solver/__init__.py:9-14)
+ * ---------------------------------------------------------------------- */
+typedef enum rtg_solver_kind {
+    /* VtrdynFullBodyPosRetargeter.retarget  full_body_pos_retargeter.py:25-217
+     * in0 = body (B,21,3), in1 = left hand (B,20,3), in2 = right hand (B,20,3);
+     * source zero pose = VTRDYN_FULL (59 joints). */
+    RTG_SOLVER_FULL_BODY_POS = 0,
+    /* HuUpperBodyFromMocapRetarget.retarget_from_global_translation  retarget_solver.py:40-99
+     * in0 = raw VTRDyn positions (B,21,3); source zero pose = VTRDYN (21). */
+    RTG_SOLVER_UPPER_BODY = 1,
+    /* VtrdynFullBodyRetargeter.retarget  full_body_retargeter.py:19-177
+     * in0 = body rotations (B,21,4), in1 = body positions (B,21,3),
+     * in2 = left hand (B,20,3), in3 = right hand (B,20,3); source = VTRDYN_FULL (59). */
+    RTG_SOLVER_FULL_BODY_ROT = 2,
+    /* Mocap2HuBodyRetargeter.retarget_from_pose  body_retargeter.py:34-81
+     * in0 = global rotations (B,21,4); source = VTRDYN (21). */
+    RTG_SOLVER_BODY_ROT = 3
+} rtg_solver_kind;
+
+/* Create a solver.  src_zero_local_t / src_zero_global_t: the source
+ * RobotZeroPose local / global translations (Js,3), src_parents (Js) -- host
+ * pointers.  The target is always Hu v5 (31 links, 30 DOFs; Hu_v5.py:12-18).
+ * Zero-pose-only terms of the joint maps (theta0 / phi0, Kabsch zero vectors,
+ * gripper denominator) are evaluated once here, on the device. */
+int rtg_solver_create(int kind, const float *src_zero_local_t, const float *src_zero_global_t,
+                      const int32_t *src_parents, int32_t Js, int precise_gripper, rtg_solver_t *out);
+int rtg_solver_destroy(rtg_solver_t solver);
+
+/* Batched retarget of B frames.  dof (B,30) required; local_rot (B,31,4) and
+ * body_rot (B,59,4, FULL_BODY_POS only: the returned body_global_rotation) may
+ * be NULL.  Unused in* must be NULL. */
+int rtg_retarget_f32(rtg_solver_t solver, const float *in0, const float *in1, const float *in2,
+                     const float *in3, int64_t B, float *dof, float *local_rot, float *body_rot,
+                     rtg_stream_t stream);
+
+/* ------------------------------------------------------------------------
+ * Elementwise primitives (poselib rotation3d.py, retarget transform3d.py)
+ * ---------------------------------------------------------------------- */
+typedef enum rtg_quat_op {
+    RTG_OP_QUAT_MUL = 0,            /* a (n,4), b (n,4) -> (n,4)   rotation3d.py:14-27   */
+    RTG_OP_QUAT_MUL_NORM = 1,       /* a, b -> (n,4)               :196-202             */
+    RTG_OP_QUAT_NORMALIZE = 2,      /* a -> (n,4)                  :92-98               */
+    RTG_OP_QUAT_ROTATE = 3,         /* q (n,4), v (n,3) -> (n,3)   :205-211             */
+    RTG_OP_QUAT_INVERSE = 4,        /* a -> (n,4)                  :214-219             */
+    RTG_OP_QUAT_FROM_ANGLE_AXIS = 5,/* angle (n), axis (n,3) -> (n,4)  :122-143         */
+    RTG_OP_QUAT_FROM_ROTMAT = 6,    /* m (n,3,3) -> (n,4)          :146-193             */
+    RTG_OP_QUAT_TO_EXP_MAP = 7,     /* q (n,4) -> (n,3)            :620-627             */
+    RTG_OP_RADIANS_BETWEEN = 8,     /* v1 (n,3), v2 (n,3), c = n (n,3) -> (n)  transform3d.py:77-100 */
+    RTG_OP_PROJ_IN_PLANE = 9,       /* v (n,3), n (n,3) -> (n,3)   transform3d.py:61-75 */
+    RTG_OP_QUAT_TO_DOF_POS = 10,    /* local_rot (n,31,4) -> dof (n,30)  transform3d.py:176-183 (Hu) */
+    RTG_OP_SHOULDER_PR = 11,        /* v1 (n,3), v0 (n,3), parent c (n,4) -> (n,2,4)  full_body_pos_retargeter.py:246-278 */
+    RTG_OP_ELBOW_PY = 12            /* v1, v0, parent -> (n,2,4)   full_body_pos_retargeter.py:220-243 */
+} rtg_quat_op;
+int rtg_quat_op_f32(int op, const float *a, const float *b, const float *c, int64_t n, float *out,
+                    rtg_stream_t stream);
+
+/* cal_joint_quat (transform3d.py:31-50): Kabsch fit of npts (1..8) point pairs.
+ * Z (n,npts,3) zero-pose vectors, M (n,npts,3) motion vectors -> (n,4). */
+int rtg_cal_joint_quat_f32(const float *Z, const float *M, int32_t npts, int64_t n, float *out,
+                           rtg_stream_t stream);
+
+/* quat_in_xyz_axis (transform3d.py:52-59): scipy Euler split (float64) into three
+ * single-axis quaternions.  seq: 3 chars of xyz/XYZ (upper = intrinsic). q (n,4) -> (n,3,4). */
+int rtg_quat_in_xyz_axis_f32(const float *q, const char *seq, int64_t n, float *out, rtg_stream_t stream);
+
+/* ------------------------------------------------------------------------
+ * Synthetic mocap (bench / tests): FK of the VTRDYN_FULL zero pose with random
+ * rotations, generated on the device from a counter-based RNG.
+ * topo must be the 59-joint VTRDYN_FULL topology.  Frame f uses stream
+ * (seed, frame_offset + f).  Outputs body (B,21,3), lh (B,20,3), rh (B,20,3)
+ * and optionally body_rot (B,21,4).
+ * ---------------------------------------------------------------------- */
+int rtg_synth_full_body_f32(rtg_topology_t topo, uint64_t seed, int64_t frame_offset, int64_t B, float *body,
+                            float *lh, float *rh, float *body_rot, rtg_stream_t stream);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* RTG_H */

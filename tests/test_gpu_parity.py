@@ -1,0 +1,222 @@
+"""GPU parity: librtg_hip.so vs the oracle (bit-level) and vs the reference's
+golden vectors (the reference-noise-bounded statistics of test_oracle_golden.py).
+
+All calls go through the C ABI (rtg._lib via rtg.runtime / rtg.ops)."""
+import numpy as np
+import pytest
+import torch
+
+from conftest import frame_stats, golden
+
+pytestmark = pytest.mark.gpu
+
+TOPOS = ["hu_v5", "vtrdyn", "vtrdyn_full", "noitom"]
+
+
+def _topo(name):
+    from rtg import assets
+    from rtg.runtime import Topology
+    return Topology(assets.parents(name), assets.local_translation(name), assets.tree_quat(name))
+
+
+def _np(t):
+    return t.detach().cpu().numpy()
+
+
+# ----------------------------------------------------------------- kinematics
+@pytest.mark.parametrize("name", TOPOS)
+def test_fk_bit_exact_vs_reference(gpu, name):
+    from rtg import ops
+    k = golden("kinematics")
+    T = _topo(name)
+    gr, gp = ops.forward_kinematics(T, k[f"{name}_local_rot"], k[f"{name}_root_t"])
+    np.testing.assert_array_equal(_np(gr), k[f"{name}_g_rot"])
+    np.testing.assert_array_equal(_np(gp), k[f"{name}_g_pos"])
+    loc = ops.local_rotation(T, k[f"{name}_g_rot"])
+    np.testing.assert_array_equal(_np(loc), k[f"{name}_inv_local"])
+
+
+@pytest.mark.parametrize("name", TOPOS)
+def test_state_fk_bit_exact_vs_reference(gpu, name):
+    from rtg import ops
+    k = golden("kinematics")
+    T = _topo(name)
+    lr = ops.quat_normalize(k[f"{name}_local_rot"])     # SkeletonState stores normalised rotations
+    gr, gp = ops.forward_kinematics(T, lr, k[f"{name}_root_t"], state=True)
+    np.testing.assert_array_equal(_np(gr), k[f"{name}_state_g_rot"])
+    np.testing.assert_array_equal(_np(gp), k[f"{name}_state_g_pos"])
+    g = ops.quat_normalize(k[f"{name}_state_g_rot"])
+    np.testing.assert_array_equal(_np(ops.local_rotation(T, g, state=True)), k[f"{name}_state_local_rot"])
+
+
+def test_fk_multi_one_launch_bit_exact(gpu):
+    from rtg import ops
+    k = golden("kinematics")
+    segs = [(_topo(n), k[f"{n}_local_rot"], k[f"{n}_root_t"]) for n in TOPOS]
+    outs = ops.forward_kinematics_multi(segs)
+    for n, (gr, gp) in zip(TOPOS, outs):
+        np.testing.assert_array_equal(_np(gr), k[f"{n}_g_rot"])
+        np.testing.assert_array_equal(_np(gp), k[f"{n}_g_pos"])
+
+
+def test_fk_large_batch_vs_oracle(gpu):
+    import oracle as orc
+    from rtg import assets, ops, synth
+    B = 50000
+    lr = synth.random_local_quats(B, 31, 11)
+    rt = np.random.default_rng(3).normal(0, 0.3, (B, 3)).astype(np.float32)
+    gr, gp = ops.forward_kinematics(_topo("hu_v5"), lr, rt)
+    ogr, ogp = orc.fk(assets.parents("hu_v5"), assets.local_translation("hu_v5"), lr, rt)
+    np.testing.assert_array_equal(_np(gr), ogr)
+    np.testing.assert_array_equal(_np(gp), ogp)
+
+
+def test_fk_empty_and_single(gpu):
+    from rtg import ops
+    T = _topo("hu_v5")
+    gr, gp = ops.forward_kinematics(T, np.zeros((0, 31, 4), np.float32), np.zeros((0, 3), np.float32))
+    assert gr.shape == (0, 31, 4) and gp.shape == (0, 31, 3)
+    k = golden("kinematics")
+    gr, gp = ops.forward_kinematics(T, k["hu_v5_local_rot"][:1], k["hu_v5_root_t"][:1])
+    np.testing.assert_array_equal(_np(gr), k["hu_v5_g_rot"][:1])
+
+
+# ----------------------------------------------------------------- primitives
+def test_quaternion_algebra_bit_exact(gpu):
+    from rtg import ops
+    p = golden("primitives")
+    np.testing.assert_array_equal(_np(ops.quat_mul(p["qm_a"], p["qm_b"])), p["quat_mul"])
+    np.testing.assert_array_equal(_np(ops.quat_mul_norm(p["qm_a"], p["qm_b"])), p["quat_mul_norm"])
+    np.testing.assert_array_equal(_np(ops.quat_normalize(p["qm_a"])), p["quat_normalize"])
+    np.testing.assert_array_equal(_np(ops.quat_rotate(p["qm_b"], p["qr_v"])), p["quat_rotate"])
+
+
+def test_transcendental_primitives_vs_oracle(gpu):
+    import oracle as orc
+    from rtg import ops
+    p = golden("primitives")
+    cases = [
+        (ops.quat_from_angle_axis(p["qaa_angle"], p["qaa_axis"]), orc.quat_from_angle_axis(p["qaa_angle"], p["qaa_axis"])),
+        (ops.quat_from_rotation_matrix(p["qrm_m"]), orc.quat_from_rotation_matrix(p["qrm_m"])),
+        (ops.quat_to_dof_pos_hu(p["dof_q31"]), orc.quat_to_dof_pos(p["dof_q31"])),
+        (ops.radians_between_vecs(p["rbv_v1"], p["rbv_v2"], p["rbv_n"]), orc.radians_between(p["rbv_v1"], p["rbv_v2"], p["rbv_n"])),
+        (torch.stack(ops.cal_shoulder_pr(p["sh_v1"], p["sh_v0"], p["sh_parent"]), -2), orc.shoulder_pr(p["sh_v1"], p["sh_v0"], p["sh_parent"])),
+        (torch.stack(ops.cal_elbow_py(p["sh_v1"], p["el_v0"], p["sh_parent"]), -2), orc.elbow_py(p["sh_v1"], p["el_v0"], p["sh_parent"])),
+    ]
+    for seq in ("XYZ", "YXZ", "ZYX"):
+        cases.append((torch.stack(ops.quat_in_xyz_axis(p["qxyz_q"], seq), -2), orc.quat_in_xyz_axis(p["qxyz_q"], seq)))
+    for npts in (3, 5):
+        cases.append((ops.cal_joint_quat(p[f"cjq{npts}_Z"], p[f"cjq{npts}_M"]), orc.cal_joint_quat(p[f"cjq{npts}_Z"], p[f"cjq{npts}_M"])))
+    for i, (g, o) in enumerate(cases):
+        s = frame_stats(_np(g), o)
+        assert s["exact_elems"] >= 0.999 and s["max"] <= 2.5e-7, (i, s)
+
+
+def test_proj_in_plane_and_reference(gpu):
+    from rtg import ops
+    p = golden("primitives")
+    e = torch.eye(3)
+    np.testing.assert_array_equal(_np(ops.proj_in_plane(p["rbv_v1"], e[1])), p["proj_in_plane_y"])
+    np.testing.assert_array_equal(_np(ops.proj_in_plane(p["rbv_v1"], e[2])), p["proj_in_plane_z"])
+    with pytest.raises(AssertionError):
+        ops.proj_in_plane(p["rbv_v1"], torch.zeros(3))
+
+
+# ----------------------------------------------------------------- solvers
+def _solver(kind, precise=False):
+    from rtg import _lib
+    from rtg.runtime import Solver
+    zp = golden("zero_pose")
+    from rtg import assets
+    if kind in (_lib.SOLVER_FULL_BODY_POS, _lib.SOLVER_FULL_BODY_ROT):
+        return Solver(kind, zp["vtrdyn_full_local_t"], zp["vtrdyn_full_global_t"], assets.parents("vtrdyn_full"), precise)
+    return Solver(kind, zp["vtrdyn_local_t"], zp["vtrdyn_global_t"], assets.parents("vtrdyn"), precise)
+
+
+def _dev(*arrs):
+    return [torch.from_numpy(np.ascontiguousarray(a)).cuda() for a in arrs]
+
+
+# reference-vs-port bounds (same numbers the oracle meets in test_oracle_golden.py)
+GOLD_BOUNDS = {
+    "full_body_pos_precise": dict(max=2e-3, p99=2e-4, frac=0.25),
+    "full_body_pos_binary": dict(max=2e-3, p99=2e-4, frac=0.25),
+    "upper_body": dict(max=2e-3, p99=2e-4, frac=0.25),
+    "full_body_rot": dict(max=2e-4, p99=2e-5, frac=0.03),
+    "body_rot": dict(max=1e-6, p99=1e-6, frac=0.0),
+}
+
+
+def _check_gold(name, dof_gpu, dof_ref):
+    s = frame_stats(dof_gpu, dof_ref)
+    b = GOLD_BOUNDS[name]
+    assert s["max"] <= b["max"] and s["p99_frame"] <= b["p99"] and s["frac_frames_gt_1e5"] <= b["frac"], (name, s)
+    return s
+
+
+@pytest.mark.parametrize("precise", [True, False])
+def test_full_body_pos_solver(gpu, precise):
+    import oracle as orc
+    from rtg import _lib
+    name = "full_body_pos_precise" if precise else "full_body_pos_binary"
+    d = golden(name)
+    zp = golden("zero_pose")
+    S = _solver(_lib.SOLVER_FULL_BODY_POS, precise)
+    dof, lr, br = S.retarget(_dev(d["body"], d["lh"], d["rh"]), want_local_rot=True, want_body_rot=True)
+    odof, olr, obr = orc.full_body_pos(zp["vtrdyn_full_local_t"], zp["vtrdyn_full_global_t"], d["body"], d["lh"],
+                                       d["rh"], precise)
+    so = frame_stats(_np(dof), odof)
+    assert so["exact_elems"] >= 0.999 and so["max"] <= 1e-5, so
+    assert frame_stats(_np(lr), olr)["exact_elems"] >= 0.999
+    assert frame_stats(_np(br), obr)["exact_elems"] >= 0.999
+    _check_gold(name, _np(dof), d["dof"])
+    np.testing.assert_array_equal(_np(dof)[:, list(range(11)) + [29]], 0.0)
+
+
+@pytest.mark.parametrize("name,kind", [("upper_body", 1), ("full_body_rot", 2), ("body_rot", 3)])
+def test_other_solvers(gpu, name, kind):
+    import oracle as orc
+    from rtg import assets
+    d = golden(name)
+    zp = golden("zero_pose")
+    S = _solver(kind)
+    if kind == 1:
+        dof, lr, _ = S.retarget(_dev(d["x"]), want_local_rot=True)
+        odof, olr = orc.upper_body(zp["vtrdyn_local_t"], d["x"])
+    elif kind == 2:
+        dof, lr, _ = S.retarget(_dev(d["body_rot"], d["body_pos"], d["lh"], d["rh"]), want_local_rot=True)
+        odof, olr = orc.full_body_rot(zp["vtrdyn_full_local_t"], d["body_rot"], d["body_pos"], d["lh"], d["rh"])
+    else:
+        dof, lr, _ = S.retarget(_dev(d["global_rot"]), want_local_rot=True)
+        odof, olr = orc.body_rot(assets.parents("vtrdyn"), d["global_rot"])
+    so = frame_stats(_np(dof), odof)
+    assert so["exact_elems"] >= 0.999 and so["max"] <= 1e-5, so
+    assert frame_stats(_np(lr), olr)["exact_elems"] >= 0.999
+    _check_gold(name, _np(dof), d["dof"])
+
+
+def test_solver_full_size_properties(gpu):
+    """BASELINE config 3 size (262144 frames, device-generated): finite, zero
+    DOFs where the reference never writes, gripper range, and a 2048-frame
+    sample identical to the oracle."""
+    import oracle as orc
+    from rtg import _lib, ops
+    zp = golden("zero_pose")
+    T = _topo("vtrdyn_full")
+    B = 262144
+    body, lh, rh = ops.synth_full_body(T, B, seed=99)
+    S = _solver(_lib.SOLVER_FULL_BODY_POS, True)
+    dof, _, _ = S.retarget([body, lh, rh])
+    dof_np = _np(dof)
+    assert np.isfinite(dof_np).all()
+    np.testing.assert_array_equal(dof_np[:, list(range(11)) + [29]], 0.0)
+    assert (dof_np[:, [18, 27]] >= 0).all() and (dof_np[:, [18, 27]] <= np.float32(0.044)).all()
+    np.testing.assert_array_equal(dof_np[:, 19], -dof_np[:, 18])
+    idx = np.random.default_rng(0).choice(B, 2048, replace=False)
+    odof, _, _ = orc.full_body_pos(zp["vtrdyn_full_local_t"], zp["vtrdyn_full_global_t"], _np(body)[idx],
+                                   _np(lh)[idx], _np(rh)[idx], True, want_rot=False)
+    s = frame_stats(dof_np[idx], odof)
+    assert s["exact_elems"] >= 0.999 and s["max"] <= 1e-5, s
+    # determinism: a second launch is bit-identical
+    dof2, _, _ = S.retarget([body, lh, rh])
+    assert torch.equal(dof, dof2)
