@@ -303,11 +303,12 @@ int rtg_retarget_f32(rtg_solver_t s, const float *in0, const float *in1, const f
 int rtg_quat_op_f32(int op, const float *a, const float *b, const float *c, int64_t n, float *out,
                     rtg_stream_t stream)
 {
-    if (op < RTG_OP_QUAT_MUL || op > RTG_OP_ELBOW_PY) return fail(RTG_ERR_INVALID_ARGUMENT, "rtg_quat_op_f32: bad op %d", op);
+    if (op < RTG_OP_QUAT_MUL || op > RTG_OP_NORMALIZE_ANGLE) return fail(RTG_ERR_INVALID_ARGUMENT, "rtg_quat_op_f32: bad op %d", op);
     if (n < 0) return fail(RTG_ERR_INVALID_ARGUMENT, "rtg_quat_op_f32: negative n");
     if (n == 0) return RTG_OK;
     const bool needs_b = !(op == RTG_OP_QUAT_NORMALIZE || op == RTG_OP_QUAT_INVERSE || op == RTG_OP_QUAT_FROM_ROTMAT ||
-                           op == RTG_OP_QUAT_TO_EXP_MAP || op == RTG_OP_QUAT_TO_DOF_POS);
+                           op == RTG_OP_QUAT_TO_EXP_MAP || op == RTG_OP_QUAT_TO_DOF_POS ||
+                           op == RTG_OP_QUAT_TO_ANGLE_AXIS || op == RTG_OP_NORMALIZE_ANGLE);
     const bool needs_c = op == RTG_OP_RADIANS_BETWEEN || op == RTG_OP_SHOULDER_PR || op == RTG_OP_ELBOW_PY;
     if (!a || !out || (needs_b && !b) || (needs_c && !c))
         return fail(RTG_ERR_INVALID_ARGUMENT, "rtg_quat_op_f32: NULL operand for op %d", op);

@@ -39,159 +39,191 @@ __global__ void k_solver_prep(SolverConsts *c)
 }
 
 // ----------------------------------------------------------------------------
-// solver bodies: each produces the 14 non-identity links (12..18, 21..27) and
-// the four gripper DOFs; everything else is the identity / 0 by construction.
+// solver bodies.  Each link quaternion is emitted as soon as it is final: its
+// DOF (quat_to_dof_pos, transform3d.py:176-183: dof k <-> link k+1, component
+// Hu_DOF_AXIS[k]) goes to the block's LDS tile and, if requested, the
+// quaternion to local_rot -- so only the few values later steps need (parents,
+// wrist fits) stay live in VGPRs.
 // ----------------------------------------------------------------------------
-struct FrameOut {
-    Q l[14];          // links 12..18 then 21..27
-    float grip[4];    // dof 18, 19, 27, 28
-    bool has_grip;
-    Q kab[3];         // FULL_BODY_POS: body_global_rotation rows 10, 14, 39
+struct Emit {
+    float *row;                  // LDS row of this frame (30 DOFs)
+    float *__restrict__ lr;      // local_rot row (31 x 4) or nullptr
+    template <int LINK>
+    RTG_DEV void link(Q q) const
+    {
+        row[LINK - 1] = qexp_component(q, hu_dof_axis(LINK - 1));
+        if (lr) st4(lr + 4 * LINK, q);
+    }
+    template <int LINK>
+    RTG_DEV void identity() const   // untouched link: exp-map of the identity is +0
+    {
+        row[LINK - 1] = 0.0f;
+        if (lr) st4(lr + 4 * LINK, qident());
+    }
 };
+
+RTG_DEV void emit_fixed_links(const Emit &E)
+{
+#pragma unroll
+    for (int k = 0; k < 11; ++k) E.row[k] = 0.0f;
+    E.row[29] = 0.0f;
+    if (E.lr) {
+#pragma unroll
+        for (int j = 0; j < 12; ++j) st4(E.lr + 4 * j, qident());
+        st4(E.lr + 4 * 19, qident());
+        st4(E.lr + 4 * 20, qident());
+        st4(E.lr + 4 * 28, qident());
+        st4(E.lr + 4 * 29, qident());
+        st4(E.lr + 4 * 30, qident());
+    }
+}
+
+// one arm: shoulder pitch/roll then shoulder yaw / elbow pitch (full_body_pos_retargeter.py:75-93);
+// returns quat_mul_four of the four link rotations (the wrist parent chain, :128-136)
+template <int L0>
+RTG_DEV Q solve_arm(const Emit &E, V upper, V fore, ArmZero zs, ArmZero ze, Q parent)
+{
+    Q p, r, y, e;
+    shoulder_pr(upper, zs, parent, p, r);
+    E.link<L0>(p);
+    E.link<L0 + 1>(r);
+    elbow_py(fore, ze, qmul(qmul(parent, p), r), y, e);
+    E.link<L0 + 2>(y);
+    E.link<L0 + 3>(e);
+    return qmul(qmul(qmul(p, r), y), e);
+}
+
+template <int L0>
+RTG_DEV void emit_euler_xyz(const Emit &E, Q local)   // quat_in_xyz_axis(q, 'XYZ') -> links L0..L0+2
+{
+    Q eul[3];
+    quat_in_xyz_axis(local, 0, 1, 2, false, eul);
+    E.link<L0>(eul[0]);
+    E.link<L0 + 1>(eul[1]);
+    E.link<L0 + 2>(eul[2]);
+}
+
+RTG_DEV float hand_x_mean(Q rot, const float *__restrict__ H, const int (&idx)[5])   // gripper x-spread
+{
+    const float h0 = qrotate(rot, ld3(H)).x;
+    return mean5(qrotate(rot, ld3(H + 3 * idx[0])).x - h0, qrotate(rot, ld3(H + 3 * idx[1])).x - h0,
+                 qrotate(rot, ld3(H + 3 * idx[2])).x - h0, qrotate(rot, ld3(H + 3 * idx[3])).x - h0,
+                 qrotate(rot, ld3(H + 3 * idx[4])).x - h0);
+}
 
 // VtrdynFullBodyPosRetargeter.retarget  full_body_pos_retargeter.py:25-217
 template <bool PRECISE>
 RTG_DEV void solve_full_body_pos(const SolverConsts &C, const float *__restrict__ b, const float *__restrict__ L,
-                                 const float *__restrict__ R, FrameOut &o)
+                                 const float *__restrict__ R, const Emit &E, float *__restrict__ body_rot)
 {
     // _retarget_arm_from_global_translation :61-118
-    const V b10 = ld3(b + 30);
-    const V Mt[3] = {vsub(ld3(b + 51), b10), vsub(ld3(b + 39), b10), vsub(ld3(b + 33), b10)};
-    const Q R10 = cal_joint_quat<3>(C.Zt, Mt);
-    const V b14 = ld3(b + 42), b15 = ld3(b + 45), b16 = ld3(b + 48);
-    const V b18 = ld3(b + 54), b19 = ld3(b + 57), b20 = ld3(b + 60);
-    Q p, r, y, e;
-    shoulder_pr(vsub(b19, b18), C.lsh, R10, p, r);
-    elbow_py(vsub(b20, b19), C.lel, qmul(qmul(R10, p), r), y, e);
-    o.l[0] = p; o.l[1] = r; o.l[2] = y; o.l[3] = e;
-    shoulder_pr(vsub(b15, b14), C.rsh, R10, p, r);
-    elbow_py(vsub(b16, b15), C.rel, qmul(qmul(R10, p), r), y, e);
-    o.l[7] = p; o.l[8] = r; o.l[9] = y; o.l[10] = e;
-    // _retarget_wrist_from_global_translation :120-175
-    Q eul[3];
+    Q R10;
     {
-        const Q par = qmul_norm(R10, qmul(qmul(qmul(o.l[0], o.l[1]), o.l[2]), o.l[3]));
+        const V b10 = ld3(b + 30);
+        const V Mt[3] = {vsub(ld3(b + 51), b10), vsub(ld3(b + 39), b10), vsub(ld3(b + 33), b10)};
+        R10 = cal_joint_quat<3>(C.Zt, Mt);
+    }
+    const V b19 = ld3(b + 57), b15 = ld3(b + 45);
+    const Q chainL = solve_arm<12>(E, vsub(b19, ld3(b + 54)), vsub(ld3(b + 60), b19), C.lsh, C.lel, R10);
+    const Q chainR = solve_arm<21>(E, vsub(b15, ld3(b + 42)), vsub(ld3(b + 48), b15), C.rsh, C.rel, R10);
+    // _retarget_wrist_from_global_translation :120-175
+    Q WL, WR;
+    {
         const V l0 = ld3(L);
         const V Ml[5] = {vsub(ld3(L + 6), l0), vsub(ld3(L + 18), l0), vsub(ld3(L + 30), l0), vsub(ld3(L + 42), l0),
                          vsub(ld3(L + 51), l0)};
-        o.kab[1] = cal_joint_quat<5>(C.Zl, Ml);
-        quat_in_xyz_axis(qmul_norm(qconj(par), o.kab[1]), 0, 1, 2, false, eul);
-        o.l[4] = eul[0]; o.l[5] = eul[1]; o.l[6] = eul[2];
+        WL = cal_joint_quat<5>(C.Zl, Ml);
     }
+    emit_euler_xyz<16>(E, qmul_norm(qconj(qmul_norm(R10, chainL)), WL));
     {
-        const Q par = qmul_norm(R10, qmul(qmul(qmul(o.l[7], o.l[8]), o.l[9]), o.l[10]));
         const V r0 = ld3(R);
         const V Mr[5] = {vsub(ld3(R + 6), r0), vsub(ld3(R + 18), r0), vsub(ld3(R + 30), r0), vsub(ld3(R + 42), r0),
                          vsub(ld3(R + 51), r0)};
-        o.kab[2] = cal_joint_quat<5>(C.Zr, Mr);
-        quat_in_xyz_axis(qmul_norm(qconj(par), o.kab[2]), 0, 1, 2, false, eul);
-        o.l[11] = eul[0]; o.l[12] = eul[1]; o.l[13] = eul[2];
+        WR = cal_joint_quat<5>(C.Zr, Mr);
     }
-    o.kab[0] = R10;
-    // _retarget_gripper :177-217 (hand points rotated into the wrist frame)
-    const Q cl = qconj(o.kab[1]), cr = qconj(o.kab[2]);
-    const float hl0 = qrotate(cl, ld3(L)).x, hr0 = qrotate(cr, ld3(R)).x;
-    const float la = mean5(qrotate(cl, ld3(L + 12)).x - hl0, qrotate(cl, ld3(L + 24)).x - hl0,
-                           qrotate(cl, ld3(L + 36)).x - hl0, qrotate(cl, ld3(L + 48)).x - hl0,
-                           qrotate(cl, ld3(L + 57)).x - hl0);
-    const float ra = mean5(qrotate(cr, ld3(R + 12)).x - hr0, qrotate(cr, ld3(R + 24)).x - hr0,
-                           qrotate(cr, ld3(R + 36)).x - hr0, qrotate(cr, ld3(R + 48)).x - hr0,
-                           qrotate(cr, ld3(R + 57)).x - hr0);
+    emit_euler_xyz<25>(E, qmul_norm(qconj(qmul_norm(R10, chainR)), WR));
+    // _retarget_gripper :177-217 -- hand points in the wrist frame (rotate by conj(W))
+    constexpr int tips[5] = {4, 8, 12, 16, 19};
+    const float la = hand_x_mean(qconj(WL), L, tips), ra = hand_x_mean(qconj(WR), R, tips);
     if (PRECISE) {
         const float ls = clamp_lohi(la / C.orig - 0.5f, 0.0f, 0.5f) / 0.5f;
         const float rs = clamp_lohi(ra / C.orig - 0.5f, 0.0f, 0.5f) / 0.5f;
-        o.grip[0] = ls * 0.044f; o.grip[1] = ls * -0.044f;
-        o.grip[2] = rs * 0.044f; o.grip[3] = rs * -0.044f;
+        E.row[18] = ls * 0.044f; E.row[19] = ls * -0.044f;
+        E.row[27] = rs * 0.044f; E.row[28] = rs * -0.044f;
     } else {
         const bool lc = la / C.orig < 0.7f, rc = ra / C.orig < 0.7f;
-        o.grip[0] = lc ? 0.0f : 0.044f; o.grip[1] = lc ? 0.0f : -0.044f;
-        o.grip[2] = rc ? 0.0f : 0.044f; o.grip[3] = rc ? 0.0f : -0.044f;
+        E.row[18] = lc ? 0.0f : 0.044f; E.row[19] = lc ? 0.0f : -0.044f;
+        E.row[27] = rc ? 0.0f : 0.044f; E.row[28] = rc ? 0.0f : -0.044f;
     }
-    o.has_grip = true;
+    if (body_rot) {   // body_global_rotation: identity except rows 10, 14, 39 (:116, :172-173)
+        for (int j = 0; j < 59; ++j) st4(body_rot + 4 * j, j == 10 ? R10 : (j == 14 ? WL : (j == 39 ? WR : qident())));
+    }
 }
 
 // HuUpperBodyFromMocapRetarget.retarget_from_global_translation  retarget_solver.py:40-99
-RTG_DEV void solve_upper_body(const SolverConsts &C, const float *__restrict__ x, FrameOut &o)
+RTG_DEV void solve_upper_body(const SolverConsts &C, const float *__restrict__ x, const Emit &E)
 {
     auto pt = [&](int j) {   // coord_transform(dir=[-1,-1,1]) :41
         const V v = ld3(x + 3 * j);
         return V{v.x * -1.0f, v.y * -1.0f, v.z * 1.0f};
     };
-    const V s10 = pt(10);
-    const V Mt[3] = {vsub(pt(17), s10), vsub(pt(13), s10), vsub(pt(11), s10)};
-    const Q R10 = cal_joint_quat<3>(C.Zt, Mt);
-    const V s14 = pt(14), s15 = pt(15), s16 = pt(16), s18 = pt(18), s19 = pt(19), s20 = pt(20);
-    Q pl, rl, pr, rr, y, e;
-    shoulder_pr(vsub(s19, s18), C.lsh, R10, pl, rl);
-    shoulder_pr(vsub(s15, s14), C.rsh, R10, pr, rr);
-    o.l[0] = pl; o.l[1] = rl; o.l[7] = pr; o.l[8] = rr;
-    elbow_py(vsub(s20, s19), C.lel, qmul(qmul(R10, pl), rl), y, e);
-    o.l[2] = y; o.l[3] = e;
-    elbow_py(vsub(s16, s15), C.rel, qmul(qmul(R10, pr), rr), y, e);
-    o.l[9] = y; o.l[10] = e;
-    o.l[4] = o.l[5] = o.l[6] = o.l[11] = o.l[12] = o.l[13] = qident();
-    o.has_grip = false;
-    o.kab[0] = R10;
+    Q R10;
+    {
+        const V s10 = pt(10);
+        const V Mt[3] = {vsub(pt(17), s10), vsub(pt(13), s10), vsub(pt(11), s10)};
+        R10 = cal_joint_quat<3>(C.Zt, Mt);
+    }
+    const V s19 = pt(19), s15 = pt(15);
+    solve_arm<12>(E, vsub(s19, pt(18)), vsub(pt(20), s19), C.lsh, C.lel, R10);
+    solve_arm<21>(E, vsub(s15, pt(14)), vsub(pt(16), s15), C.rsh, C.rel, R10);
+    E.identity<16>(); E.identity<17>(); E.identity<18>();
+    E.identity<25>(); E.identity<26>(); E.identity<27>();
+    E.row[18] = 0.0f; E.row[19] = 0.0f; E.row[27] = 0.0f; E.row[28] = 0.0f;
 }
 
 // VtrdynFullBodyRetargeter.retarget  full_body_retargeter.py:19-177
 RTG_DEV void solve_full_body_rot(const SolverConsts &C, const float *__restrict__ q, const float *__restrict__ b,
-                                 const float *__restrict__ L, const float *__restrict__ R, FrameOut &o)
+                                 const float *__restrict__ L, const float *__restrict__ R, const Emit &E)
 {
     const Q parL = ld4(q + 17 * 4), parR = ld4(q + 13 * 4);
-    const V b14 = ld3(b + 42), b15 = ld3(b + 45), b16 = ld3(b + 48);
-    const V b18 = ld3(b + 54), b19 = ld3(b + 57), b20 = ld3(b + 60);
-    Q p, r, y, e;
-    shoulder_pr(vsub(b19, b18), C.lsh, parL, p, r);
-    elbow_py(vsub(b20, b19), C.lel, qmul(qmul(parL, p), r), y, e);
-    o.l[0] = p; o.l[1] = r; o.l[2] = y; o.l[3] = e;
-    shoulder_pr(vsub(b15, b14), C.rsh, parR, p, r);
-    elbow_py(vsub(b16, b15), C.rel, qmul(qmul(parR, p), r), y, e);
-    o.l[7] = p; o.l[8] = r; o.l[9] = y; o.l[10] = e;
+    const V b19 = ld3(b + 57), b15 = ld3(b + 45);
+    const Q chainL = solve_arm<12>(E, vsub(b19, ld3(b + 54)), vsub(ld3(b + 60), b19), C.lsh, C.lel, parL);
+    const Q chainR = solve_arm<21>(E, vsub(b15, ld3(b + 42)), vsub(ld3(b + 48), b15), C.rsh, C.rel, parR);
     const Q wl = ld4(q + 20 * 4), wr = ld4(q + 16 * 4);
-    Q eul[3];
-    const Q pl = qmul_norm(parL, qmul(qmul(qmul(o.l[0], o.l[1]), o.l[2]), o.l[3]));
-    quat_in_xyz_axis(qmul_norm(qconj(pl), wl), 0, 1, 2, false, eul);
-    o.l[4] = eul[0]; o.l[5] = eul[1]; o.l[6] = eul[2];
-    const Q pr = qmul_norm(parR, qmul(qmul(qmul(o.l[7], o.l[8]), o.l[9]), o.l[10]));
-    quat_in_xyz_axis(qmul_norm(qconj(pr), wr), 0, 1, 2, false, eul);
-    o.l[11] = eul[0]; o.l[12] = eul[1]; o.l[13] = eul[2];
+    emit_euler_xyz<16>(E, qmul_norm(qconj(qmul_norm(parL, chainL)), wl));
+    emit_euler_xyz<25>(E, qmul_norm(qconj(qmul_norm(parR, chainR)), wr));
     // _retarget_gripper :145-177 -- rotates by the wrist quaternion itself (not its inverse)
-    const float hl0 = qrotate(wl, ld3(L)).x, hr0 = qrotate(wr, ld3(R)).x;
-    const float la = mean5(qrotate(wl, ld3(L + 9)).x - hl0, qrotate(wl, ld3(L + 21)).x - hl0,
-                           qrotate(wl, ld3(L + 33)).x - hl0, qrotate(wl, ld3(L + 45)).x - hl0,
-                           qrotate(wl, ld3(L + 57)).x - hl0);
-    const float ra = mean5(qrotate(wr, ld3(R + 9)).x - hr0, qrotate(wr, ld3(R + 21)).x - hr0,
-                           qrotate(wr, ld3(R + 33)).x - hr0, qrotate(wr, ld3(R + 45)).x - hr0,
-                           qrotate(wr, ld3(R + 57)).x - hr0);
-    const bool lc = la / C.orig < 0.7f, rc = ra / C.orig < 0.7f;
-    o.grip[0] = lc ? 0.0f : 0.044f; o.grip[1] = lc ? 0.0f : -0.044f;
-    o.grip[2] = rc ? 0.0f : 0.044f; o.grip[3] = rc ? 0.0f : -0.044f;
-    o.has_grip = true;
+    constexpr int tips[5] = {3, 7, 11, 15, 19};
+    const bool lc = hand_x_mean(wl, L, tips) / C.orig < 0.7f, rc = hand_x_mean(wr, R, tips) / C.orig < 0.7f;
+    E.row[18] = lc ? 0.0f : 0.044f; E.row[19] = lc ? 0.0f : -0.044f;
+    E.row[27] = rc ? 0.0f : 0.044f; E.row[28] = rc ? 0.0f : -0.044f;
 }
 
 // Mocap2HuBodyRetargeter.retarget_from_pose  body_retargeter.py:34-81
-RTG_DEV void solve_body_rot(const SolverConsts &C, const float *__restrict__ g, FrameOut &o)
+RTG_DEV void solve_body_rot(const SolverConsts &C, const float *__restrict__ g, const Emit &E)
 {
     // cal_local_rotation (kinematics.py:41-63) for the four joints used
     auto local = [&](int j, int p) { return qmul_norm(qconj(ld4(g + 4 * p)), ld4(g + 4 * j)); };
-    const Q l18 = local(18, C.par[0]), l14 = local(14, C.par[1]);
-    const Q l19 = local(19, C.par[2]), l15 = local(15, C.par[3]);
-    Q sl[3], sr[3], el[3], er[3];
-    quat_in_xyz_axis(l18, 1, 0, 2, false, sl);   // 'YXZ'
-    quat_in_xyz_axis(l14, 1, 0, 2, false, sr);
-    quat_in_xyz_axis(l19, 2, 1, 0, false, el);   // 'ZYX'
-    quat_in_xyz_axis(l15, 2, 1, 0, false, er);
-    o.l[0] = sl[0]; o.l[1] = sl[1]; o.l[2] = qmul_norm(el[0], sl[2]);
-    o.l[3] = el[1]; o.l[4] = el[2];
-    o.l[7] = sr[0]; o.l[8] = sr[1]; o.l[9] = qmul_norm(er[0], sr[2]);
-    o.l[10] = er[1]; o.l[11] = er[2];
-    o.l[5] = o.l[6] = o.l[12] = o.l[13] = qident();
-    o.has_grip = false;
+#pragma unroll
+    for (int side = 0; side < 2; ++side) {
+        const int sh = side == 0 ? 18 : 14, el = side == 0 ? 19 : 15;
+        Q s3[3], e3[3];
+        quat_in_xyz_axis(local(sh, C.par[side == 0 ? 0 : 1]), 1, 0, 2, false, s3);   // 'YXZ'
+        quat_in_xyz_axis(local(el, C.par[side == 0 ? 2 : 3]), 2, 1, 0, false, e3);   // 'ZYX'
+        if (side == 0) {
+            E.link<12>(s3[0]); E.link<13>(s3[1]); E.link<14>(qmul_norm(e3[0], s3[2]));
+            E.link<15>(e3[1]); E.link<16>(e3[2]);
+        } else {
+            E.link<21>(s3[0]); E.link<22>(s3[1]); E.link<23>(qmul_norm(e3[0], s3[2]));
+            E.link<24>(e3[1]); E.link<25>(e3[2]);
+        }
+    }
+    E.identity<17>(); E.identity<18>(); E.identity<26>(); E.identity<27>();
+    E.row[18] = 0.0f; E.row[19] = 0.0f; E.row[27] = 0.0f; E.row[28] = 0.0f;
 }
 
 // ----------------------------------------------------------------------------
-// solver kernel: body + epilogue (quat_to_dof_pos, outputs)
+// solver kernel: per-frame body + coalesced DOF tile store
 // ----------------------------------------------------------------------------
 constexpr int kSolverBlock = 256;
 constexpr int kDofStride = 31;   // LDS row pitch (dwords): odd -> conflict-free ds_write_b32
@@ -207,49 +239,18 @@ __global__ __launch_bounds__(kSolverBlock) void k_retarget(SolverConsts C, const
     __shared__ float sdof[kSolverBlock * kDofStride];
     const int64_t f0 = (int64_t)blockIdx.x * kSolverBlock;
     const int64_t f = f0 + threadIdx.x;
-    float *row = sdof + threadIdx.x * kDofStride;
     if (f < B) {
-        FrameOut o;
+        const Emit E{sdof + threadIdx.x * kDofStride, local_rot ? local_rot + f * 124 : nullptr};
+        emit_fixed_links(E);
         if (KIND == RTG_SOLVER_FULL_BODY_POS)
-            solve_full_body_pos<PRECISE>(C, in0 + f * 63, in1 + f * 60, in2 + f * 60, o);
+            solve_full_body_pos<PRECISE>(C, in0 + f * 63, in1 + f * 60, in2 + f * 60, E,
+                                         body_rot ? body_rot + f * 236 : nullptr);
         else if (KIND == RTG_SOLVER_UPPER_BODY)
-            solve_upper_body(C, in0 + f * 63, o);
+            solve_upper_body(C, in0 + f * 63, E);
         else if (KIND == RTG_SOLVER_FULL_BODY_ROT)
-            solve_full_body_rot(C, in0 + f * 84, in1 + f * 63, in2 + f * 60, in3 + f * 60, o);
+            solve_full_body_rot(C, in0 + f * 84, in1 + f * 63, in2 + f * 60, in3 + f * 60, E);
         else
-            solve_body_rot(C, in0 + f * 84, o);
-        // quat_to_dof_pos (transform3d.py:176-183): dof k <-> link k+1, component Hu_DOF_AXIS[k]
-#pragma unroll
-        for (int k = 0; k < 11; ++k) row[k] = 0.0f;
-#pragma unroll
-        for (int t = 0; t < 7; ++t) row[11 + t] = qexp_component(o.l[t], hu_dof_axis(11 + t));
-#pragma unroll
-        for (int t = 0; t < 7; ++t) row[20 + t] = qexp_component(o.l[7 + t], hu_dof_axis(20 + t));
-        row[18] = o.has_grip ? o.grip[0] : 0.0f;
-        row[19] = o.has_grip ? o.grip[1] : 0.0f;
-        row[27] = o.has_grip ? o.grip[2] : 0.0f;
-        row[28] = o.has_grip ? o.grip[3] : 0.0f;
-        row[29] = 0.0f;
-        if (local_rot) {
-            float *lr = local_rot + f * 124;
-#pragma unroll
-            for (int j = 0; j < 31; ++j) {
-                Q q = qident();
-                if (j >= 12 && j <= 18) q = o.l[j - 12];
-                if (j >= 21 && j <= 27) q = o.l[j - 14];
-                st4(lr + 4 * j, q);
-            }
-        }
-        if (KIND == RTG_SOLVER_FULL_BODY_POS && body_rot) {
-            float *br = body_rot + f * 236;
-            for (int j = 0; j < 59; ++j) {
-                Q q = qident();
-                if (j == 10) q = o.kab[0];
-                if (j == 14) q = o.kab[1];
-                if (j == 39) q = o.kab[2];
-                st4(br + 4 * j, q);
-            }
-        }
+            solve_body_rot(C, in0 + f * 84, E);
     }
     __syncthreads();
     // coalesced store of the block's contiguous DOF tile: rows [f0, min(B, f0+256)) x 30.
@@ -390,6 +391,8 @@ __global__ __launch_bounds__(256) void k_quat_op(int op, const float *__restrict
         st4(out + 8 * i + 4, e);
         break;
     }
+    case RTG_OP_QUAT_TO_ANGLE_AXIS: st4(out + 4 * i, qangle_axis(ld4(a + 4 * i))); break;
+    case RTG_OP_NORMALIZE_ANGLE: out[i] = g_atan2f(cr_sin(a[i]), cr_cos(a[i])); break;
     default: break;
     }
 }

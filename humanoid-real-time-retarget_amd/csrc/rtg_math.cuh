@@ -193,6 +193,16 @@ RTG_DEV V qexp_map(Q q)
     const float az = mask ? q.z / sin_theta : 1.0f;
     return V{a * ax, a * ay, a * az};
 }
+// quat_to_angle_axis (:587-608) as [angle, axis]
+RTG_DEV Q qangle_axis(Q q)
+{
+    const float sin_theta = cr_sqrt(1.0f - q.w * q.w);
+    float angle = 2.0f * cr_acos(q.w);
+    angle = g_atan2f(cr_sin(angle), cr_cos(angle));
+    const bool mask = fabsf(sin_theta) > 1e-5f;
+    return Q{mask ? angle : 0.0f, mask ? q.x / sin_theta : 0.0f, mask ? q.y / sin_theta : 0.0f,
+             mask ? q.z / sin_theta : 1.0f};
+}
 RTG_DEV float qexp_component(Q q, int k)
 {
     const V e = qexp_map(q);
@@ -276,7 +286,7 @@ RTG_DEV void jacobi_eig3(double S[3][3], double Vm[3][3])
     }
 }
 
-RTG_DEV void kabsch_rot(const float A[9], float R[9])
+RTG_DEV void kabsch_rot_jacobi(const float A[9], float R[9])
 {
     double a[3][3], S[3][3], Vm[3][3];
 #pragma unroll
@@ -323,6 +333,101 @@ RTG_DEV void kabsch_rot(const float A[9], float R[9])
     for (int i = 0; i < 3; ++i)
 #pragma unroll
         for (int j = 0; j < 3; ++j) R[i * 3 + j] = (float)(u1[i] * v1[j] + u2[i] * v2[j] + u3[i] * v3[j]);
+}
+
+// 4x4 adjugate (and determinant) by 2x2 sub-determinants; m row-major
+RTG_DEV double adj4(const double m[16], double inv[16], bool want_adj)
+{
+    const double s0 = m[0] * m[5] - m[4] * m[1], s1 = m[0] * m[6] - m[4] * m[2];
+    const double s2 = m[0] * m[7] - m[4] * m[3], s3 = m[1] * m[6] - m[5] * m[2];
+    const double s4 = m[1] * m[7] - m[5] * m[3], s5 = m[2] * m[7] - m[6] * m[3];
+    const double c5 = m[10] * m[15] - m[14] * m[11], c4 = m[9] * m[15] - m[13] * m[11];
+    const double c3 = m[9] * m[14] - m[13] * m[10], c2 = m[8] * m[15] - m[12] * m[11];
+    const double c1 = m[8] * m[14] - m[12] * m[10], c0 = m[8] * m[13] - m[12] * m[9];
+    if (want_adj) {
+        inv[0] = m[5] * c5 - m[6] * c4 + m[7] * c3;
+        inv[1] = -m[1] * c5 + m[2] * c4 - m[3] * c3;
+        inv[2] = m[13] * s5 - m[14] * s4 + m[15] * s3;
+        inv[3] = -m[9] * s5 + m[10] * s4 - m[11] * s3;
+        inv[4] = -m[4] * c5 + m[6] * c2 - m[7] * c1;
+        inv[5] = m[0] * c5 - m[2] * c2 + m[3] * c1;
+        inv[6] = -m[12] * s5 + m[14] * s2 - m[15] * s1;
+        inv[7] = m[8] * s5 - m[10] * s2 + m[11] * s1;
+        inv[8] = m[4] * c4 - m[5] * c2 + m[7] * c0;
+        inv[9] = -m[0] * c4 + m[1] * c2 - m[3] * c0;
+        inv[10] = m[12] * s4 - m[13] * s2 + m[15] * s0;
+        inv[11] = -m[8] * s4 + m[9] * s2 - m[11] * s0;
+        inv[12] = -m[4] * c3 + m[5] * c1 - m[6] * c0;
+        inv[13] = m[0] * c3 - m[1] * c1 + m[2] * c0;
+        inv[14] = -m[12] * s3 + m[13] * s1 - m[14] * s0;
+        inv[15] = m[8] * s3 - m[9] * s1 + m[10] * s0;
+    }
+    return s0 * c5 - s1 * c4 + s2 * c3 + s3 * c2 - s4 * c1 + s5 * c0;
+}
+
+// Kabsch rotation, fast path: Horn's quaternion form of the same problem
+// (max tr(R^T A) over proper rotations == the det-fixed SVD solution).  The
+// largest eigenvalue of the 4x4 key matrix N of S = A^T comes from Newton on
+// its characteristic quartic started above the root at sqrt(3)|S|_F (QCP);
+// the quaternion is the largest-diagonal column of adj(N - lambda I).  A
+// (nearly) degenerate top eigenvalue -- a reflection fit with sigma2 ~ sigma3,
+// ill-posed for any method -- falls back to the Jacobi polar factor.
+RTG_DEV void kabsch_rot(const float A[9], float R[9])
+{
+    const double Sxx = A[0], Sxy = A[3], Sxz = A[6], Syx = A[1], Syy = A[4], Syz = A[7], Szx = A[2], Szy = A[5],
+                 Szz = A[8];
+    const double F2 = Sxx * Sxx + Sxy * Sxy + Sxz * Sxz + Syx * Syx + Syy * Syy + Syz * Syz + Szx * Szx +
+                      Szy * Szy + Szz * Szz;
+    if (F2 == 0.0) {   // all-zero fit: the reference's SVD gives U = V = I
+#pragma unroll
+        for (int i = 0; i < 9; ++i) R[i] = (i % 4 == 0) ? 1.0f : 0.0f;
+        return;
+    }
+    double N[16] = {Sxx + Syy + Szz, Syz - Szy, Szx - Sxz, Sxy - Syx,
+                    Syz - Szy, Sxx - Syy - Szz, Sxy + Syx, Szx + Sxz,
+                    Szx - Sxz, Sxy + Syx, -Sxx + Syy - Szz, Syz + Szy,
+                    Sxy - Syx, Szx + Sxz, Syz + Szy, -Sxx - Syy + Szz};
+    const double detS = Sxx * (Syy * Szz - Syz * Szy) - Sxy * (Syx * Szz - Syz * Szx) + Sxz * (Syx * Szy - Syy * Szx);
+    double scratch[16];
+    const double c0 = adj4(N, scratch, false);
+    const double c2 = -2.0 * F2, c1 = -8.0 * detS;
+    double lam = sqrt(3.0 * F2);
+    int it = 0;
+    for (; it < 50; ++it) {
+        const double P = ((lam * lam + c2) * lam + c1) * lam + c0;
+        const double dP = (4.0 * lam * lam + 2.0 * c2) * lam + c1;
+        const double d = P / dP;
+        lam -= d;
+        if (fabs(d) <= 1e-13 * fabs(lam)) break;
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i) N[i * 5] -= lam;
+    double adj[16];
+    adj4(N, adj, true);
+    int k = 0;
+    double best = fabs(adj[0]);
+    if (fabs(adj[5]) > best) { best = fabs(adj[5]); k = 1; }
+    if (fabs(adj[10]) > best) { best = fabs(adj[10]); k = 2; }
+    if (fabs(adj[15]) > best) { best = fabs(adj[15]); k = 3; }
+    if (it >= 16 || best <= 1e-6 * F2 * sqrt(F2)) {
+        kabsch_rot_jacobi(A, R);
+        return;
+    }
+    double q[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+        q[r] = k == 0 ? adj[r * 4] : (k == 1 ? adj[r * 4 + 1] : (k == 2 ? adj[r * 4 + 2] : adj[r * 4 + 3]));
+    const double qn = sqrt(q[0] * q[0] + q[1] * q[1] + q[2] * q[2] + q[3] * q[3]);
+    const double w = q[0] / qn, x = q[1] / qn, y = q[2] / qn, z = q[3] / qn;
+    R[0] = (float)(1.0 - 2.0 * (y * y + z * z));
+    R[1] = (float)(2.0 * (x * y - w * z));
+    R[2] = (float)(2.0 * (x * z + w * y));
+    R[3] = (float)(2.0 * (x * y + w * z));
+    R[4] = (float)(1.0 - 2.0 * (x * x + z * z));
+    R[5] = (float)(2.0 * (y * z - w * x));
+    R[6] = (float)(2.0 * (x * z - w * y));
+    R[7] = (float)(2.0 * (y * z + w * x));
+    R[8] = (float)(1.0 - 2.0 * (x * x + y * y));
 }
 
 // cal_joint_quat (transform3d.py:31-50): A = M^T Z by einsum (sequential in j, no FMA)

@@ -36,6 +36,8 @@ OP_PROJ_IN_PLANE = 9
 OP_QUAT_TO_DOF_POS = 10
 OP_SHOULDER_PR = 11
 OP_ELBOW_PY = 12
+OP_QUAT_TO_ANGLE_AXIS = 13
+OP_NORMALIZE_ANGLE = 14
 
 MAX_SEGMENTS = 8
 

@@ -96,6 +96,20 @@ def quat_to_exp_map(q):
     return _quat_op(_lib.OP_QUAT_TO_EXP_MAP, q, out_tail=3)
 
 
+def quat_to_angle_axis(q):
+    """rotation3d.py:587-608 -> (angle (...), axis (...,3))"""
+    r = _quat_op(_lib.OP_QUAT_TO_ANGLE_AXIS, q, out_tail=4)
+    return r[..., 0], r[..., 1:]
+
+
+def normalize_angle(x):
+    """rotation3d.py:582-584 (atan2 with glibc atan2f semantics: the reference's <32-element path)"""
+    x = dev_f32(x)
+    out = torch.empty_like(x)
+    check(lib().rtg_quat_op_f32(_lib.OP_NORMALIZE_ANGLE, ptr(x), None, None, x.numel(), ptr(out), stream_handle()))
+    return out
+
+
 def radians_between_vecs(v1, v2, n):
     """transform3d.py:77-100, batched over leading dims"""
     v1, v2, n = dev_f32(v1), dev_f32(v2), dev_f32(n)

@@ -143,7 +143,9 @@ typedef enum rtg_quat_op {
     RTG_OP_PROJ_IN_PLANE = 9,       /* v (n,3), n (n,3) -> (n,3)   transform3d.py:61-75 */
     RTG_OP_QUAT_TO_DOF_POS = 10,    /* local_rot (n,31,4) -> dof (n,30)  transform3d.py:176-183 (Hu) */
     RTG_OP_SHOULDER_PR = 11,        /* v1 (n,3), v0 (n,3), parent c (n,4) -> (n,2,4)  full_body_pos_retargeter.py:246-278 */
-    RTG_OP_ELBOW_PY = 12            /* v1, v0, parent -> (n,2,4)   full_body_pos_retargeter.py:220-243 */
+    RTG_OP_ELBOW_PY = 12,           /* v1, v0, parent -> (n,2,4)   full_body_pos_retargeter.py:220-243 */
+    RTG_OP_QUAT_TO_ANGLE_AXIS = 13, /* q (n,4) -> (n,4) = [angle, axis xyz]  rotation3d.py:587-608 */
+    RTG_OP_NORMALIZE_ANGLE = 14     /* x (n) -> (n) atan2(sin x, cos x)      rotation3d.py:582-584 */
 } rtg_quat_op;
 int rtg_quat_op_f32(int op, const float *a, const float *b, const float *c, int64_t n, float *out,
                     rtg_stream_t stream);

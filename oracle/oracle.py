@@ -197,6 +197,15 @@ def kabsch_rotmat(A):
     return out.reshape(-1, 3, 3)
 
 
+def kabsch_rotmat_horn(A):
+    """Cross-check of the device formulation (Horn/QCP) -- not used by the oracle solvers."""
+    A = _c32(np.reshape(A, (-1, 9)))
+    out = np.empty_like(A)
+    it = np.empty(len(A), np.int32)
+    lib().oracle_kabsch_rotmat_horn(_fp(A), _i64(len(A)), _fp(out), it.ctypes.data_as(_i))
+    return out.reshape(-1, 3, 3), it
+
+
 def quat_in_xyz_axis(q, seq):
     q = _c32(q)
     out = np.empty((len(q), 3, 4), np.float32)

@@ -1,0 +1,126 @@
+"""Secondary measurements (not the driver's bench line):
+
+  latency  -- batch-1 / small-batch retarget latency (teleop path, SURVEY §7 "Latency path"):
+              kernel-only (HIP events) and end-to-end host->device->host wall time
+  fk       -- FK throughput: Hu (B=262144) and the mixed 4-topology config (4 x 65536, one launch)
+  solvers  -- throughput of all four solver kinds at B=262144
+"""
+from __future__ import annotations
+
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(REPO, "humanoid-real-time-retarget_amd"))
+
+from rtg import _lib, assets, ops, synth  # noqa: E402
+from rtg.runtime import Solver, Topology  # noqa: E402
+
+G = os.path.join(REPO, "tests", "golden")
+
+
+def topo(name):
+    return Topology(assets.parents(name), assets.local_translation(name), assets.tree_quat(name))
+
+
+def time_events(fn, reps=50, warm=5):
+    for _ in range(warm):
+        fn()
+    torch.cuda.synchronize()
+    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    s.record()
+    for _ in range(reps):
+        fn()
+    e.record()
+    e.synchronize()
+    return s.elapsed_time(e) / reps
+
+
+def latency():
+    zp = np.load(os.path.join(G, "zero_pose.npz"))
+    g = np.load(os.path.join(G, "full_body_pos_precise.npz"))
+    S = Solver(_lib.SOLVER_FULL_BODY_POS, zp["vtrdyn_full_local_t"], zp["vtrdyn_full_global_t"],
+               assets.parents("vtrdyn_full"), True)
+    out = {}
+    for B in (1, 16, 256, 4096):
+        idx = np.arange(B) % len(g["body"])
+        hb, hl, hr = (np.ascontiguousarray(g[k][idx]) for k in ("body", "lh", "rh"))
+        db, dl, dr = (torch.from_numpy(a).cuda() for a in (hb, hl, hr))
+        dof = torch.empty((B, 30), device="cuda")
+        k_ms = time_events(lambda: S.retarget([db, dl, dr], out_dof=dof))
+        pb, pl, pr = (torch.from_numpy(a).pin_memory() for a in (hb, hl, hr))
+        hdof = torch.empty((B, 30)).pin_memory()
+
+        def e2e():
+            db.copy_(pb, non_blocking=True); dl.copy_(pl, non_blocking=True); dr.copy_(pr, non_blocking=True)
+            S.retarget([db, dl, dr], out_dof=dof)
+            hdof.copy_(dof, non_blocking=True)
+            torch.cuda.current_stream().synchronize()
+        for _ in range(10):
+            e2e()
+        ts = []
+        for _ in range(200):
+            t0 = time.perf_counter()
+            e2e()
+            ts.append(time.perf_counter() - t0)
+        out[str(B)] = {"kernel_us": k_ms * 1e3, "e2e_median_us": float(np.median(ts) * 1e6),
+                       "e2e_p99_us": float(np.quantile(ts, 0.99) * 1e6)}
+    return out
+
+
+def fk():
+    res = {}
+    B = 262144
+    T = topo("hu_v5")
+    lr = torch.from_numpy(synth.random_local_quats(B, 31, 5)).cuda()
+    rt = torch.zeros((B, 3), device="cuda")
+    ms = time_events(lambda: ops.forward_kinematics(T, lr, rt))
+    res["hu_fk_262144"] = {"ms": ms, "frames_per_s": B / (ms * 1e-3),
+                           "GBs_algorithmic": 1376 * B / (ms * 1e-3) / 1e9}
+    segs = []
+    nbytes = 0
+    for i, n in enumerate(["hu_v5", "vtrdyn", "vtrdyn_full", "noitom"]):
+        t = topo(n)
+        J = t.num_joints
+        segs.append((t, torch.from_numpy(synth.random_local_quats(65536, J, 10 + i)).cuda(),
+                     torch.zeros((65536, 3), device="cuda")))
+        nbytes += 65536 * (J * 16 + 12 + J * 28)
+    ms = time_events(lambda: ops.forward_kinematics_multi(segs))
+    res["mixed_4x65536"] = {"ms": ms, "frames_per_s": 4 * 65536 / (ms * 1e-3), "GBs_algorithmic": nbytes / (ms * 1e-3) / 1e9}
+    return res
+
+
+def solvers():
+    zp = np.load(os.path.join(G, "zero_pose.npz"))
+    B = 262144
+    res = {}
+    Tf = topo("vtrdyn_full")
+    body, lh, rh, brot = ops.synth_full_body(Tf, B, seed=7, want_rot=True)
+    x = torch.from_numpy(synth.synth_upper_body_inputs(4096, 3)).cuda().repeat(64, 1, 1).contiguous()
+    g21 = torch.from_numpy(synth.synth_body21_pose(4096, 4)[1]).cuda().repeat(64, 1, 1).contiguous()
+    cfg = {
+        "full_body_pos": (Solver(_lib.SOLVER_FULL_BODY_POS, zp["vtrdyn_full_local_t"], zp["vtrdyn_full_global_t"],
+                                 assets.parents("vtrdyn_full"), True), [body, lh, rh]),
+        "upper_body": (Solver(_lib.SOLVER_UPPER_BODY, zp["vtrdyn_local_t"], zp["vtrdyn_global_t"],
+                              assets.parents("vtrdyn")), [x]),
+        "full_body_rot": (Solver(_lib.SOLVER_FULL_BODY_ROT, zp["vtrdyn_full_local_t"], zp["vtrdyn_full_global_t"],
+                                 assets.parents("vtrdyn_full")), [brot, body, lh, rh]),
+        "body_rot": (Solver(_lib.SOLVER_BODY_ROT, zp["vtrdyn_local_t"], zp["vtrdyn_global_t"],
+                            assets.parents("vtrdyn")), [g21]),
+    }
+    for k, (S, ins) in cfg.items():
+        dof = torch.empty((B, 30), device="cuda")
+        ms = time_events(lambda: S.retarget(ins, out_dof=dof))
+        res[k] = {"ms": ms, "frames_per_s": B / (ms * 1e-3)}
+    return res
+
+
+if __name__ == "__main__":
+    modes = sys.argv[1:] or ["latency", "fk", "solvers"]
+    out = {m: globals()[m]() for m in modes}
+    print(json.dumps(out, indent=1))
