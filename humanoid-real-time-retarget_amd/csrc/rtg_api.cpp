@@ -303,12 +303,13 @@ int rtg_retarget_f32(rtg_solver_t s, const float *in0, const float *in1, const f
 int rtg_quat_op_f32(int op, const float *a, const float *b, const float *c, int64_t n, float *out,
                     rtg_stream_t stream)
 {
-    if (op < RTG_OP_QUAT_MUL || op > RTG_OP_NORMALIZE_ANGLE) return fail(RTG_ERR_INVALID_ARGUMENT, "rtg_quat_op_f32: bad op %d", op);
+    if (op < RTG_OP_QUAT_MUL || op > RTG_OP_QUAT_ANGLE_AXIS) return fail(RTG_ERR_INVALID_ARGUMENT, "rtg_quat_op_f32: bad op %d", op);
     if (n < 0) return fail(RTG_ERR_INVALID_ARGUMENT, "rtg_quat_op_f32: negative n");
     if (n == 0) return RTG_OK;
     const bool needs_b = !(op == RTG_OP_QUAT_NORMALIZE || op == RTG_OP_QUAT_INVERSE || op == RTG_OP_QUAT_FROM_ROTMAT ||
                            op == RTG_OP_QUAT_TO_EXP_MAP || op == RTG_OP_QUAT_TO_DOF_POS ||
-                           op == RTG_OP_QUAT_TO_ANGLE_AXIS || op == RTG_OP_NORMALIZE_ANGLE);
+                           op == RTG_OP_QUAT_TO_ANGLE_AXIS || op == RTG_OP_NORMALIZE_ANGLE ||
+                           op == RTG_OP_QUAT_ABS || op == RTG_OP_QUAT_UNIT || op == RTG_OP_QUAT_ANGLE_AXIS);
     const bool needs_c = op == RTG_OP_RADIANS_BETWEEN || op == RTG_OP_SHOULDER_PR || op == RTG_OP_ELBOW_PY;
     if (!a || !out || (needs_b && !b) || (needs_c && !c))
         return fail(RTG_ERR_INVALID_ARGUMENT, "rtg_quat_op_f32: NULL operand for op %d", op);
@@ -341,6 +342,44 @@ int rtg_quat_in_xyz_axis_f32(const float *q, const char *seq, int64_t n, float *
     if (n == 0) return RTG_OK;
     if (!q || !out) return fail(RTG_ERR_INVALID_ARGUMENT, "rtg_quat_in_xyz_axis_f32: NULL buffer");
     RTG_TRY(launch_quat_in_xyz_axis(q, ax[0], ax[1], ax[2], lower[0], n, out, as_stream(stream)), "k_quat_in_xyz_axis");
+    return RTG_OK;
+}
+
+// ---------------------------------------------------------------- motion velocities
+static int make_taps(const double *w, int32_t radius, GaussTaps *taps, const char *fn)
+{
+    if (!w) return RTG_OK;
+    if (radius < 0 || radius > RTG_MAX_FILTER_RADIUS)
+        return fail(RTG_ERR_UNSUPPORTED, "%s: filter radius %d (max %d)", fn, radius, RTG_MAX_FILTER_RADIUS);
+    taps->radius = radius;
+    for (int i = 0; i < 2 * radius + 1; ++i) taps->w[i] = w[i];
+    return RTG_OK;
+}
+
+int rtg_linear_velocity_f32(const float *p, int64_t nseq, int64_t L, int64_t S, float dt, const double *w,
+                            int32_t radius, float *tmp, float *out, rtg_stream_t stream)
+{
+    if (nseq < 0 || L < 0 || S < 0) return fail(RTG_ERR_INVALID_ARGUMENT, "rtg_linear_velocity_f32: negative shape");
+    if (nseq * L * S == 0) return RTG_OK;
+    if (L < 2) return fail(RTG_ERR_INVALID_ARGUMENT, "rtg_linear_velocity_f32: np.gradient needs >= 2 frames");
+    if (!p || !out || (w && !tmp)) return fail(RTG_ERR_INVALID_ARGUMENT, "rtg_linear_velocity_f32: NULL buffer");
+    GaussTaps taps{};
+    int rc = make_taps(w, radius, &taps, "rtg_linear_velocity_f32");
+    if (rc != RTG_OK) return rc;
+    RTG_TRY(launch_linear_velocity(p, nseq, L, S, dt, w ? &taps : nullptr, tmp, out, as_stream(stream)), "k_gradient_dt");
+    return RTG_OK;
+}
+
+int rtg_angular_velocity_f32(const float *r, int64_t nseq, int64_t L, int64_t J, float dt, const double *w,
+                             int32_t radius, float *tmp, float *out, rtg_stream_t stream)
+{
+    if (nseq < 0 || L < 0 || J < 0) return fail(RTG_ERR_INVALID_ARGUMENT, "rtg_angular_velocity_f32: negative shape");
+    if (nseq * L * J == 0) return RTG_OK;
+    if (!r || !out || (w && !tmp)) return fail(RTG_ERR_INVALID_ARGUMENT, "rtg_angular_velocity_f32: NULL buffer");
+    GaussTaps taps{};
+    int rc = make_taps(w, radius, &taps, "rtg_angular_velocity_f32");
+    if (rc != RTG_OK) return rc;
+    RTG_TRY(launch_angular_velocity(r, nseq, L, J, dt, w ? &taps : nullptr, tmp, out, as_stream(stream)), "k_angular_raw");
     return RTG_OK;
 }
 

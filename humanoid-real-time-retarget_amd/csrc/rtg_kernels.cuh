@@ -51,6 +51,14 @@ hipError_t launch_quat_op(int op, const float *a, const float *b, const float *c
 hipError_t launch_cal_joint_quat(const float *Z, const float *M, int npts, int64_t n, float *out, hipStream_t s);
 hipError_t launch_quat_in_xyz_axis(const float *q, int s0, int s1, int s2, int extrinsic, int64_t n, float *out,
                                    hipStream_t s);
+struct GaussTaps {
+    double w[2 * RTG_MAX_FILTER_RADIUS + 1];
+    int32_t radius;
+};
+hipError_t launch_linear_velocity(const float *p, int64_t nseq, int64_t L, int64_t S, float dt, const GaussTaps *taps,
+                                  float *tmp, float *out, hipStream_t s);
+hipError_t launch_angular_velocity(const float *r, int64_t nseq, int64_t L, int64_t J, float dt,
+                                   const GaussTaps *taps, float *tmp, float *out, hipStream_t s);
 hipError_t launch_synth_full_body(const TopoView &T, uint64_t seed, int64_t off, int64_t B, float *body, float *lh,
                                   float *rh, float *body_rot, hipStream_t s);
 

@@ -393,6 +393,9 @@ __global__ __launch_bounds__(256) void k_quat_op(int op, const float *__restrict
     }
     case RTG_OP_QUAT_TO_ANGLE_AXIS: st4(out + 4 * i, qangle_axis(ld4(a + 4 * i))); break;
     case RTG_OP_NORMALIZE_ANGLE: out[i] = g_atan2f(cr_sin(a[i]), cr_cos(a[i])); break;
+    case RTG_OP_QUAT_ABS: out[i] = qabs(ld4(a + 4 * i)); break;
+    case RTG_OP_QUAT_UNIT: st4(out + 4 * i, qunit(ld4(a + 4 * i))); break;
+    case RTG_OP_QUAT_ANGLE_AXIS: st4(out + 4 * i, qangle_axis_abs(ld4(a + 4 * i))); break;
     default: break;
     }
 }
@@ -421,6 +424,77 @@ __global__ __launch_bounds__(256) void k_quat_in_xyz_axis(const float *__restric
     quat_in_xyz_axis(ld4(q + 4 * i), s0, s1, s2, extrinsic != 0, e);
 #pragma unroll
     for (int t = 0; t < 3; ++t) st4(out + (i * 3 + t) * 4, e[t]);
+}
+
+// ----------------------------------------------------------------------------
+// motion velocities: thread per (sequence, frame, channel), channel fastest
+// (coalesced over the J*C channels of a frame).
+// ----------------------------------------------------------------------------
+// np.gradient along frames (edge_order 1, unit spacing) then / dt, all float32
+__global__ __launch_bounds__(256) void k_gradient_dt(const float *__restrict__ p, int64_t nseq, int64_t L, int64_t S,
+                                                     float dt, float *__restrict__ v)
+{
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= nseq * L * S) return;
+    const int64_t s = i % S, t = (i / S) % L, base = i - s - t * S;
+    float g;
+    if (L == 1) g = 0.0f;   // numpy raises for < 2 frames; rtg_* rejects L < 2 before launch
+    else if (t == 0) g = (p[base + S + s] - p[base + s]) / 1.0f;
+    else if (t == L - 1) g = (p[base + t * S + s] - p[base + (t - 1) * S + s]) / 1.0f;
+    else g = (p[base + (t + 1) * S + s] - p[base + (t - 1) * S + s]) / 2.0f;
+    v[i] = g / dt;
+}
+
+// quat_mul_norm(r[t+1], quat_inverse(r[t])) -> quat_angle_axis -> axis * angle / dt (last frame: identity -> 0)
+__global__ __launch_bounds__(256) void k_angular_raw(const float *__restrict__ r, int64_t nseq, int64_t L, int64_t J,
+                                                     float dt, float *__restrict__ v)
+{
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= nseq * L * J) return;
+    const int64_t t = (i / J) % L;
+    Q d = qident();
+    if (t < L - 1) d = qmul_norm(ld4(r + 4 * (i + J)), qconj(ld4(r + 4 * i)));
+    const Q aa = qangle_axis_abs(d);
+    v[3 * i + 0] = (aa.y * aa.x) / dt;
+    v[3 * i + 1] = (aa.z * aa.x) / dt;
+    v[3 * i + 2] = (aa.w * aa.x) / dt;
+}
+
+// scipy.ndimage.gaussian_filter1d(mode='nearest') along frames: symmetric correlate1d,
+// float64 accumulation from the outermost tap pair inwards, rounded to float32 once
+__global__ __launch_bounds__(256) void k_gauss_nearest(const float *__restrict__ v, int64_t nseq, int64_t L, int64_t S,
+                                                       GaussTaps taps, float *__restrict__ out)
+{
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= nseq * L * S) return;
+    const int64_t s = i % S, t = (i / S) % L, base = i - s - t * S;
+    const int R = taps.radius;
+    auto at = [&](int64_t tt) { tt = tt < 0 ? 0 : (tt > L - 1 ? L - 1 : tt); return (double)v[base + tt * S + s]; };
+    double acc = at(t) * taps.w[R];
+    for (int jj = -R; jj < 0; ++jj) acc += (at(t + jj) + at(t - jj)) * taps.w[R + jj];
+    out[i] = (float)acc;
+}
+
+hipError_t launch_linear_velocity(const float *p, int64_t nseq, int64_t L, int64_t S, float dt, const GaussTaps *taps,
+                                  float *tmp, float *out, hipStream_t s)
+{
+    const int64_t n = nseq * L * S;
+    const unsigned g = (unsigned)((n + 255) / 256);
+    hipLaunchKernelGGL(k_gradient_dt, dim3(g), dim3(256), 0, s, p, nseq, L, S, dt, taps ? tmp : out);
+    if (taps) hipLaunchKernelGGL(k_gauss_nearest, dim3(g), dim3(256), 0, s, tmp, nseq, L, S, *taps, out);
+    return hipGetLastError();
+}
+
+hipError_t launch_angular_velocity(const float *r, int64_t nseq, int64_t L, int64_t J, float dt,
+                                   const GaussTaps *taps, float *tmp, float *out, hipStream_t s)
+{
+    const int64_t n = nseq * L * J;
+    hipLaunchKernelGGL(k_angular_raw, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, r, nseq, L, J, dt,
+                       taps ? tmp : out);
+    if (taps)
+        hipLaunchKernelGGL(k_gauss_nearest, dim3((unsigned)((3 * n + 255) / 256)), dim3(256), 0, s, tmp, nseq, L,
+                           3 * J, *taps, out);
+    return hipGetLastError();
 }
 
 // ----------------------------------------------------------------------------

@@ -133,6 +133,19 @@ RTG_DEV Q qnormalize(Q q)  // quat_unit(quat_pos(q)) :30-56,92-98
     return Q{q.x / n, q.y / n, q.z / n, q.w / n};
 }
 RTG_DEV Q qmul_norm(Q a, Q b) { return qnormalize(qmul(a, b)); }
+RTG_DEV float qabs(Q q) { return cr_sqrt(((q.x * q.x + q.y * q.y) + q.z * q.z) + q.w * q.w); }   // :41-47
+RTG_DEV Q qunit(Q q)                                                                                 // :50-56
+{
+    const float n = clamp_lo(qabs(q), 1e-9f);
+    return Q{q.x / n, q.y / n, q.z / n, q.w / n};
+}
+// quat_angle_axis (:230-240): angle = acos(clamp(2 w^2 - 1)), axis = xyz / max(|xyz|, 1e-9)
+RTG_DEV Q qangle_axis_abs(Q q)
+{
+    const float s = clamp_lohi(2.0f * (q.w * q.w) - 1.0f, -1.0f, 1.0f);
+    const float n = clamp_lo(cr_sqrt((q.x * q.x + q.y * q.y) + q.z * q.z), 1e-9f);
+    return Q{cr_acos(s), q.x / n, q.y / n, q.z / n};
+}
 
 RTG_DEV V qrotate(Q q, V v)  // :205-211, two Hamilton products
 {

@@ -1,0 +1,91 @@
+"""``BaseHumanoidRetargeter`` (retarget/retarget_solver/base_retargeter.py:15-58) on the MI355X.
+
+Keeps the reference's per-frame accumulation API (``_motion_local_rotation`` /
+``_motion_dof_pos`` lists, ``motion_*`` properties, FK cached until the length
+changes) and adds batched solving: every solver runs through one
+``rtg_retarget_f32`` launch whether it is handed one frame or millions.
+"""
+from __future__ import annotations
+
+from abc import ABC
+from typing import Optional, Sequence
+
+import torch
+
+from robot_kinematics_model import RobotZeroPose, cal_forward_kinematics
+from rtg import _lib
+from rtg.bridge import as_tensor, back, home_device
+from rtg.runtime import Solver, dev_f32
+
+
+class BaseHumanoidRetargeter(ABC):
+    #: rtg_solver_kind of the subclass
+    SOLVER_KIND: Optional[int] = None
+
+    def __init__(self, source_zero_pose: RobotZeroPose, target_zero_pose: RobotZeroPose, precise_gripper=False):
+        self.source_zero_pose = source_zero_pose
+        self.target_zero_pose = target_zero_pose
+        self._motion_local_rotation = []
+        self._motion_dof_pos = []
+        self._solver = None
+        self._precise = bool(precise_gripper)
+
+    # -- device solver (built lazily so construction works before a GPU is touched)
+    @property
+    def solver(self) -> Solver:
+        if self._solver is None:
+            if self.target_zero_pose.num_joints != 31:
+                raise ValueError("the retarget solvers target the 31-link Hu v5 robot "
+                                 f"(got {self.target_zero_pose.num_joints} links)")
+            self._solver = Solver(self.SOLVER_KIND, self.source_zero_pose.local_translation,
+                                  self.source_zero_pose.global_translation, self.source_zero_pose.parent_indices,
+                                  self._precise)
+        return self._solver
+
+    def _solve(self, inputs: Sequence, batched: bool, want_body_rot=False):
+        """Run the device solver on (B, ...) or single-frame inputs; returns (local_rot, dof, body_rot)."""
+        dev = home_device(*inputs)
+        tails = [tuple(as_tensor(x).shape[-2:]) for x in inputs]
+        xs = [dev_f32(as_tensor(x).reshape(-1, *t)) for x, t in zip(inputs, tails)]
+        dof, lr, br = self.solver.retarget(xs, want_local_rot=True, want_body_rot=want_body_rot)
+        if not batched:
+            dof, lr = dof[0], lr[0]
+            br = br[0] if br is not None else None
+        return back(lr, dev), back(dof, dev), (back(br, dev) if br is not None else None)
+
+    def _record(self, local_rot, dof):
+        self._motion_local_rotation.append(local_rot)
+        self._motion_dof_pos.append(dof)
+
+    # -- accumulated motion (base_retargeter.py:22-58)
+    @property
+    def motion_local_rotation(self):
+        return torch.cat([x.reshape(-1, *x.shape[-2:]) for x in self._motion_local_rotation]).clone()
+
+    @property
+    def motion_dof_pos(self):
+        return torch.cat([x.reshape(-1, x.shape[-1]) for x in self._motion_dof_pos]).clone()
+
+    @property
+    def motion_length(self):
+        return sum(1 if x.dim() == 2 else x.shape[0] for x in self._motion_local_rotation)
+
+    def _fk(self):
+        lr = self.motion_local_rotation
+        self._motion_global_rotation, self._motion_global_translation = cal_forward_kinematics(
+            motion_local_rotation=lr, motion_root_translation=torch.zeros((self.motion_length, 3), device=lr.device),
+            parent_indices=self.target_zero_pose.parent_indices,
+            zero_pose_local_translation=self.target_zero_pose.local_translation)
+
+    @property
+    def motion_global_rotation(self):
+        if not (hasattr(self, "_motion_global_rotation") and len(self._motion_global_rotation) == self.motion_length):
+            self._fk()
+        return self._motion_global_rotation.clone()
+
+    @property
+    def motion_global_translation(self):
+        if not (hasattr(self, "_motion_global_translation")
+                and len(self._motion_global_translation) == self.motion_length):
+            self._fk()
+        return self._motion_global_translation.clone()

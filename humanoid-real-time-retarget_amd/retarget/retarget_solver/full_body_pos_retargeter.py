@@ -1,0 +1,51 @@
+"""``VtrdynFullBodyPosRetargeter`` (retarget/retarget_solver/full_body_pos_retargeter.py:17-217).
+
+Positions-only full-body solver (the live teleop path, sim_full_body_teleop.py:115-119):
+torso Kabsch fit, shoulder pitch/roll + shoulder yaw/elbow pitch plane
+decompositions, wrist Kabsch fits split into XYZ Euler single-axis rotations,
+finger-spread gripper -- one frame per GPU lane (``RTG_SOLVER_FULL_BODY_POS``).
+"""
+from __future__ import annotations
+
+from rtg import _lib, ops
+from rtg.bridge import as_tensor, back, home_device
+
+from retarget.retarget_solver.base_retargeter import BaseHumanoidRetargeter
+
+
+class VtrdynFullBodyPosRetargeter(BaseHumanoidRetargeter):
+    SOLVER_KIND = _lib.SOLVER_FULL_BODY_POS
+
+    def __init__(self, mocap_zero_pose, target_zero_pose, precise_gripper=False):
+        super().__init__(mocap_zero_pose, target_zero_pose, precise_gripper)
+        self.precise_gripper = precise_gripper
+
+    def retarget(self, body_global_translation, left_hand_global_translation, right_hand_global_translation):
+        """One frame: body (21,3), hands (20,3) -> (local_rot (31,4), dof (30,), body_global_rotation (59,4))."""
+        lr, dof, br = self._solve([body_global_translation, left_hand_global_translation,
+                                   right_hand_global_translation], batched=False, want_body_rot=True)
+        self._record(lr, dof)
+        return lr, dof, br
+
+    def retarget_batch(self, body_global_translation, left_hand_global_translation, right_hand_global_translation,
+                       record=False, want_body_rot=False):
+        """B frames: (B,21,3), (B,20,3), (B,20,3) -> (local_rot (B,31,4), dof (B,30), body_rot (B,59,4) | None)."""
+        lr, dof, br = self._solve([body_global_translation, left_hand_global_translation,
+                                   right_hand_global_translation], batched=True, want_body_rot=want_body_rot)
+        if record:
+            self._record(lr, dof)
+        return lr, dof, br
+
+
+def cal_elbowP_and_shoulderY(v1, v0, parent_global_rotation):
+    """:220-243 -> (shoulder_yaw_quat, elbow_pitch_quat)"""
+    dev = home_device(v1, v0, parent_global_rotation)
+    y, e = ops.cal_elbow_py(as_tensor(v1), as_tensor(v0), as_tensor(parent_global_rotation))
+    return back(y, dev), back(e, dev)
+
+
+def cal_shoulderPR(v1, v0, parent_global_rotation):
+    """:246-278 -> (pitch_joint_quat, roll_joint_quat)"""
+    dev = home_device(v1, v0, parent_global_rotation)
+    p, r = ops.cal_shoulder_pr(as_tensor(v1), as_tensor(v0), as_tensor(parent_global_rotation))
+    return back(p, dev), back(r, dev)

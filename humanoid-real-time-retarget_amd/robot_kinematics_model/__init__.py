@@ -1,0 +1,5 @@
+"""Drop-in ``robot_kinematics_model`` (reference robot_kinematics_model/__init__.py:8-12)."""
+from robot_kinematics_model.base_robot import RobotZeroPose
+from robot_kinematics_model.kinematics import cal_forward_kinematics, cal_local_rotation
+
+__all__ = ["RobotZeroPose", "cal_forward_kinematics", "cal_local_rotation"]

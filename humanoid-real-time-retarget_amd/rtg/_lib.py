@@ -38,6 +38,9 @@ OP_SHOULDER_PR = 11
 OP_ELBOW_PY = 12
 OP_QUAT_TO_ANGLE_AXIS = 13
 OP_NORMALIZE_ANGLE = 14
+OP_QUAT_ABS = 15
+OP_QUAT_UNIT = 16
+OP_QUAT_ANGLE_AXIS = 17
 
 MAX_SEGMENTS = 8
 
@@ -76,6 +79,10 @@ SIGNATURES = {
     "rtg_quat_op_f32": (c_int, [c_int, c_void_p, c_void_p, c_void_p, c_int64, c_void_p, c_void_p]),
     "rtg_cal_joint_quat_f32": (c_int, [c_void_p, c_void_p, c_int32, c_int64, c_void_p, c_void_p]),
     "rtg_quat_in_xyz_axis_f32": (c_int, [c_void_p, c_char_p, c_int64, c_void_p, c_void_p]),
+    "rtg_linear_velocity_f32": (c_int, [c_void_p, c_int64, c_int64, c_int64, c_float, c_void_p, c_int32, c_void_p,
+                                        c_void_p, c_void_p]),
+    "rtg_angular_velocity_f32": (c_int, [c_void_p, c_int64, c_int64, c_int64, c_float, c_void_p, c_int32, c_void_p,
+                                         c_void_p, c_void_p]),
     "rtg_synth_full_body_f32": (c_int, [c_void_p, c_uint64, c_int64, c_int64, c_void_p, c_void_p, c_void_p, c_void_p,
                                         c_void_p]),
 }

@@ -102,6 +102,22 @@ def quat_to_angle_axis(q):
     return r[..., 0], r[..., 1:]
 
 
+def quat_abs(q):
+    """rotation3d.py:41-47"""
+    return _quat_op(_lib.OP_QUAT_ABS, q, out_tail=0)
+
+
+def quat_unit(q):
+    """rotation3d.py:50-56"""
+    return _quat_op(_lib.OP_QUAT_UNIT, q)
+
+
+def quat_angle_axis(q):
+    """rotation3d.py:230-240 -> (angle in [0, pi] (...), unit axis (...,3))"""
+    r = _quat_op(_lib.OP_QUAT_ANGLE_AXIS, q, out_tail=4)
+    return r[..., 0], r[..., 1:]
+
+
 def normalize_angle(x):
     """rotation3d.py:582-584 (atan2 with glibc atan2f semantics: the reference's <32-element path)"""
     x = dev_f32(x)
@@ -234,6 +250,55 @@ def forward_kinematics_multi(segments: Sequence[tuple]):
         outs.append((g_rot, g_pos))
     check(lib().rtg_fk_multi_f32(segs, len(segments), stream_handle()))
     return outs
+
+
+def gaussian_taps(sigma: float = 2.0, truncate: float = 4.0):
+    """scipy.ndimage.gaussian_filter1d's taps (float64), as the reference applies them (sigma 2)."""
+    import numpy as np
+    radius = int(truncate * float(sigma) + 0.5)
+    try:
+        from scipy.ndimage._filters import _gaussian_kernel1d
+        w = _gaussian_kernel1d(sigma, 0, radius)[::-1]
+    except Exception:  # noqa: BLE001 -- same formula without scipy
+        x = np.arange(-radius, radius + 1)
+        w = np.exp(-0.5 / (sigma * sigma) * x ** 2)
+        w = (w / w.sum())[::-1]
+    return np.ascontiguousarray(w, dtype=np.float64), radius
+
+
+def _time_axis_view(x, tail):
+    x = dev_f32(x)
+    if x.dim() < 1 + tail:
+        raise ValueError("need a frame axis")
+    L = int(x.shape[-1 - tail])
+    nseq = int(torch.Size(x.shape[:-1 - tail]).numel())
+    return x, nseq, L
+
+
+def motion_velocity(p, dt: float, smooth: bool = True):
+    """SkeletonMotion._compute_velocity (skeleton3d.py:1126-1135): p (..., L, J, 3) -> (..., L, J, 3)."""
+    x, nseq, L = _time_axis_view(p, 2)
+    S = int(x.shape[-2] * x.shape[-1])
+    out = torch.empty_like(x)
+    tmp = torch.empty_like(x) if smooth else None
+    w, r = gaussian_taps() if smooth else (None, 0)
+    check(lib().rtg_linear_velocity_f32(ptr(x), nseq, L, S, ctypes.c_float(dt),
+                                        w.ctypes.data_as(ctypes.c_void_p) if smooth else None, r, ptr(tmp), ptr(out),
+                                        stream_handle()))
+    return out
+
+
+def motion_angular_velocity(r, dt: float, smooth: bool = True):
+    """SkeletonMotion._compute_angular_velocity (skeleton3d.py:1137-1146): r (..., L, J, 4) -> (..., L, J, 3)."""
+    x, nseq, L = _time_axis_view(r, 2)
+    J = int(x.shape[-2])
+    out = torch.empty(tuple(x.shape[:-1]) + (3,), device=x.device, dtype=torch.float32)
+    tmp = torch.empty_like(out) if smooth else None
+    w, rad = gaussian_taps() if smooth else (None, 0)
+    check(lib().rtg_angular_velocity_f32(ptr(x), nseq, L, J, ctypes.c_float(dt),
+                                         w.ctypes.data_as(ctypes.c_void_p) if smooth else None, rad, ptr(tmp),
+                                         ptr(out), stream_handle()))
+    return out
 
 
 def synth_full_body(topo_full: Topology, B: int, seed: int = 1234, frame_offset: int = 0, want_rot: bool = False,

@@ -145,7 +145,10 @@ typedef enum rtg_quat_op {
     RTG_OP_SHOULDER_PR = 11,        /* v1 (n,3), v0 (n,3), parent c (n,4) -> (n,2,4)  full_body_pos_retargeter.py:246-278 */
     RTG_OP_ELBOW_PY = 12,           /* v1, v0, parent -> (n,2,4)   full_body_pos_retargeter.py:220-243 */
     RTG_OP_QUAT_TO_ANGLE_AXIS = 13, /* q (n,4) -> (n,4) = [angle, axis xyz]  rotation3d.py:587-608 */
-    RTG_OP_NORMALIZE_ANGLE = 14     /* x (n) -> (n) atan2(sin x, cos x)      rotation3d.py:582-584 */
+    RTG_OP_NORMALIZE_ANGLE = 14,    /* x (n) -> (n) atan2(sin x, cos x)      rotation3d.py:582-584 */
+    RTG_OP_QUAT_ABS = 15,           /* q (n,4) -> (n) |q|                    rotation3d.py:41-47  */
+    RTG_OP_QUAT_UNIT = 16,          /* q (n,4) -> q / max(|q|, 1e-9)         rotation3d.py:50-56  */
+    RTG_OP_QUAT_ANGLE_AXIS = 17     /* q (n,4) -> [acos(2w^2-1), xyz/|xyz|]  rotation3d.py:230-240 */
 } rtg_quat_op;
 int rtg_quat_op_f32(int op, const float *a, const float *b, const float *c, int64_t n, float *out,
                     rtg_stream_t stream);
@@ -158,6 +161,23 @@ int rtg_cal_joint_quat_f32(const float *Z, const float *M, int32_t npts, int64_t
 /* quat_in_xyz_axis (transform3d.py:52-59): scipy Euler split (float64) into three
  * single-axis quaternions.  seq: 3 chars of xyz/XYZ (upper = intrinsic). q (n,4) -> (n,3,4). */
 int rtg_quat_in_xyz_axis_f32(const float *q, const char *seq, int64_t n, float *out, rtg_stream_t stream);
+
+/* ------------------------------------------------------------------------
+ * Motion velocities (SkeletonMotion.from_skeleton_state, poselib skeleton3d.py:1026-1049,
+ * _compute_velocity :1126-1135, _compute_angular_velocity :1137-1146).
+ * Time is the middle axis: nseq independent sequences of L frames of S channels.
+ * weights: the 2*radius+1 Gaussian taps (scipy _gaussian_kernel1d, sigma=2 ->
+ * radius 8, applied with mode='nearest' and float64 accumulation); NULL = no
+ * smoothing.  tmp: caller-owned scratch of the output's size.
+ * ---------------------------------------------------------------------- */
+#define RTG_MAX_FILTER_RADIUS 16
+/* p (nseq,L,S) -> out (nseq,L,S): np.gradient over frames / dt, then smoothing. */
+int rtg_linear_velocity_f32(const float *p, int64_t nseq, int64_t L, int64_t S, float dt, const double *weights,
+                            int32_t radius, float *tmp, float *out, rtg_stream_t stream);
+/* r (nseq,L,J,4) global rotations -> out (nseq,L,J,3): axis*angle of
+ * quat_mul_norm(r[t+1], conj(r[t])) / dt (last frame 0), then smoothing. */
+int rtg_angular_velocity_f32(const float *r, int64_t nseq, int64_t L, int64_t J, float dt, const double *weights,
+                             int32_t radius, float *tmp, float *out, rtg_stream_t stream);
 
 /* ------------------------------------------------------------------------
  * Synthetic mocap (bench / tests): FK of the VTRDYN_FULL zero pose with random

@@ -234,6 +234,30 @@ def elbow_py(v1, v0, parent):
     return out
 
 
+def linear_velocity(p, dt, weights=None):
+    p = _c32(p)
+    L, J = p.shape[-3], p.shape[-2]
+    nseq = int(np.prod(p.shape[:-3])) if p.ndim > 3 else 1
+    out = np.empty_like(p)
+    w = None if weights is None else np.ascontiguousarray(weights, np.float64)
+    R = 0 if w is None else (len(w) - 1) // 2
+    lib().oracle_linear_velocity(_fp(p), _i64(nseq), _i64(L), _i64(J * 3), ctypes.c_float(dt),
+                                 None if w is None else w.ctypes.data_as(_d), ctypes.c_int32(R), _fp(out))
+    return out
+
+
+def angular_velocity(r, dt, weights=None):
+    r = _c32(r)
+    L, J = r.shape[-3], r.shape[-2]
+    nseq = int(np.prod(r.shape[:-3])) if r.ndim > 3 else 1
+    out = np.empty(r.shape[:-1] + (3,), np.float32)
+    w = None if weights is None else np.ascontiguousarray(weights, np.float64)
+    R = 0 if w is None else (len(w) - 1) // 2
+    lib().oracle_angular_velocity(_fp(r), _i64(nseq), _i64(L), _i64(J), ctypes.c_float(dt),
+                                  None if w is None else w.ctypes.data_as(_d), ctypes.c_int32(R), _fp(out))
+    return out
+
+
 def atan2f(y, x):
     y, x = _c32(y), _c32(x)
     out = np.empty_like(y)

@@ -1,0 +1,169 @@
+"""The reference's Python API (retarget.retarget_solver, robot_kinematics_model,
+poselib ...skeleton3d / ...rotation3d, retarget.spatial_transform.transform3d)
+served by the drop-in modules, called exactly the way the reference's entry
+points call it (sim_full_body_teleop.py:115-119, sim_teleop.py:102,
+base_retargeter.py:22-58), with CPU tensors in and CPU tensors out."""
+import numpy as np
+import pytest
+import torch
+
+from conftest import frame_stats, golden
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def poses(gpu):
+    from robot_kinematics_model import RobotZeroPose
+    return {n: RobotZeroPose.from_asset(n) for n in ("hu_v5", "vtrdyn_full", "vtrdyn")}
+
+
+def test_zero_pose_global_translation_bit_exact(poses):
+    zp = golden("zero_pose")
+    for n in ("hu_v5", "vtrdyn_full", "vtrdyn"):
+        gt = poses[n].global_translation
+        assert gt.device.type == "cpu"
+        np.testing.assert_array_equal(gt.numpy(), zp[f"{n}_global_t"])
+
+
+def test_full_body_pos_per_frame_api(poses):
+    import oracle as orc
+    from retarget.retarget_solver import VtrdynFullBodyPosRetargeter
+    d = golden("full_body_pos_precise")
+    zp = golden("zero_pose")
+    s = VtrdynFullBodyPosRetargeter(poses["vtrdyn_full"], poses["hu_v5"], precise_gripper=True)
+    n = 24
+    outs = [s.retarget(torch.from_numpy(d["body"][i]), torch.from_numpy(d["lh"][i]), torch.from_numpy(d["rh"][i]))
+            for i in range(n)]
+    lr, dof, br = outs[0]
+    assert lr.shape == (31, 4) and dof.shape == (30,) and br.shape == (59, 4) and dof.device.type == "cpu"
+    dof = np.stack([o[1].numpy() for o in outs])
+    odof, olr, obr = orc.full_body_pos(zp["vtrdyn_full_local_t"], zp["vtrdyn_full_global_t"], d["body"][:n],
+                                       d["lh"][:n], d["rh"][:n], True)
+    np.testing.assert_array_equal(dof, odof)
+    np.testing.assert_array_equal(np.stack([o[2].numpy() for o in outs]), obr)
+    assert frame_stats(dof, d["dof"][:n])["max"] <= 2e-3
+    # accumulated motion + FK of the retargeted motion (base_retargeter.py:22-58)
+    assert s.motion_length == n
+    np.testing.assert_array_equal(s.motion_dof_pos.numpy(), odof)
+    from rtg import assets
+    gr, gp = orc.fk(assets.parents("hu_v5"), poses["hu_v5"].local_translation.numpy(), olr, np.zeros((n, 3), np.float32))
+    np.testing.assert_array_equal(s.motion_global_rotation.numpy(), gr)
+    np.testing.assert_array_equal(s.motion_global_translation.numpy(), gp)
+
+
+def test_batched_equals_per_frame(poses):
+    from retarget.retarget_solver import VtrdynFullBodyPosRetargeter
+    d = golden("full_body_pos_binary")
+    s = VtrdynFullBodyPosRetargeter(poses["vtrdyn_full"], poses["hu_v5"], precise_gripper=False)
+    lr_b, dof_b, br_b = s.retarget_batch(torch.from_numpy(d["body"]).cuda(), torch.from_numpy(d["lh"]).cuda(),
+                                         torch.from_numpy(d["rh"]).cuda(), want_body_rot=True)
+    assert dof_b.is_cuda and dof_b.shape == (len(d["body"]), 30)
+    for i in (0, 7, 63):
+        lr, dof, br = s.retarget(torch.from_numpy(d["body"][i]), torch.from_numpy(d["lh"][i]),
+                                 torch.from_numpy(d["rh"][i]))
+        assert torch.equal(dof, dof_b[i].cpu()) and torch.equal(lr, lr_b[i].cpu()) and torch.equal(br, br_b[i].cpu())
+
+
+def test_other_solver_classes(poses):
+    import oracle as orc
+    from rtg import assets
+    from retarget.retarget_solver import (HuUpperBodyFromMocapRetarget, Mocap2HuBodyRetargeter,
+                                          VtrdynFullBodyRetargeter)
+    zp = golden("zero_pose")
+    d = golden("upper_body")
+    s = HuUpperBodyFromMocapRetarget(poses["vtrdyn"], poses["hu_v5"])
+    lr, dof = s.retarget_from_global_translation(torch.from_numpy(d["x"][3]))
+    np.testing.assert_array_equal(dof.numpy(), orc.upper_body(zp["vtrdyn_local_t"], d["x"][3:4])[0][0])
+    d = golden("full_body_rot")
+    s = VtrdynFullBodyRetargeter(poses["vtrdyn_full"], poses["hu_v5"])
+    lr, dof = s.retarget(torch.from_numpy(d["body_rot"][5]), torch.from_numpy(d["body_pos"][5]), None,
+                         torch.from_numpy(d["lh"][5]), None, torch.from_numpy(d["rh"][5]))
+    np.testing.assert_array_equal(dof.numpy(), orc.full_body_rot(zp["vtrdyn_full_local_t"], d["body_rot"][5:6],
+                                                                 d["body_pos"][5:6], d["lh"][5:6], d["rh"][5:6])[0][0])
+    d = golden("body_rot")
+    s = Mocap2HuBodyRetargeter(poses["vtrdyn"], poses["hu_v5"])
+    lr, dof = s.retarget_from_pose(torch.from_numpy(d["global_rot"][9]))
+    np.testing.assert_array_equal(dof.numpy(), orc.body_rot(assets.parents("vtrdyn"), d["global_rot"][9:10])[0][0])
+    assert frame_stats(dof.numpy()[None], d["dof"][9:10])["max"] <= 1e-6
+
+
+def test_rotation3d_mirror_bit_exact_cpu_in_cpu_out(gpu):
+    from poselib.poselib.core import rotation3d as r3
+    p = golden("primitives")
+    a, b = torch.from_numpy(p["qm_a"]), torch.from_numpy(p["qm_b"])
+    out = r3.quat_mul(a, b)
+    assert out.device.type == "cpu"
+    np.testing.assert_array_equal(out.numpy(), p["quat_mul"])
+    np.testing.assert_array_equal(r3.quat_mul_norm(a, b).numpy(), p["quat_mul_norm"])
+    np.testing.assert_array_equal(r3.quat_normalize(a).numpy(), p["quat_normalize"])
+    np.testing.assert_array_equal(r3.quat_rotate(b, torch.from_numpy(p["qr_v"])).numpy(), p["quat_rotate"])
+    q = r3.quat_mul_three(a, b, a)
+    np.testing.assert_array_equal(q.numpy(), r3.quat_mul(r3.quat_mul(a, b), a).numpy())
+    t = r3.transform_mul(torch.cat([b, torch.ones(len(b), 3)], -1), torch.cat([a, torch.zeros(len(a), 3)], -1))
+    assert t.shape == (len(a), 7)
+
+
+def test_transform3d_mirror(gpu):
+    from retarget.spatial_transform import transform3d as tf
+    from retarget.robot_config.Hu_v5 import Hu_DOF_AXIS
+    p = golden("primitives")
+    eye = torch.eye(3)
+    v1 = torch.from_numpy(p["rbv_v1"])
+    np.testing.assert_array_equal(tf.proj_in_plane(v1[0], eye[1]).numpy(), p["proj_in_plane_y"][0])
+    r = tf.radians_between_vecs(v1[2], torch.from_numpy(p["rbv_v2"][2]), torch.from_numpy(p["rbv_n"][2]))
+    assert r.dim() == 0 and abs(float(r) - float(p["radians_between_vecs"][2])) <= 2.5e-7
+    dof = tf.quat_to_dof_pos(torch.from_numpy(p["dof_q31"][3, 1:]), Hu_DOF_AXIS)
+    assert frame_stats(dof.numpy()[None], p["quat_to_dof_pos"][3:4])["max"] <= 2.5e-7
+    q1, q2, q3 = tf.quat_in_xyz_axis(torch.from_numpy(p["qxyz_q"][:4]), "XYZ")
+    np.testing.assert_array_equal(torch.stack([q1, q2, q3], 1).numpy(), p["quat_in_xyz_axis_XYZ"][:4])
+    Z, M = torch.from_numpy(p["cjq5_Z"][:1]), torch.from_numpy(p["cjq5_M"][:1])
+    assert tf.cal_joint_quat(Z, M).shape == (1, 4)
+    x = torch.arange(6, dtype=torch.float32).reshape(2, 3)
+    np.testing.assert_array_equal(tf.coord_transform(x, dir=torch.Tensor([-1, -1, 1])).numpy(),
+                                  (x * torch.Tensor([-1, -1, 1])).numpy())
+
+
+def test_skeleton_state_and_kinematics_mirror(gpu):
+    from poselib.poselib.skeleton.skeleton3d import SkeletonState, SkeletonTree
+    from robot_kinematics_model import cal_forward_kinematics, cal_local_rotation
+    from rtg import assets
+    k = golden("kinematics")
+    for name in ("hu_v5", "vtrdyn_full"):
+        tree = SkeletonTree([str(s) for s in assets.load(name)["node_names"]], torch.from_numpy(assets.parents(name)),
+                            torch.from_numpy(assets.local_translation(name)), torch.from_numpy(assets.tree_quat(name)))
+        st = SkeletonState.from_rotation_and_root_translation(tree, torch.from_numpy(k[f"{name}_local_rot"]),
+                                                              torch.from_numpy(k[f"{name}_root_t"]), is_local=True)
+        np.testing.assert_array_equal(st.global_rotation.numpy(), k[f"{name}_state_g_rot"])
+        np.testing.assert_array_equal(st.global_translation.numpy(), k[f"{name}_state_g_pos"])
+        sg = SkeletonState.from_rotation_and_root_translation(tree, st.global_rotation, st.root_translation,
+                                                              is_local=False)
+        np.testing.assert_array_equal(sg.local_rotation.numpy(), k[f"{name}_state_local_rot"])
+        gr, gp = cal_forward_kinematics(torch.from_numpy(k[f"{name}_local_rot"]), torch.from_numpy(k[f"{name}_root_t"]),
+                                        tree.parent_indices, tree.local_translation)
+        np.testing.assert_array_equal(gr.numpy(), k[f"{name}_g_rot"])
+        np.testing.assert_array_equal(gp.numpy(), k[f"{name}_g_pos"])
+        np.testing.assert_array_equal(cal_local_rotation(gr, tree.parent_indices).numpy(), k[f"{name}_inv_local"])
+
+
+def test_skeleton_state_pickle_roundtrip(gpu):
+    import pickle
+    from robot_kinematics_model import RobotZeroPose
+    from poselib.poselib.skeleton.skeleton3d import SkeletonState
+    st = SkeletonState.zero_pose(RobotZeroPose.from_asset("hu_v5").skeleton_tree)
+    st2 = pickle.loads(pickle.dumps(st))
+    assert torch.equal(st2.global_translation, st.global_translation)
+
+
+def test_skeleton_motion_from_state(gpu):
+    from poselib.poselib.skeleton.skeleton3d import SkeletonMotion, SkeletonState
+    from robot_kinematics_model import RobotZeroPose
+    m = golden("motion")
+    tree = RobotZeroPose.from_asset("hu_v5").skeleton_tree
+    st = SkeletonState.from_rotation_and_root_translation(tree, torch.from_numpy(m["local_rot"]),
+                                                          torch.from_numpy(m["root_t"]), is_local=True)
+    mo = SkeletonMotion.from_skeleton_state(st, fps=30)
+    assert mo.tensor.device.type == "cpu" and mo.fps == 30
+    np.testing.assert_array_equal(mo.global_velocity.numpy(), m["global_velocity"])
+    assert frame_stats(mo.global_angular_velocity.numpy(), m["global_angular_velocity"])["max"] <= 1e-6
+    np.testing.assert_array_equal(mo.tensor.numpy()[:, :31 * 4 + 3], m["tensor"][:, :31 * 4 + 3])

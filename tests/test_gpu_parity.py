@@ -220,3 +220,17 @@ def test_solver_full_size_properties(gpu):
     # determinism: a second launch is bit-identical
     dof2, _, _ = S.retarget([body, lh, rh])
     assert torch.equal(dof, dof2)
+
+
+def test_motion_velocities_vs_oracle(gpu):
+    import oracle as orc
+    from rtg import ops
+    m = golden("motion")
+    w, _ = ops.gaussian_taps()
+    np.testing.assert_array_equal(_np(ops.motion_velocity(m["global_pos"], 1 / 30)), m["global_velocity"])
+    av = _np(ops.motion_angular_velocity(m["global_rot"], 1 / 30))
+    s = frame_stats(av, orc.angular_velocity(m["global_rot"], 1 / 30, w))
+    assert s["exact_elems"] >= 0.999 and s["max"] <= 1e-6, s
+    # unsmoothed variant and batched sequences
+    lv = _np(ops.motion_velocity(np.stack([m["global_pos"]] * 3), 1 / 30, smooth=False))
+    np.testing.assert_array_equal(lv[1], orc.linear_velocity(m["global_pos"], 1 / 30, None))

@@ -168,3 +168,13 @@ def test_rotation_test_kat():
     ey = orc.elbow_py(k["v2t"][0][None], k["vec2"][0][None], comb)
     v2cal = orc.quat_rotate(orc.quat_mul(orc.quat_mul(comb, ey[:, 0]), ey[:, 1]), k["vec2"])
     np.testing.assert_allclose(v2cal, k["v2t"], rtol=1e-3, atol=1e-6)
+
+
+def test_motion_velocities_vs_reference():
+    """SkeletonMotion.from_skeleton_state velocities (skeleton3d.py:1126-1146)."""
+    from scipy.ndimage._filters import _gaussian_kernel1d
+    m = golden("motion")
+    w = _gaussian_kernel1d(2, 0, 8)[::-1]
+    np.testing.assert_array_equal(orc.linear_velocity(m["global_pos"], 1 / 30, w), m["global_velocity"])
+    s = frame_stats(orc.angular_velocity(m["global_rot"], 1 / 30, w), m["global_angular_velocity"])
+    assert s["max"] <= 1e-6 and s["exact_elems"] >= 0.5, s   # MKL acos ulps

@@ -29,10 +29,10 @@ import numpy as np
 HERE = os.path.dirname(os.path.abspath(__file__))
 REPO = os.path.dirname(HERE)
 sys.path.insert(0, HERE)
-sys.path.insert(0, os.path.join(REPO, "humanoid-real-time-retarget_amd"))
 
 import refharness as rh  # noqa: E402
-from rtg import synth  # noqa: E402
+
+synth = rh.load_rtg_module("synth")
 
 OUT = os.path.join(REPO, "tests", "golden")
 warnings.filterwarnings("ignore")
@@ -132,6 +132,25 @@ def _rand_quats(rng, n):
     q = rng.normal(size=(n, 4))
     q /= np.linalg.norm(q, axis=-1, keepdims=True)
     return q.astype(np.float32)
+
+
+def gen_motion(ref, torch, L=96):
+    """SkeletonMotion.from_skeleton_state (skeleton3d.py:1026-1049): smooth random Hu motion at 30 fps."""
+    st0 = rh.ref_skeleton_state(ref, "hu_v5")
+    tree = st0.skeleton_tree
+    J = tree.num_joints
+    rng = np.random.default_rng(77)
+    # smooth trajectories: cumulative small axis-angle steps per joint
+    steps = rng.normal(0, 0.05, (L, J, 3)).cumsum(0)
+    ang = np.linalg.norm(steps, axis=-1, keepdims=True)
+    q = np.concatenate([steps / np.maximum(ang, 1e-12) * np.sin(ang / 2), np.cos(ang / 2)], -1).astype(np.float32)
+    rt = (rng.normal(0, 0.01, (L, 3)).cumsum(0)).astype(np.float32)
+    st = ref.skeleton3d.SkeletonState.from_rotation_and_root_translation(tree, torch.from_numpy(q), torch.from_numpy(rt),
+                                                                         is_local=True)
+    mo = ref.skeleton3d.SkeletonMotion.from_skeleton_state(st, fps=30)
+    return dict(local_rot=q, root_t=rt, global_rot=t2n(st.global_rotation), global_pos=t2n(st.global_translation),
+                global_velocity=t2n(mo.global_velocity), global_angular_velocity=t2n(mo.global_angular_velocity),
+                tensor=t2n(mo.tensor), fps=np.array(30))
 
 
 def gen_primitives(ref, torch):
@@ -281,6 +300,7 @@ def main() -> None:
         "body_rot": lambda: gen_body_rot(ref, torch, 256, 5678),
         "kinematics": lambda: gen_kinematics(ref, torch, 128),
         "primitives": lambda: gen_primitives(ref, torch),
+        "motion": lambda: gen_motion(ref, torch),
         "kat_rotation_test": lambda: gen_kat(ref, torch),
     }
     only = set(sys.argv[1:])

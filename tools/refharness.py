@@ -23,6 +23,22 @@ REPO = os.path.dirname(HERE)
 ASSETS = os.path.join(REPO, "humanoid-real-time-retarget_amd", "assets")
 
 
+def load_rtg_module(name: str):
+    """Import ``rtg.<name>`` by file location.  The package root also holds the
+    drop-in ``retarget`` / ``poselib`` / ``robot_kinematics_model`` packages, which
+    must not shadow the reference's (namespace) packages, so it is never put on
+    sys.path here."""
+    import importlib.util
+    pkg_dir = os.path.join(REPO, "humanoid-real-time-retarget_amd", "rtg")
+    if "rtg" not in sys.modules:
+        spec = importlib.util.spec_from_file_location("rtg", os.path.join(pkg_dir, "__init__.py"),
+                                                      submodule_search_locations=[pkg_dir])
+        mod = importlib.util.module_from_spec(spec)
+        sys.modules["rtg"] = mod
+        spec.loader.exec_module(mod)
+    return importlib.import_module(f"rtg.{name}")
+
+
 def _stub(name: str, **attrs) -> types.ModuleType:
     mod = types.ModuleType(name)
     for k, v in attrs.items():
