@@ -331,6 +331,134 @@ __global__ __launch_bounds__(256) void k_local_rotation(TopoView T, const float 
     }
 }
 
+// ----------------------------------------------------------------------------
+// LDS-tiled FK (the production path).  One wave = one tile of 64 consecutive
+// frames.  The tile's local rotations are one contiguous span of global memory,
+// copied into LDS with dwordx4 loads (the LDS image has the global layout, so no
+// index math; with odd J the per-frame pitch J*4 dwords keeps the lanes'
+// ds_read_b128 conflict-free).  Each lane then walks its frame's chain in LDS:
+// the global rotation of joint j overwrites its local rotation in place (joint
+// j's parent p < j is already global), positions go to a second LDS image, and
+// both images are stored back as contiguous dwordx4 spans.
+// LDS: 64 * J * 28 bytes (Hu 55.5 KiB, VTRDYN_FULL 106 KiB).
+// ----------------------------------------------------------------------------
+constexpr int kFkTile = 64;
+
+RTG_DEV void copy_span_to_lds(float *__restrict__ dst, const float *__restrict__ src, int n)   // n floats
+{
+    const int nv = n >> 2;
+    const bool aligned = ((reinterpret_cast<uintptr_t>(src) & 15) == 0);
+    if (aligned) {
+        for (int v = threadIdx.x; v < nv; v += kFkTile)
+            reinterpret_cast<float4 *>(dst)[v] = reinterpret_cast<const float4 *>(src)[v];
+        for (int i = (nv << 2) + threadIdx.x; i < n; i += kFkTile) dst[i] = src[i];
+    } else {
+        for (int i = threadIdx.x; i < n; i += kFkTile) dst[i] = src[i];
+    }
+}
+RTG_DEV void copy_span_from_lds(float *__restrict__ dst, const float *__restrict__ src, int n)
+{
+    const int nv = n >> 2;
+    const bool aligned = ((reinterpret_cast<uintptr_t>(dst) & 15) == 0);
+    if (aligned) {
+        for (int v = threadIdx.x; v < nv; v += kFkTile)
+            reinterpret_cast<float4 *>(dst)[v] = reinterpret_cast<const float4 *>(src)[v];
+        for (int i = (nv << 2) + threadIdx.x; i < n; i += kFkTile) dst[i] = src[i];
+    } else {
+        for (int i = threadIdx.x; i < n; i += kFkTile) dst[i] = src[i];
+    }
+}
+
+template <bool STATE>
+RTG_DEV void fk_tile(const TopoView &T, const float *__restrict__ local_rot, const float *__restrict__ root_t,
+                     int64_t B, int64_t f0, float *__restrict__ g_rot, float *__restrict__ g_pos, float *lds)
+{
+    const int J = T.J;
+    const int nfr = (int)((B - f0) < kFkTile ? (B - f0) : kFkTile);
+    float *rot = lds;                          // [nfr][J][4]
+    float *pos = lds + kFkTile * J * 4;        // [nfr][J][3]
+    copy_span_to_lds(rot, local_rot + f0 * J * 4, nfr * J * 4);
+    __syncthreads();
+    const int f = threadIdx.x;
+    if (f < nfr) {
+        float *R = rot + f * J * 4;
+        float *P = pos + f * J * 3;
+        Q g = Q{R[0], R[1], R[2], R[3]};       // root: global = local, unnormalised (kinematics.py:27-29)
+        V t = ld3(root_t + (f0 + f) * 3);
+        P[0] = t.x; P[1] = t.y; P[2] = t.z;
+        for (int j = 1; j < J; ++j) {
+            const int p = T.parents[j];
+            if (p != j - 1) {
+                g = Q{R[4 * p], R[4 * p + 1], R[4 * p + 2], R[4 * p + 3]};
+                t = V{P[3 * p], P[3 * p + 1], P[3 * p + 2]};
+            }
+            Q lq = Q{R[4 * j], R[4 * j + 1], R[4 * j + 2], R[4 * j + 3]};
+            if (STATE) lq = qmul_norm(T.tree_quat[j], lq);
+            const V rv = qrotate(g, T.local_t[j]);
+            const Q ng = qmul_norm(g, lq);
+            const V nt = V{rv.x + t.x, rv.y + t.y, rv.z + t.z};
+            R[4 * j] = ng.x; R[4 * j + 1] = ng.y; R[4 * j + 2] = ng.z; R[4 * j + 3] = ng.w;
+            P[3 * j] = nt.x; P[3 * j + 1] = nt.y; P[3 * j + 2] = nt.z;
+            g = ng;
+            t = nt;
+        }
+    }
+    __syncthreads();
+    copy_span_from_lds(g_rot + f0 * J * 4, rot, nfr * J * 4);
+    copy_span_from_lds(g_pos + f0 * J * 3, pos, nfr * J * 3);
+}
+
+template <bool STATE>
+__global__ __launch_bounds__(kFkTile) void k_fk_tiled(TopoView T, const float *__restrict__ local_rot,
+                                                      const float *__restrict__ root_t, int64_t B,
+                                                      float *__restrict__ g_rot, float *__restrict__ g_pos)
+{
+    extern __shared__ __attribute__((aligned(16))) float fk_lds[];
+    fk_tile<STATE>(T, local_rot, root_t, B, (int64_t)blockIdx.x * kFkTile, g_rot, g_pos, fk_lds);
+}
+
+// inverse FK, tiled the same way: input image -> per-lane chain -> output image
+template <bool STATE>
+__global__ __launch_bounds__(kFkTile) void k_local_rotation_tiled(TopoView T, const float *__restrict__ g_rot,
+                                                                  int64_t B, float *__restrict__ local_rot)
+{
+    extern __shared__ __attribute__((aligned(16))) float fk_lds[];
+    const int J = T.J;
+    const int64_t f0 = (int64_t)blockIdx.x * kFkTile;
+    const int nfr = (int)((B - f0) < kFkTile ? (B - f0) : kFkTile);
+    float *gin = fk_lds;                   // [nfr][J][4]
+    float *lout = fk_lds + kFkTile * J * 4;
+    copy_span_to_lds(gin, g_rot + f0 * J * 4, nfr * J * 4);
+    __syncthreads();
+    const int f = threadIdx.x;
+    if (f < nfr) {
+        const float *G = gin + f * J * 4;
+        float *L = lout + f * J * 4;
+        L[0] = G[0]; L[1] = G[1]; L[2] = G[2]; L[3] = G[3];
+        for (int j = 1; j < J; ++j) {
+            const int p = T.parents[j];
+            Q q = qmul_norm(qconj(Q{G[4 * p], G[4 * p + 1], G[4 * p + 2], G[4 * p + 3]}),
+                            Q{G[4 * j], G[4 * j + 1], G[4 * j + 2], G[4 * j + 3]});
+            if (STATE) q = qmul_norm(qnormalize(qconj(T.tree_quat[j])), q);
+            L[4 * j] = q.x; L[4 * j + 1] = q.y; L[4 * j + 2] = q.z; L[4 * j + 3] = q.w;
+        }
+    }
+    __syncthreads();
+    copy_span_from_lds(local_rot + f0 * J * 4, lout, nfr * J * 4);
+}
+
+__global__ __launch_bounds__(kFkTile) void k_fk_multi_tiled(FkMultiArgs A)
+{
+    extern __shared__ __attribute__((aligned(16))) float fk_lds[];
+    int s = 0;
+#pragma unroll
+    for (int i = 1; i < RTG_MAX_SEGMENTS; ++i)
+        if (i < A.n && (int64_t)blockIdx.x >= A.block_start[i]) s = i;
+    const FkSeg &S = A.seg[s];
+    fk_tile<false>(S.T, S.local_rot, S.root_t, S.B, ((int64_t)blockIdx.x - A.block_start[s]) * kFkTile, S.g_rot,
+                   S.g_pos, fk_lds);
+}
+
 __global__ __launch_bounds__(256) void k_fk_multi(FkMultiArgs A)
 {
     int s = 0;
@@ -649,35 +777,60 @@ hipError_t launch_retarget(int kind, int precise, const SolverConsts &C, const f
     return hipGetLastError();
 }
 
+static inline size_t fk_lds_bytes(int J) { return (size_t)kFkTile * J * 28; }
+constexpr size_t kMaxLds = 160 * 1024;
+// A shared multi-segment launch sizes LDS for its largest skeleton; above 64 KiB
+// per wave the smaller skeletons lose more occupancy than the tiling gains.
+constexpr size_t kMaxMultiLds = 64 * 1024;
+
 hipError_t launch_fk(const TopoView &T, bool state, const float *lr, const float *rt, int64_t B, float *gr, float *gp,
                      hipStream_t s)
 {
-    if (state)
+    const size_t lds = fk_lds_bytes(T.J);
+    if (lds <= kMaxLds) {
+        const dim3 g(grid_for(B, kFkTile)), b(kFkTile);
+        if (state) hipLaunchKernelGGL(k_fk_tiled<true>, g, b, lds, s, T, lr, rt, B, gr, gp);
+        else hipLaunchKernelGGL(k_fk_tiled<false>, g, b, lds, s, T, lr, rt, B, gr, gp);
+    } else if (state) {
         hipLaunchKernelGGL(k_fk<true>, dim3(grid_for(B, 256)), dim3(256), 0, s, T, lr, rt, B, gr, gp);
-    else
+    } else {
         hipLaunchKernelGGL(k_fk<false>, dim3(grid_for(B, 256)), dim3(256), 0, s, T, lr, rt, B, gr, gp);
+    }
     return hipGetLastError();
 }
 
 hipError_t launch_local_rotation(const TopoView &T, bool state, const float *g, int64_t B, float *l, hipStream_t s)
 {
-    if (state)
+    const size_t lds = (size_t)kFkTile * T.J * 32;
+    if (lds <= kMaxLds) {
+        const dim3 gd(grid_for(B, kFkTile)), b(kFkTile);
+        if (state) hipLaunchKernelGGL(k_local_rotation_tiled<true>, gd, b, lds, s, T, g, B, l);
+        else hipLaunchKernelGGL(k_local_rotation_tiled<false>, gd, b, lds, s, T, g, B, l);
+    } else if (state) {
         hipLaunchKernelGGL(k_local_rotation<true>, dim3(grid_for(B, 256)), dim3(256), 0, s, T, g, B, l);
-    else
+    } else {
         hipLaunchKernelGGL(k_local_rotation<false>, dim3(grid_for(B, 256)), dim3(256), 0, s, T, g, B, l);
+    }
     return hipGetLastError();
 }
 
 hipError_t launch_fk_multi(FkMultiArgs &A, hipStream_t s)
 {
+    int maxJ = 0;
+    for (int i = 0; i < A.n; ++i) maxJ = A.seg[i].T.J > maxJ ? A.seg[i].T.J : maxJ;
+    const bool tiled = fk_lds_bytes(maxJ) <= kMaxMultiLds;
+    const int per = tiled ? kFkTile : 256;
     int64_t blocks = 0;
     for (int i = 0; i < A.n; ++i) {
         A.block_start[i] = blocks;
-        blocks += grid_for(A.seg[i].B, 256);
+        blocks += grid_for(A.seg[i].B, per);
     }
     for (int i = A.n; i < RTG_MAX_SEGMENTS; ++i) A.block_start[i] = blocks;
     if (blocks == 0) return hipSuccess;
-    hipLaunchKernelGGL(k_fk_multi, dim3((unsigned)blocks), dim3(256), 0, s, A);
+    if (tiled)
+        hipLaunchKernelGGL(k_fk_multi_tiled, dim3((unsigned)blocks), dim3(kFkTile), fk_lds_bytes(maxJ), s, A);
+    else
+        hipLaunchKernelGGL(k_fk_multi, dim3((unsigned)blocks), dim3(256), 0, s, A);
     return hipGetLastError();
 }
 

@@ -143,7 +143,7 @@ def proj_in_plane(v, n):
     if bool((torch.linalg.norm(nn, dim=-1) <= 1e-6).any()):
         raise AssertionError("proj_in_plane: plane normal has (near) zero length")   # transform3d.py:70
     v, nn = _bcast(v, nn, 3, 3)
-    return _quat_op(_lib.OP_PROJ_IN_PLANE, v, nn, b_tail=3, out_tail=3)
+    return _quat_op(_lib.OP_PROJ_IN_PLANE, v, nn, a_tail=3, b_tail=3, out_tail=3)
 
 
 def quat_to_dof_pos_hu(local_rot):
