@@ -85,6 +85,19 @@ def cpu_baseline(body, lh, rh, zl, zg, seconds):
                       f"OpenMP x{threads}, {dt:.1f} s", "cpu": model}
 
 
+def pmc_traffic(B):
+    """HBM bytes per k_retarget launch from the committed rocprofv3 FETCH_SIZE + WRITE_SIZE passes
+    (profiles/pmc_traffic.json, written by tools/pmc_summary.py), when they were taken at this batch."""
+    path = os.path.join(REPO, "profiles", "pmc_traffic.json")
+    try:
+        rec = json.load(open(path)).get("rtg::k_retarget<0, true>")
+    except (OSError, ValueError):
+        return None
+    if not rec or rec.get("grid") != B:
+        return None
+    return rec["traffic_bytes"]
+
+
 def parity_vs_reference():
     """max / p99 |dof_gpu - dof_ref| on the committed reference golden vectors."""
     import torch
@@ -179,9 +192,9 @@ def main():
                        "frames_per_gpu_per_step": B, "global_batch": B * world, "parallelism": f"dp{world}",
                        "input_ring_sets": ring, "precise_gripper": True},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": achieved / HBM_PEAK_GBS, "traffic": None,
+                         "frac": achieved / HBM_PEAK_GBS, "traffic": pmc_traffic(B),
                          "kernel": "k_retarget<FULL_BODY_POS>", "kernel_ms": kern_ms,
-                         "bytes_per_frame": BYTES_PER_FRAME},
+                         "bytes_per_frame": BYTES_PER_FRAME, "traffic_unit": "bytes/launch (rocprofv3 PMC)"},
         }
         if gather_ms is not None:
             line["gather_ms"] = gather_ms
