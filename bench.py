@@ -125,15 +125,16 @@ def main():
     B = args.batch
     dev = torch.device("cuda", local)
     # solver constants: rank 0 owns the zero pose; RCCL broadcast to the other ranks (setup, untimed)
-    zl = torch.from_numpy(assets.local_translation("vtrdyn_full")).to(dev)
-    topo_full = Topology(assets.parents("vtrdyn_full"), zl.cpu().numpy(), assets.tree_quat("vtrdyn_full"))
-    zg = ops.forward_kinematics(topo_full, torch.tensor([[0, 0, 0, 1.0]]).expand(1, 59, 4),
-                                torch.zeros(1, 3), state=True)[1][0]
+    from rtg import shard
+    topo_full = Topology(assets.parents("vtrdyn_full"), assets.local_translation("vtrdyn_full"),
+                         assets.tree_quat("vtrdyn_full"))
+    zl = zg = None
+    if rank == 0:
+        zl = torch.from_numpy(assets.local_translation("vtrdyn_full")).to(dev)
+        zg = ops.forward_kinematics(topo_full, torch.tensor([[0, 0, 0, 1.0]]).expand(1, 59, 4),
+                                    torch.zeros(1, 3), state=True)[1][0].to(dev)
     if world > 1:
-        import torch.distributed as dist
-        blob = torch.cat([zl.reshape(-1), zg.reshape(-1)]).contiguous()
-        dist.broadcast(blob, src=0)
-        zl, zg = blob[:177].reshape(59, 3), blob[177:].reshape(59, 3)
+        zl, zg = shard.broadcast_solver_consts(zl, zg, max_joints=64, device=dev)
     solver = Solver(_lib.SOLVER_FULL_BODY_POS, zl.cpu().numpy(), zg.cpu().numpy(), assets.parents("vtrdyn_full"),
                     precise_gripper=True)
 
@@ -163,22 +164,17 @@ def main():
     wall = time.perf_counter() - t0
     kern_ms = float(np.mean([s.elapsed_time(e) for s, e in zip(starts, ends)]))
     if world > 1:
-        import torch.distributed as dist
-        tw = torch.tensor([wall], device=dev, dtype=torch.float64)
-        dist.all_reduce(tw, op=dist.ReduceOp.MAX)
-        wall = float(tw.item())
+        wall = shard.max_over_ranks(wall, dev)
     frames = world * B * args.steps
     value = frames / wall
     ms_per_step = wall * 1e3 / args.steps
 
     gather_ms = None
     if world > 1:   # final DOF gather to rank 0 over RCCL (untimed region, reported separately)
-        import torch.distributed as dist
         d = sets[(args.steps - 1) % ring][3]
-        outs = [torch.empty_like(d) for _ in range(world)] if rank == 0 else None
         torch.cuda.synchronize()
         tg = time.perf_counter()
-        dist.gather(d, outs, dst=0)
+        shard.gather_shards(d, [B] * world, dst=0)
         torch.cuda.synchronize()
         gather_ms = (time.perf_counter() - tg) * 1e3
 

@@ -1,0 +1,131 @@
+"""world_size-2 gloo tests of the multi-GPU host logic (rtg/shard.py, bench.py's N>1 path) on CPU."""
+from __future__ import annotations
+
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from conftest import PKG  # noqa: F401  (puts the package on sys.path)
+from rtg import shard
+
+
+def _free_port() -> int:
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _worker(rank, world, port, fn, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        q.put((rank, fn(rank, world)))
+    except Exception as e:  # noqa: BLE001
+        q.put((rank, e))
+    finally:
+        dist.destroy_process_group()
+
+
+def _run(fn, world=2):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, fn, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=120) for _ in procs)
+    for p in procs:
+        p.join(timeout=60)
+    for r, v in res.items():
+        if isinstance(v, Exception):
+            raise v
+    return res
+
+
+def test_shard_range_partitions():
+    for total in (0, 1, 7, 262144, 2 * 1024 * 1024 + 3):
+        for world in (1, 2, 3, 8):
+            spans = [shard.shard_range(total, world, r) for r in range(world)]
+            assert spans[0][0] == 0 and sum(c for _, c in spans) == total
+            for (s0, c0), (s1, _) in zip(spans, spans[1:]):
+                assert s0 + c0 == s1
+            assert max(c for _, c in spans) - min(c for _, c in spans) <= 1
+    with pytest.raises(ValueError):
+        shard.shard_range(10, 2, 2)
+
+
+def test_pack_roundtrip():
+    zl, zg = torch.randn(59, 3), torch.randn(59, 3)
+    a, b = shard.unpack_solver_consts(shard.pack_solver_consts(zl, zg))
+    assert torch.equal(a, zl) and torch.equal(b, zg)
+    with pytest.raises(ValueError):
+        shard.pack_solver_consts(zl, zg[:5])
+
+
+def _bcast(rank, world):
+    from rtg import assets
+    zl = torch.from_numpy(assets.local_translation("vtrdyn_full")) if rank == 0 else None
+    zg = torch.arange(177, dtype=torch.float32).reshape(59, 3) if rank == 0 else None
+    a, b = shard.broadcast_solver_consts(zl, zg, max_joints=64, device=torch.device("cpu"))
+    return a.numpy(), b.numpy()
+
+
+def test_broadcast_solver_consts_world2():
+    from rtg import assets
+    res = _run(_bcast)
+    for r in (0, 1):
+        np.testing.assert_array_equal(res[r][0], assets.local_translation("vtrdyn_full"))
+        np.testing.assert_array_equal(res[r][1], np.arange(177, dtype=np.float32).reshape(59, 3))
+
+
+def _gather_ragged(rank, world):
+    total = 11
+    start, count = shard.shard_range(total, world, rank)
+    full = torch.arange(total * 30, dtype=torch.float32).reshape(total, 30)
+    mine = full[start:start + count].clone()
+    counts = [shard.shard_range(total, world, r)[1] for r in range(world)]
+    out = shard.gather_shards(mine, counts)
+    t = shard.max_over_ranks(float(rank + 1), torch.device("cpu"))
+    return (None if out is None else out.numpy()), t
+
+
+def test_gather_and_max_world2():
+    res = _run(_gather_ragged)
+    np.testing.assert_array_equal(res[0][0], np.arange(330, dtype=np.float32).reshape(11, 30))
+    assert res[1][0] is None
+    assert res[0][1] == res[1][1] == 2.0
+
+
+def _sharded_solve(rank, world):
+    """bench.py's data flow at world 2 with the oracle standing in for the device solver:
+    per-rank seeded shards, broadcast constants, local solve, gather -> identical to a 1-rank solve."""
+    import oracle as orc
+    from rtg import synth
+    zp = np.load(os.path.join(os.path.dirname(__file__), "golden", "zero_pose.npz"))
+    zl_t = torch.from_numpy(zp["vtrdyn_full_local_t"]) if rank == 0 else None
+    zg_t = torch.from_numpy(zp["vtrdyn_full_global_t"]) if rank == 0 else None
+    zl, zg = shard.broadcast_solver_consts(zl_t, zg_t, 64, torch.device("cpu"))
+    total = 37
+    body, lh, rh = synth.synth_full_body_inputs(total, seed=99)
+    start, count = shard.shard_range(total, world, rank)
+    sl = slice(start, start + count)
+    dof, _, _ = orc.full_body_pos(zl.numpy(), zg.numpy(), body[sl], lh[sl], rh[sl], True, want_rot=False)
+    counts = [shard.shard_range(total, world, r)[1] for r in range(world)]
+    out = shard.gather_shards(torch.from_numpy(np.ascontiguousarray(dof)), counts)
+    return None if out is None else out.numpy()
+
+
+def test_sharded_solve_matches_single_rank():
+    import oracle as orc
+    from rtg import synth
+    res = _run(_sharded_solve)
+    zp = np.load(os.path.join(os.path.dirname(__file__), "golden", "zero_pose.npz"))
+    body, lh, rh = synth.synth_full_body_inputs(37, seed=99)
+    ref, _, _ = orc.full_body_pos(zp["vtrdyn_full_local_t"], zp["vtrdyn_full_global_t"], body, lh, rh, True,
+                                  want_rot=False)
+    np.testing.assert_array_equal(res[0], ref)
