@@ -20,7 +20,9 @@ struct rtg_topology_s {
     int32_t *d_parents = nullptr;
     V *d_local_t = nullptr;
     Q *d_tree_quat = nullptr;
-    TopoView view() const { return TopoView{d_parents, d_local_t, d_tree_quat, J}; }
+    int32_t *d_sched = nullptr;
+    int32_t nslots = 0;
+    TopoView view() const { return TopoView{d_parents, d_local_t, d_tree_quat, d_sched, J, nslots}; }
 };
 
 struct rtg_solver_s {
@@ -107,10 +109,14 @@ int rtg_topology_create(const int32_t *parents, const float *local_t, const floa
     if (!t) return fail(RTG_ERR_OUT_OF_MEMORY, "rtg_topology_create: host allocation failed");
     t->J = J;
     Q *tq = new (std::nothrow) Q[J];
-    if (!tq) {
+    int32_t *sched = new (std::nothrow) int32_t[J];
+    if (!tq || !sched) {
+        delete[] tq;
+        delete[] sched;
         delete t;
         return fail(RTG_ERR_OUT_OF_MEMORY, "rtg_topology_create: host allocation failed");
     }
+    t->nslots = fk_schedule(parents, J, sched);
     for (int j = 0; j < J; ++j)
         tq[j] = tree_quat ? Q{tree_quat[4 * j], tree_quat[4 * j + 1], tree_quat[4 * j + 2], tree_quat[4 * j + 3]}
                           : Q{0.f, 0.f, 0.f, 1.f};
@@ -122,11 +128,16 @@ int rtg_topology_create(const int32_t *parents, const float *local_t, const floa
     if (rc == RTG_OK)
         rc = hip_check(hipMemcpy(t->d_local_t, local_t, sizeof(V) * J, hipMemcpyHostToDevice), "hipMemcpy");
     if (rc == RTG_OK) rc = hip_check(hipMemcpy(t->d_tree_quat, tq, sizeof(Q) * J, hipMemcpyHostToDevice), "hipMemcpy");
+    if (rc == RTG_OK) rc = hip_check(hipMalloc(&t->d_sched, sizeof(int32_t) * J), "hipMalloc(sched)");
+    if (rc == RTG_OK)
+        rc = hip_check(hipMemcpy(t->d_sched, sched, sizeof(int32_t) * J, hipMemcpyHostToDevice), "hipMemcpy");
     delete[] tq;
+    delete[] sched;
     if (rc != RTG_OK) {
         (void)hipFree(t->d_parents);
         (void)hipFree(t->d_local_t);
         (void)hipFree(t->d_tree_quat);
+        (void)hipFree(t->d_sched);
         delete t;
         return rc;
     }
@@ -140,6 +151,7 @@ int rtg_topology_destroy(rtg_topology_t t)
     (void)hipFree(t->d_parents);
     (void)hipFree(t->d_local_t);
     (void)hipFree(t->d_tree_quat);
+    (void)hipFree(t->d_sched);
     delete t;
     return RTG_OK;
 }

@@ -10,6 +10,13 @@
 // tile instead of 64 lanes writing 120-byte-strided rows.
 #include "rtg_kernels.cuh"
 
+#ifndef RTG_PREFETCH
+#define RTG_PREFETCH 0
+#endif
+#ifndef RTG_WAVE_TILE
+#define RTG_WAVE_TILE 0
+#endif
+
 namespace rtg {
 
 // ----------------------------------------------------------------------------
@@ -103,48 +110,81 @@ RTG_DEV void emit_euler_xyz(const Emit &E, Q local)   // quat_in_xyz_axis(q, 'XY
     E.link<L0 + 2>(eul[2]);
 }
 
-RTG_DEV float hand_x_mean(Q rot, const float *__restrict__ H, const int (&idx)[5])   // gripper x-spread
+RTG_DEV float hand_x_mean(Q rot, V h0, const V (&tip)[5])   // gripper x-spread
 {
-    const float h0 = qrotate(rot, ld3(H)).x;
-    return mean5(qrotate(rot, ld3(H + 3 * idx[0])).x - h0, qrotate(rot, ld3(H + 3 * idx[1])).x - h0,
-                 qrotate(rot, ld3(H + 3 * idx[2])).x - h0, qrotate(rot, ld3(H + 3 * idx[3])).x - h0,
-                 qrotate(rot, ld3(H + 3 * idx[4])).x - h0);
+    const float x0 = qrotate(rot, h0).x;
+    return mean5(qrotate(rot, tip[0]).x - x0, qrotate(rot, tip[1]).x - x0, qrotate(rot, tip[2]).x - x0,
+                 qrotate(rot, tip[3]).x - x0, qrotate(rot, tip[4]).x - x0);
+}
+RTG_DEV float hand_x_mean(Q rot, const float *__restrict__ H, const int (&idx)[5])
+{
+    const V tip[5] = {ld3(H + 3 * idx[0]), ld3(H + 3 * idx[1]), ld3(H + 3 * idx[2]), ld3(H + 3 * idx[3]),
+                      ld3(H + 3 * idx[4])};
+    return hand_x_mean(rot, ld3(H), tip);
+}
+
+// Pin a value in VGPRs at this point: every load feeding it is issued above
+// and waited for here, so the frame's inputs cost one memory latency instead
+// of one per first use deep inside the solver.
+RTG_DEV void pin(V &v) { asm volatile("" : "+v"(v.x), "+v"(v.y), "+v"(v.z)); }
+
+// The 32 input points VtrdynFullBodyPosRetargeter reads (body 10,11,13..20; per
+// hand 0 + the Kabsch points 2,6,10,14,17 + the tips 4,8,12,16,19).
+struct FbpIn {
+    V b10, b11, b13, b17, b18, b19, b20, b14, b15, b16;
+    V l0, lk[5], lt[5];
+    V r0, rk[5], rt[5];
+};
+RTG_DEV FbpIn load_fbp(const float *__restrict__ b, const float *__restrict__ L, const float *__restrict__ R)
+{
+    FbpIn I;
+    I.b10 = ld3(b + 30); I.b11 = ld3(b + 33); I.b13 = ld3(b + 39); I.b17 = ld3(b + 51);
+    I.b18 = ld3(b + 54); I.b19 = ld3(b + 57); I.b20 = ld3(b + 60);
+    I.b14 = ld3(b + 42); I.b15 = ld3(b + 45); I.b16 = ld3(b + 48);
+    constexpr int kp[5] = {2, 6, 10, 14, 17}, tp[5] = {4, 8, 12, 16, 19};
+    I.l0 = ld3(L); I.r0 = ld3(R);
+#pragma unroll
+    for (int i = 0; i < 5; ++i) {
+        I.lk[i] = ld3(L + 3 * kp[i]); I.lt[i] = ld3(L + 3 * tp[i]);
+        I.rk[i] = ld3(R + 3 * kp[i]); I.rt[i] = ld3(R + 3 * tp[i]);
+    }
+#if RTG_PREFETCH
+    pin(I.b10); pin(I.b11); pin(I.b13); pin(I.b17); pin(I.b18); pin(I.b19); pin(I.b20);
+    pin(I.b14); pin(I.b15); pin(I.b16); pin(I.l0); pin(I.r0);
+#pragma unroll
+    for (int i = 0; i < 5; ++i) { pin(I.lk[i]); pin(I.lt[i]); pin(I.rk[i]); pin(I.rt[i]); }
+#endif
+    return I;
 }
 
 // VtrdynFullBodyPosRetargeter.retarget  full_body_pos_retargeter.py:25-217
 template <bool PRECISE>
-RTG_DEV void solve_full_body_pos(const SolverConsts &C, const float *__restrict__ b, const float *__restrict__ L,
-                                 const float *__restrict__ R, const Emit &E, float *__restrict__ body_rot)
+RTG_DEV void solve_full_body_pos(const SolverConsts &C, const FbpIn &I, const Emit &E, float *__restrict__ body_rot)
 {
     // _retarget_arm_from_global_translation :61-118
     Q R10;
     {
-        const V b10 = ld3(b + 30);
-        const V Mt[3] = {vsub(ld3(b + 51), b10), vsub(ld3(b + 39), b10), vsub(ld3(b + 33), b10)};
+        const V Mt[3] = {vsub(I.b17, I.b10), vsub(I.b13, I.b10), vsub(I.b11, I.b10)};
         R10 = cal_joint_quat<3>(C.Zt, Mt);
     }
-    const V b19 = ld3(b + 57), b15 = ld3(b + 45);
-    const Q chainL = solve_arm<12>(E, vsub(b19, ld3(b + 54)), vsub(ld3(b + 60), b19), C.lsh, C.lel, R10);
-    const Q chainR = solve_arm<21>(E, vsub(b15, ld3(b + 42)), vsub(ld3(b + 48), b15), C.rsh, C.rel, R10);
+    const Q chainL = solve_arm<12>(E, vsub(I.b19, I.b18), vsub(I.b20, I.b19), C.lsh, C.lel, R10);
+    const Q chainR = solve_arm<21>(E, vsub(I.b15, I.b14), vsub(I.b16, I.b15), C.rsh, C.rel, R10);
     // _retarget_wrist_from_global_translation :120-175
     Q WL, WR;
     {
-        const V l0 = ld3(L);
-        const V Ml[5] = {vsub(ld3(L + 6), l0), vsub(ld3(L + 18), l0), vsub(ld3(L + 30), l0), vsub(ld3(L + 42), l0),
-                         vsub(ld3(L + 51), l0)};
+        const V Ml[5] = {vsub(I.lk[0], I.l0), vsub(I.lk[1], I.l0), vsub(I.lk[2], I.l0), vsub(I.lk[3], I.l0),
+                         vsub(I.lk[4], I.l0)};
         WL = cal_joint_quat<5>(C.Zl, Ml);
     }
     emit_euler_xyz<16>(E, qmul_norm(qconj(qmul_norm(R10, chainL)), WL));
     {
-        const V r0 = ld3(R);
-        const V Mr[5] = {vsub(ld3(R + 6), r0), vsub(ld3(R + 18), r0), vsub(ld3(R + 30), r0), vsub(ld3(R + 42), r0),
-                         vsub(ld3(R + 51), r0)};
+        const V Mr[5] = {vsub(I.rk[0], I.r0), vsub(I.rk[1], I.r0), vsub(I.rk[2], I.r0), vsub(I.rk[3], I.r0),
+                         vsub(I.rk[4], I.r0)};
         WR = cal_joint_quat<5>(C.Zr, Mr);
     }
     emit_euler_xyz<25>(E, qmul_norm(qconj(qmul_norm(R10, chainR)), WR));
     // _retarget_gripper :177-217 -- hand points in the wrist frame (rotate by conj(W))
-    constexpr int tips[5] = {4, 8, 12, 16, 19};
-    const float la = hand_x_mean(qconj(WL), L, tips), ra = hand_x_mean(qconj(WR), R, tips);
+    const float la = hand_x_mean(qconj(WL), I.l0, I.lt), ra = hand_x_mean(qconj(WR), I.r0, I.rt);
     if (PRECISE) {
         const float ls = clamp_lohi(la / C.orig - 0.5f, 0.0f, 0.5f) / 0.5f;
         const float rs = clamp_lohi(ra / C.orig - 0.5f, 0.0f, 0.5f) / 0.5f;
@@ -237,13 +277,12 @@ __global__ __launch_bounds__(kSolverBlock) void k_retarget(SolverConsts C, const
                                                            float *__restrict__ body_rot)
 {
     __shared__ float sdof[kSolverBlock * kDofStride];
-    const int64_t f0 = (int64_t)blockIdx.x * kSolverBlock;
-    const int64_t f = f0 + threadIdx.x;
+    const int64_t f = (int64_t)blockIdx.x * kSolverBlock + threadIdx.x;
     if (f < B) {
         const Emit E{sdof + threadIdx.x * kDofStride, local_rot ? local_rot + f * 124 : nullptr};
         emit_fixed_links(E);
         if (KIND == RTG_SOLVER_FULL_BODY_POS)
-            solve_full_body_pos<PRECISE>(C, in0 + f * 63, in1 + f * 60, in2 + f * 60, E,
+            solve_full_body_pos<PRECISE>(C, load_fbp(in0 + f * 63, in1 + f * 60, in2 + f * 60), E,
                                          body_rot ? body_rot + f * 236 : nullptr);
         else if (KIND == RTG_SOLVER_UPPER_BODY)
             solve_upper_body(C, in0 + f * 63, E);
@@ -252,9 +291,34 @@ __global__ __launch_bounds__(kSolverBlock) void k_retarget(SolverConsts C, const
         else
             solve_body_rot(C, in0 + f * 84, E);
     }
+#if RTG_WAVE_TILE
+    // Each wave stores its own 64-row tile: LDS traffic of one wave is processed
+    // in order, so a wavefront-scope fence (no block barrier) orders the rows
+    // other lanes wrote before this lane reads them; waves never wait for each other.
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int64_t f0 = (int64_t)blockIdx.x * kSolverBlock + wave * 64;
+    const float *tile = sdof + wave * 64 * kDofStride;
+    const int64_t nrows = (B - f0) < 64 ? (B - f0) : 64;
+    const int nvals = nrows > 0 ? (int)nrows * 30 : 0;
+    float *dst = dof + f0 * 30;
+    auto lds_at = [&](int i) {
+        const int r = i / 30;
+        return tile[r * kDofStride + (i - r * 30)];
+    };
+    const int nvec = nvals >> 2;
+    for (int v = lane; v < nvec; v += 64) {
+        const int i = v << 2;
+        *reinterpret_cast<float4 *>(dst + i) = make_float4(lds_at(i), lds_at(i + 1), lds_at(i + 2), lds_at(i + 3));
+    }
+    for (int i = (nvec << 2) + lane; i < nvals; i += 64) dst[i] = lds_at(i);
+#else
     __syncthreads();
     // coalesced store of the block's contiguous DOF tile: rows [f0, min(B, f0+256)) x 30.
     // f0*120 B is 16-byte aligned, so the tile goes out as dwordx4 (full-line writes).
+    const int64_t f0 = (int64_t)blockIdx.x * kSolverBlock;
     const int64_t nrows = (B - f0) < kSolverBlock ? (B - f0) : kSolverBlock;
     const int nvals = (int)nrows * 30;
     float *dst = dof + f0 * 30;
@@ -268,6 +332,7 @@ __global__ __launch_bounds__(kSolverBlock) void k_retarget(SolverConsts C, const
         *reinterpret_cast<float4 *>(dst + i) = make_float4(lds_at(i), lds_at(i + 1), lds_at(i + 2), lds_at(i + 3));
     }
     for (int i = (nvec << 2) + threadIdx.x; i < nvals; i += kSolverBlock) dst[i] = lds_at(i);
+#endif
 }
 
 // ----------------------------------------------------------------------------
@@ -332,122 +397,172 @@ __global__ __launch_bounds__(256) void k_local_rotation(TopoView T, const float 
 }
 
 // ----------------------------------------------------------------------------
-// LDS-tiled FK (the production path).  One wave = one tile of 64 consecutive
-// frames.  The tile's local rotations are one contiguous span of global memory,
-// copied into LDS with dwordx4 loads (the LDS image has the global layout, so no
-// index math; with odd J the per-frame pitch J*4 dwords keeps the lanes'
-// ds_read_b128 conflict-free).  Each lane then walks its frame's chain in LDS:
-// the global rotation of joint j overwrites its local rotation in place (joint
-// j's parent p < j is already global), positions go to a second LDS image, and
-// both images are stored back as contiguous dwordx4 spans.
-// LDS: 64 * J * 28 bytes (Hu 55.5 KiB, VTRDYN_FULL 106 KiB).
+// Streaming FK (the production path).  One wave = one tile of 64 consecutive
+// frames, walked in chunks of kFkChunk joints:
+//   1. the chunk's local rotations -- kFkChunk*16 contiguous bytes per frame --
+//      are copied into an LDS window with dwordx4 loads (8 lanes per frame
+//      row: 128-byte segments);
+//   2. each lane composes its own frame's joints in index order, keeping the
+//      previous joint's global transform in registers; a parent that is not
+//      j-1 comes from an LDS slot (fk_schedule);
+//   3. the window -- global rotations written over the locals in place, and
+//      positions -- goes back out as 128- / 96-byte row segments.
+// LDS per wave: 9.2 KiB rotation window (row pitch 9 float4: ds_read_b128
+// conflict-free) + 6.4 KiB position window (odd pitch 25) + 1.8 KiB per slot,
+// ~19 KiB for every shipped skeleton, i.e. 8 waves per CU whatever J is.
 // ----------------------------------------------------------------------------
 constexpr int kFkTile = 64;
+constexpr int kFkChunk = 8;
+constexpr int kRotPitch = 4 * (kFkChunk + 1);   // floats per frame row (LDS)
+constexpr int kPosPitch = 3 * kFkChunk + 1;
 
-RTG_DEV void copy_span_to_lds(float *__restrict__ dst, const float *__restrict__ src, int n)   // n floats
+static inline size_t fk_stream_lds_bytes(int nslots)
 {
-    const int nv = n >> 2;
-    const bool aligned = ((reinterpret_cast<uintptr_t>(src) & 15) == 0);
-    if (aligned) {
-        for (int v = threadIdx.x; v < nv; v += kFkTile)
-            reinterpret_cast<float4 *>(dst)[v] = reinterpret_cast<const float4 *>(src)[v];
-        for (int i = (nv << 2) + threadIdx.x; i < n; i += kFkTile) dst[i] = src[i];
-    } else {
-        for (int i = threadIdx.x; i < n; i += kFkTile) dst[i] = src[i];
+    return sizeof(float) * ((size_t)kFkTile * (kRotPitch + kPosPitch) + (size_t)nslots * 7 * kFkTile);
+}
+
+// Copy the chunk [c0, c0+nC) of rows f0.. (nfr frames, row length J joints of W floats) between global and
+// an LDS window of pitch `pitch` floats per frame.  Lane v handles (frame v / kFkChunk, joint v % kFkChunk).
+template <int W, bool TO_LDS>
+RTG_DEV void chunk_copy(float *lds, int pitch, float *g, int64_t f0, int nfr, int J, int c0, int nC)
+{
+#pragma unroll
+    for (int it = 0; it < kFkChunk; ++it) {
+        const int v = it * kFkTile + (int)threadIdx.x;
+        const int fr = v / kFkChunk, k = v % kFkChunk;
+        if (fr < nfr && k < nC) {
+            float *gp = g + ((f0 + fr) * J + c0 + k) * W;
+            float *lp = lds + fr * pitch + k * W;
+            if (W == 4) {
+                if (TO_LDS) *reinterpret_cast<float4 *>(lp) = *reinterpret_cast<const float4 *>(gp);
+                else *reinterpret_cast<float4 *>(gp) = *reinterpret_cast<const float4 *>(lp);
+            } else {
+#pragma unroll
+                for (int c = 0; c < W; ++c) {
+                    if (TO_LDS) lp[c] = gp[c];
+                    else gp[c] = lp[c];
+                }
+            }
+        }
     }
 }
-RTG_DEV void copy_span_from_lds(float *__restrict__ dst, const float *__restrict__ src, int n)
+
+RTG_DEV void slot_put(float *slots, int s, Q q, V t)
 {
-    const int nv = n >> 2;
-    const bool aligned = ((reinterpret_cast<uintptr_t>(dst) & 15) == 0);
-    if (aligned) {
-        for (int v = threadIdx.x; v < nv; v += kFkTile)
-            reinterpret_cast<float4 *>(dst)[v] = reinterpret_cast<const float4 *>(src)[v];
-        for (int i = (nv << 2) + threadIdx.x; i < n; i += kFkTile) dst[i] = src[i];
-    } else {
-        for (int i = threadIdx.x; i < n; i += kFkTile) dst[i] = src[i];
-    }
+    float *p = slots + s * 7 * kFkTile + threadIdx.x;
+    p[0] = q.x; p[kFkTile] = q.y; p[2 * kFkTile] = q.z; p[3 * kFkTile] = q.w;
+    p[4 * kFkTile] = t.x; p[5 * kFkTile] = t.y; p[6 * kFkTile] = t.z;
+}
+RTG_DEV void slot_get(const float *slots, int s, Q &q, V &t)
+{
+    const float *p = slots + s * 7 * kFkTile + threadIdx.x;
+    q = Q{p[0], p[kFkTile], p[2 * kFkTile], p[3 * kFkTile]};
+    t = V{p[4 * kFkTile], p[5 * kFkTile], p[6 * kFkTile]};
 }
 
 template <bool STATE>
-RTG_DEV void fk_tile(const TopoView &T, const float *__restrict__ local_rot, const float *__restrict__ root_t,
-                     int64_t B, int64_t f0, float *__restrict__ g_rot, float *__restrict__ g_pos, float *lds)
+RTG_DEV void fk_stream_tile(const TopoView &T, const float *__restrict__ local_rot, const float *__restrict__ root_t,
+                            int64_t B, int64_t f0, float *__restrict__ g_rot, float *__restrict__ g_pos, float *lds)
 {
     const int J = T.J;
     const int nfr = (int)((B - f0) < kFkTile ? (B - f0) : kFkTile);
-    float *rot = lds;                          // [nfr][J][4]
-    float *pos = lds + kFkTile * J * 4;        // [nfr][J][3]
-    copy_span_to_lds(rot, local_rot + f0 * J * 4, nfr * J * 4);
-    __syncthreads();
-    const int f = threadIdx.x;
-    if (f < nfr) {
-        float *R = rot + f * J * 4;
-        float *P = pos + f * J * 3;
-        Q g = Q{R[0], R[1], R[2], R[3]};       // root: global = local, unnormalised (kinematics.py:27-29)
-        V t = ld3(root_t + (f0 + f) * 3);
-        P[0] = t.x; P[1] = t.y; P[2] = t.z;
-        for (int j = 1; j < J; ++j) {
-            const int p = T.parents[j];
-            if (p != j - 1) {
-                g = Q{R[4 * p], R[4 * p + 1], R[4 * p + 2], R[4 * p + 3]};
-                t = V{P[3 * p], P[3 * p + 1], P[3 * p + 2]};
+    float *rot = lds;                                   // [64][kRotPitch]
+    float *pos = lds + kFkTile * kRotPitch;             // [64][kPosPitch]
+    float *slots = pos + kFkTile * kPosPitch;           // [nslots][7][64]
+    const int lane = threadIdx.x;
+    const bool active = lane < nfr;
+    Q g = qident();
+    V t = V{0.0f, 0.0f, 0.0f};
+    for (int c0 = 0; c0 < J; c0 += kFkChunk) {
+        const int nC = (J - c0) < kFkChunk ? (J - c0) : kFkChunk;
+        chunk_copy<4, true>(rot, kRotPitch, const_cast<float *>(local_rot), f0, nfr, J, c0, nC);
+        __syncthreads();
+        if (active) {
+            float *R = rot + lane * kRotPitch;
+            float *P = pos + lane * kPosPitch;
+            for (int k = 0; k < nC; ++k) {
+                const int j = c0 + k;
+                const int32_t sc = T.sched[j];
+                Q lq = Q{R[4 * k], R[4 * k + 1], R[4 * k + 2], R[4 * k + 3]};
+                Q ng;
+                V nt;
+                if (j == 0) {   // root: global = local, unnormalised (kinematics.py:27-29)
+                    ng = lq;
+                    nt = ld3(root_t + (f0 + lane) * 3);
+                } else {
+                    if ((sc & 0xFF) != kNoSlot) slot_get(slots, sc & 0xFF, g, t);
+                    if (STATE) lq = qmul_norm(T.tree_quat[j], lq);   // skeleton3d.py:412-418
+                    const V rv = qrotate(g, T.local_t[j]);
+                    ng = qmul_norm(g, lq);
+                    nt = V{rv.x + t.x, rv.y + t.y, rv.z + t.z};
+                }
+                R[4 * k] = ng.x; R[4 * k + 1] = ng.y; R[4 * k + 2] = ng.z; R[4 * k + 3] = ng.w;
+                P[3 * k] = nt.x; P[3 * k + 1] = nt.y; P[3 * k + 2] = nt.z;
+                if (((sc >> 8) & 0xFF) != kNoSlot) slot_put(slots, (sc >> 8) & 0xFF, ng, nt);
+                g = ng;
+                t = nt;
             }
-            Q lq = Q{R[4 * j], R[4 * j + 1], R[4 * j + 2], R[4 * j + 3]};
-            if (STATE) lq = qmul_norm(T.tree_quat[j], lq);
-            const V rv = qrotate(g, T.local_t[j]);
-            const Q ng = qmul_norm(g, lq);
-            const V nt = V{rv.x + t.x, rv.y + t.y, rv.z + t.z};
-            R[4 * j] = ng.x; R[4 * j + 1] = ng.y; R[4 * j + 2] = ng.z; R[4 * j + 3] = ng.w;
-            P[3 * j] = nt.x; P[3 * j + 1] = nt.y; P[3 * j + 2] = nt.z;
-            g = ng;
-            t = nt;
         }
+        __syncthreads();
+        chunk_copy<4, false>(rot, kRotPitch, g_rot, f0, nfr, J, c0, nC);
+        chunk_copy<3, false>(pos, kPosPitch, g_pos, f0, nfr, J, c0, nC);
+        __syncthreads();
     }
-    __syncthreads();
-    copy_span_from_lds(g_rot + f0 * J * 4, rot, nfr * J * 4);
-    copy_span_from_lds(g_pos + f0 * J * 3, pos, nfr * J * 3);
 }
 
 template <bool STATE>
-__global__ __launch_bounds__(kFkTile) void k_fk_tiled(TopoView T, const float *__restrict__ local_rot,
-                                                      const float *__restrict__ root_t, int64_t B,
-                                                      float *__restrict__ g_rot, float *__restrict__ g_pos)
+__global__ __launch_bounds__(kFkTile) void k_fk_stream(TopoView T, const float *__restrict__ local_rot,
+                                                       const float *__restrict__ root_t, int64_t B,
+                                                       float *__restrict__ g_rot, float *__restrict__ g_pos)
 {
     extern __shared__ __attribute__((aligned(16))) float fk_lds[];
-    fk_tile<STATE>(T, local_rot, root_t, B, (int64_t)blockIdx.x * kFkTile, g_rot, g_pos, fk_lds);
+    fk_stream_tile<STATE>(T, local_rot, root_t, B, (int64_t)blockIdx.x * kFkTile, g_rot, g_pos, fk_lds);
 }
 
-// inverse FK, tiled the same way: input image -> per-lane chain -> output image
+// inverse FK, streamed the same way: local[j] = normalise(conj(g[p]) * g[j]) (kinematics.py:41-63).
+// The previous joint's global rotation stays in registers; branch parents come from slots.
 template <bool STATE>
-__global__ __launch_bounds__(kFkTile) void k_local_rotation_tiled(TopoView T, const float *__restrict__ g_rot,
-                                                                  int64_t B, float *__restrict__ local_rot)
+__global__ __launch_bounds__(kFkTile) void k_local_rotation_stream(TopoView T, const float *__restrict__ g_rot,
+                                                                   int64_t B, float *__restrict__ local_rot)
 {
     extern __shared__ __attribute__((aligned(16))) float fk_lds[];
     const int J = T.J;
     const int64_t f0 = (int64_t)blockIdx.x * kFkTile;
     const int nfr = (int)((B - f0) < kFkTile ? (B - f0) : kFkTile);
-    float *gin = fk_lds;                   // [nfr][J][4]
-    float *lout = fk_lds + kFkTile * J * 4;
-    copy_span_to_lds(gin, g_rot + f0 * J * 4, nfr * J * 4);
-    __syncthreads();
-    const int f = threadIdx.x;
-    if (f < nfr) {
-        const float *G = gin + f * J * 4;
-        float *L = lout + f * J * 4;
-        L[0] = G[0]; L[1] = G[1]; L[2] = G[2]; L[3] = G[3];
-        for (int j = 1; j < J; ++j) {
-            const int p = T.parents[j];
-            Q q = qmul_norm(qconj(Q{G[4 * p], G[4 * p + 1], G[4 * p + 2], G[4 * p + 3]}),
-                            Q{G[4 * j], G[4 * j + 1], G[4 * j + 2], G[4 * j + 3]});
-            if (STATE) q = qmul_norm(qnormalize(qconj(T.tree_quat[j])), q);
-            L[4 * j] = q.x; L[4 * j + 1] = q.y; L[4 * j + 2] = q.z; L[4 * j + 3] = q.w;
+    float *win = fk_lds;                                 // [64][kRotPitch]
+    float *slots = fk_lds + kFkTile * (kRotPitch + kPosPitch);
+    const int lane = threadIdx.x;
+    Q prev = qident();
+    V unused = V{0.0f, 0.0f, 0.0f};
+    for (int c0 = 0; c0 < J; c0 += kFkChunk) {
+        const int nC = (J - c0) < kFkChunk ? (J - c0) : kFkChunk;
+        chunk_copy<4, true>(win, kRotPitch, const_cast<float *>(g_rot), f0, nfr, J, c0, nC);
+        __syncthreads();
+        if (lane < nfr) {
+            float *W = win + lane * kRotPitch;
+            for (int k = 0; k < nC; ++k) {
+                const int j = c0 + k;
+                const int32_t sc = T.sched[j];
+                const Q gj = Q{W[4 * k], W[4 * k + 1], W[4 * k + 2], W[4 * k + 3]};
+                Q q = gj;   // root copied (kinematics.py:49)
+                if (j > 0) {
+                    Q gp = prev;
+                    if ((sc & 0xFF) != kNoSlot) slot_get(slots, sc & 0xFF, gp, unused);
+                    q = qmul_norm(qconj(gp), gj);
+                    if (STATE) q = qmul_norm(qnormalize(qconj(T.tree_quat[j])), q);   // skeleton3d.py:470-478
+                }
+                if (((sc >> 8) & 0xFF) != kNoSlot) slot_put(slots, (sc >> 8) & 0xFF, gj, unused);
+                W[4 * k] = q.x; W[4 * k + 1] = q.y; W[4 * k + 2] = q.z; W[4 * k + 3] = q.w;
+                prev = gj;
+            }
         }
+        __syncthreads();
+        chunk_copy<4, false>(win, kRotPitch, local_rot, f0, nfr, J, c0, nC);
+        __syncthreads();
     }
-    __syncthreads();
-    copy_span_from_lds(local_rot + f0 * J * 4, lout, nfr * J * 4);
 }
 
-__global__ __launch_bounds__(kFkTile) void k_fk_multi_tiled(FkMultiArgs A)
+__global__ __launch_bounds__(kFkTile) void k_fk_multi_stream(FkMultiArgs A)
 {
     extern __shared__ __attribute__((aligned(16))) float fk_lds[];
     int s = 0;
@@ -455,8 +570,41 @@ __global__ __launch_bounds__(kFkTile) void k_fk_multi_tiled(FkMultiArgs A)
     for (int i = 1; i < RTG_MAX_SEGMENTS; ++i)
         if (i < A.n && (int64_t)blockIdx.x >= A.block_start[i]) s = i;
     const FkSeg &S = A.seg[s];
-    fk_tile<false>(S.T, S.local_rot, S.root_t, S.B, ((int64_t)blockIdx.x - A.block_start[s]) * kFkTile, S.g_rot,
-                   S.g_pos, fk_lds);
+    fk_stream_tile<false>(S.T, S.local_rot, S.root_t, S.B, ((int64_t)blockIdx.x - A.block_start[s]) * kFkTile,
+                          S.g_rot, S.g_pos, fk_lds);
+}
+
+int32_t fk_schedule(const int32_t *parents, int32_t J, int32_t *sched)
+{
+    // last non-consecutive child of every branch parent
+    int32_t *last = new int32_t[J];
+    int32_t *slot_of = new int32_t[J];
+    for (int j = 0; j < J; ++j) last[j] = slot_of[j] = -1;
+    for (int k = 1; k < J; ++k)
+        if (parents[k] != k - 1) last[parents[k]] = k;
+    uint32_t used = 0;   // bitmask of live slots (the schedule is only used when nslots <= kMaxFkSlots)
+    int32_t nslots = 0, overflow = 0;
+    for (int j = 0; j < J; ++j) {
+        int32_t ld = kNoSlot, sv = kNoSlot;
+        const int p = j > 0 ? parents[j] : -1;
+        if (j > 0 && p != j - 1) {
+            ld = slot_of[p];
+            if (last[p] == j && ld >= 0 && ld < 32) used &= ~(1u << ld);   // free after this read
+        }
+        if (last[j] >= 0) {
+            int s = 0;
+            while (s < 32 && (used >> s) & 1u) ++s;
+            if (s >= 32) { overflow = 1; s = 31; }
+            used |= 1u << s;
+            slot_of[j] = s;
+            sv = s;
+            nslots = s + 1 > nslots ? s + 1 : nslots;
+        }
+        sched[j] = (ld & 0xFF) | ((sv & 0xFF) << 8);
+    }
+    delete[] last;
+    delete[] slot_of;
+    return overflow ? 1 << 30 : nslots;
 }
 
 __global__ __launch_bounds__(256) void k_fk_multi(FkMultiArgs A)
@@ -777,21 +925,15 @@ hipError_t launch_retarget(int kind, int precise, const SolverConsts &C, const f
     return hipGetLastError();
 }
 
-static inline size_t fk_lds_bytes(int J) { return (size_t)kFkTile * J * 28; }
-constexpr size_t kMaxLds = 160 * 1024;
-// A shared multi-segment launch sizes LDS for its largest skeleton; above 64 KiB
-// per wave the smaller skeletons lose more occupancy than the tiling gains.
-constexpr size_t kMaxMultiLds = 64 * 1024;
-
 hipError_t launch_fk(const TopoView &T, bool state, const float *lr, const float *rt, int64_t B, float *gr, float *gp,
                      hipStream_t s)
 {
-    const size_t lds = fk_lds_bytes(T.J);
-    if (lds <= kMaxLds) {
+    if (T.nslots <= kMaxFkSlots) {
         const dim3 g(grid_for(B, kFkTile)), b(kFkTile);
-        if (state) hipLaunchKernelGGL(k_fk_tiled<true>, g, b, lds, s, T, lr, rt, B, gr, gp);
-        else hipLaunchKernelGGL(k_fk_tiled<false>, g, b, lds, s, T, lr, rt, B, gr, gp);
-    } else if (state) {
+        const size_t lds = fk_stream_lds_bytes(T.nslots);
+        if (state) hipLaunchKernelGGL(k_fk_stream<true>, g, b, lds, s, T, lr, rt, B, gr, gp);
+        else hipLaunchKernelGGL(k_fk_stream<false>, g, b, lds, s, T, lr, rt, B, gr, gp);
+    } else if (state) {   // pathological branching (> kMaxFkSlots live branch parents): lane-walk kernel
         hipLaunchKernelGGL(k_fk<true>, dim3(grid_for(B, 256)), dim3(256), 0, s, T, lr, rt, B, gr, gp);
     } else {
         hipLaunchKernelGGL(k_fk<false>, dim3(grid_for(B, 256)), dim3(256), 0, s, T, lr, rt, B, gr, gp);
@@ -801,11 +943,11 @@ hipError_t launch_fk(const TopoView &T, bool state, const float *lr, const float
 
 hipError_t launch_local_rotation(const TopoView &T, bool state, const float *g, int64_t B, float *l, hipStream_t s)
 {
-    const size_t lds = (size_t)kFkTile * T.J * 32;
-    if (lds <= kMaxLds) {
+    if (T.nslots <= kMaxFkSlots) {
         const dim3 gd(grid_for(B, kFkTile)), b(kFkTile);
-        if (state) hipLaunchKernelGGL(k_local_rotation_tiled<true>, gd, b, lds, s, T, g, B, l);
-        else hipLaunchKernelGGL(k_local_rotation_tiled<false>, gd, b, lds, s, T, g, B, l);
+        const size_t lds = fk_stream_lds_bytes(T.nslots);
+        if (state) hipLaunchKernelGGL(k_local_rotation_stream<true>, gd, b, lds, s, T, g, B, l);
+        else hipLaunchKernelGGL(k_local_rotation_stream<false>, gd, b, lds, s, T, g, B, l);
     } else if (state) {
         hipLaunchKernelGGL(k_local_rotation<true>, dim3(grid_for(B, 256)), dim3(256), 0, s, T, g, B, l);
     } else {
@@ -816,10 +958,10 @@ hipError_t launch_local_rotation(const TopoView &T, bool state, const float *g, 
 
 hipError_t launch_fk_multi(FkMultiArgs &A, hipStream_t s)
 {
-    int maxJ = 0;
-    for (int i = 0; i < A.n; ++i) maxJ = A.seg[i].T.J > maxJ ? A.seg[i].T.J : maxJ;
-    const bool tiled = fk_lds_bytes(maxJ) <= kMaxMultiLds;
-    const int per = tiled ? kFkTile : 256;
+    int maxS = 0;
+    for (int i = 0; i < A.n; ++i) maxS = A.seg[i].T.nslots > maxS ? A.seg[i].T.nslots : maxS;
+    const bool stream = maxS <= kMaxFkSlots;
+    const int per = stream ? kFkTile : 256;
     int64_t blocks = 0;
     for (int i = 0; i < A.n; ++i) {
         A.block_start[i] = blocks;
@@ -827,8 +969,8 @@ hipError_t launch_fk_multi(FkMultiArgs &A, hipStream_t s)
     }
     for (int i = A.n; i < RTG_MAX_SEGMENTS; ++i) A.block_start[i] = blocks;
     if (blocks == 0) return hipSuccess;
-    if (tiled)
-        hipLaunchKernelGGL(k_fk_multi_tiled, dim3((unsigned)blocks), dim3(kFkTile), fk_lds_bytes(maxJ), s, A);
+    if (stream)
+        hipLaunchKernelGGL(k_fk_multi_stream, dim3((unsigned)blocks), dim3(kFkTile), fk_stream_lds_bytes(maxS), s, A);
     else
         hipLaunchKernelGGL(k_fk_multi, dim3((unsigned)blocks), dim3(256), 0, s, A);
     return hipGetLastError();

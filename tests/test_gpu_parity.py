@@ -81,6 +81,58 @@ def test_fk_empty_and_single(gpu):
     np.testing.assert_array_equal(_np(gr), k["hu_v5_g_rot"][:1])
 
 
+def _random_tree(rng, J, kind):
+    """Parent arrays that stress the streaming-FK slot schedule: 'bushy' (random
+    earlier parents, many live branch points), 'star' (20 chains hanging off the
+    root, interleaved -> more live slots than the kernel keeps, lane-walk fallback),
+    'chain' (no branch points)."""
+    if kind == "chain":
+        return np.arange(-1, J - 1, dtype=np.int32)
+    if kind == "star":
+        par = np.empty(J, np.int32)
+        par[0] = -1
+        nch = 20
+        for j in range(1, J):
+            par[j] = 0 if j <= nch else j - nch   # chain c: 0 -> c -> c+20 -> ...
+        return par
+    par = np.empty(J, np.int32)
+    par[0] = -1
+    for j in range(1, J):
+        par[j] = rng.integers(0, j)
+    return par
+
+
+@pytest.mark.parametrize("kind,J", [("bushy", 31), ("bushy", 97), ("star", 81), ("chain", 17), ("chain", 1)])
+def test_fk_random_topologies_vs_oracle(gpu, kind, J):
+    """Any parent-indexed tree (parents[j] < j): FK, inverse FK and the state
+    variants agree bit for bit with the oracle, on ragged batch sizes."""
+    import oracle as orc
+    from rtg import ops
+    from rtg.runtime import Topology
+    rng = np.random.default_rng(J * 7 + len(kind))
+    par = _random_tree(rng, J, kind)
+    lt = rng.normal(0, 0.2, (J, 3)).astype(np.float32)
+    tq = ops.quat_normalize(rng.normal(size=(J, 4)).astype(np.float32))
+    tq = tq.cpu().numpy() if hasattr(tq, "cpu") else tq
+    T = Topology(par, lt, tq)
+    for B in (1, 63, 65, 1000):
+        lr = np.ascontiguousarray(rng.normal(size=(B, J, 4)).astype(np.float32))
+        rt = rng.normal(0, 0.3, (B, 3)).astype(np.float32)
+        gr, gp = ops.forward_kinematics(T, lr, rt)
+        ogr, ogp = orc.fk(par, lt, lr, rt)
+        np.testing.assert_array_equal(_np(gr), ogr)
+        np.testing.assert_array_equal(_np(gp), ogp)
+        np.testing.assert_array_equal(_np(ops.local_rotation(T, ogr)), orc.local_rotation(par, ogr))
+        nlr = _np(ops.quat_normalize(lr))
+        sgr, sgp = ops.forward_kinematics(T, nlr, rt, state=True)
+        osgr, osgp = orc.state_fk(par, tq, lt, nlr, rt)
+        np.testing.assert_array_equal(_np(sgr), osgr)
+        np.testing.assert_array_equal(_np(sgp), osgp)
+        ng = _np(ops.quat_normalize(osgr))
+        np.testing.assert_array_equal(_np(ops.local_rotation(T, ng, state=True)),
+                                      orc.state_local_rotation(par, tq, ng))
+
+
 # ----------------------------------------------------------------- primitives
 def test_quaternion_algebra_bit_exact(gpu):
     from rtg import ops
