@@ -31,6 +31,18 @@ RTG_DEV Q ld4(const float *__restrict__ p)
 RTG_DEV void st4(float *__restrict__ p, Q q) { *reinterpret_cast<float4 *>(p) = make_float4(q.x, q.y, q.z, q.w); }
 RTG_DEV void st3(float *__restrict__ p, V v) { p[0] = v.x; p[1] = v.y; p[2] = v.z; }
 
+// Launch-uniform tables (topology, schedule) read through the constant address
+// space: the compiler cannot prove them unclobbered in a kernel that stores to
+// global memory, so a plain load would be a vector load, and its s_waitcnt
+// vmcnt would also drain every prefetch in flight.  These become s_load (lgkmcnt).
+template <typename T>
+RTG_DEV T ld_const(const T *p)
+{
+    return *(const __attribute__((address_space(4))) T *)p;
+}
+RTG_DEV V ld_const(const V *p) { return V{ld_const(&p->x), ld_const(&p->y), ld_const(&p->z)}; }
+RTG_DEV Q ld_const(const Q *p) { return Q{ld_const(&p->x), ld_const(&p->y), ld_const(&p->z), ld_const(&p->w)}; }
+
 // ----------------------------------------------------------------------------
 // solver constants prep (1 thread): theta0 / phi0 of the four arm maps and the
 // gripper denominator, computed with exactly the per-frame device math.
@@ -421,28 +433,75 @@ static inline size_t fk_stream_lds_bytes(int nslots)
     return sizeof(float) * ((size_t)kFkTile * (kRotPitch + kPosPitch) + (size_t)nslots * 7 * kFkTile);
 }
 
-// Copy the chunk [c0, c0+nC) of rows f0.. (nfr frames, row length J joints of W floats) between global and
-// an LDS window of pitch `pitch` floats per frame.  Lane v handles (frame v / kFkChunk, joint v % kFkChunk).
-template <int W, bool TO_LDS>
-RTG_DEV void chunk_copy(float *lds, int pitch, float *g, int64_t f0, int nfr, int J, int c0, int nC)
+// A streaming tile is one wave, so ordering its LDS traffic needs no block
+// barrier: a wave's LDS instructions execute in issue order, and the
+// wavefront-scope fence + wave_barrier only stop the compiler from moving
+// memory operations across this point.  (__syncthreads would also make the
+// compiler drain every outstanding global store, s_waitcnt vmcnt(0), per chunk.)
+RTG_DEV void wave_sync()
 {
-#pragma unroll
-    for (int it = 0; it < kFkChunk; ++it) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+// Chunk [c0, c0+nC) of rows f0.. (nfr frames, J joints of W floats per row).
+// Lane v of iteration `it` handles (frame (it*64+v) / kFkChunk, joint % kFkChunk):
+// 8 lanes cover one frame's contiguous segment.
+// eight named registers (an indexed array of them is left in scratch by the compiler)
+struct ChunkRegs {
+    Q v0, v1, v2, v3, v4, v5, v6, v7;
+};
+#define RTG_REP8(X) X(0) X(1) X(2) X(3) X(4) X(5) X(6) X(7)
+RTG_DEV void chunk_load(ChunkRegs &r, const float *__restrict__ g, int64_t f0, int nfr, int J, int c0, int nC)
+{
+    // unconditional loads (lanes past the tile re-read the tile's first element)
+    // keep the prefetch registers fully defined across the chunk loop
+#define RTG_LD(I)                                                                          \
+    {                                                                                      \
+        const int v = (I) * kFkTile + (int)threadIdx.x;                                    \
+        const int fr = v / kFkChunk, k = v % kFkChunk;                                     \
+        const int64_t e = (fr < nfr && k < nC) ? (f0 + fr) * J + c0 + k : f0 * J;         \
+        r.v##I = ld4(g + e * 4);                                                           \
+    }
+    RTG_REP8(RTG_LD)
+#undef RTG_LD
+}
+RTG_DEV void chunk_to_lds(const ChunkRegs &r, float *lds, int nfr, int nC)
+{
+    const bool full = nfr == kFkTile && nC == kFkChunk;   // unpredicated: the writes issue back to back
+#define RTG_ST(I)                                                                          \
+    {                                                                                      \
+        const int v = (I) * kFkTile + (int)threadIdx.x;                                    \
+        const int fr = v / kFkChunk, k = v % kFkChunk;                                     \
+        if (full || (fr < nfr && k < nC)) st4(lds + fr * kRotPitch + k * 4, r.v##I);       \
+    }
+    RTG_REP8(RTG_ST)
+#undef RTG_ST
+}
+template <int W>
+RTG_DEV void chunk_store(float *__restrict__ g, const float *lds, int pitch, int64_t f0, int nfr, int J, int c0, int nC)
+{
+    auto one = [&](int it) {
         const int v = it * kFkTile + (int)threadIdx.x;
         const int fr = v / kFkChunk, k = v % kFkChunk;
-        if (fr < nfr && k < nC) {
-            float *gp = g + ((f0 + fr) * J + c0 + k) * W;
-            float *lp = lds + fr * pitch + k * W;
-            if (W == 4) {
-                if (TO_LDS) *reinterpret_cast<float4 *>(lp) = *reinterpret_cast<const float4 *>(gp);
-                else *reinterpret_cast<float4 *>(gp) = *reinterpret_cast<const float4 *>(lp);
-            } else {
+        float *gp = g + ((f0 + fr) * J + c0 + k) * W;
+        const float *lp = lds + fr * pitch + k * W;
+        if (W == 4) {
+            *reinterpret_cast<float4 *>(gp) = *reinterpret_cast<const float4 *>(lp);
+        } else {
 #pragma unroll
-                for (int c = 0; c < W; ++c) {
-                    if (TO_LDS) lp[c] = gp[c];
-                    else gp[c] = lp[c];
-                }
-            }
+            for (int c = 0; c < W; ++c) gp[c] = lp[c];
+        }
+    };
+    if (nfr == kFkTile && nC == kFkChunk) {   // full window: unpredicated, LDS reads batch ahead of the stores
+#pragma unroll
+        for (int it = 0; it < kFkChunk; ++it) one(it);
+    } else {
+#pragma unroll
+        for (int it = 0; it < kFkChunk; ++it) {
+            const int v = it * kFkTile + (int)threadIdx.x;
+            if (v / kFkChunk < nfr && v % kFkChunk < nC) one(it);
         }
     }
 }
@@ -473,26 +532,36 @@ RTG_DEV void fk_stream_tile(const TopoView &T, const float *__restrict__ local_r
     const bool active = lane < nfr;
     Q g = qident();
     V t = V{0.0f, 0.0f, 0.0f};
+    const V root = ld3(root_t + (f0 + (active ? lane : 0)) * 3);   // before the prefetches (vmcnt order)
+    ChunkRegs next;
+    chunk_load(next, local_rot, f0, nfr, J, 0, J < kFkChunk ? J : kFkChunk);
     for (int c0 = 0; c0 < J; c0 += kFkChunk) {
         const int nC = (J - c0) < kFkChunk ? (J - c0) : kFkChunk;
-        chunk_copy<4, true>(rot, kRotPitch, const_cast<float *>(local_rot), f0, nfr, J, c0, nC);
-        __syncthreads();
+        chunk_to_lds(next, rot, nfr, nC);
+        wave_sync();
+        if (c0 + kFkChunk < J)   // prefetch the next window while this one is composed
+            chunk_load(next, local_rot, f0, nfr, J, c0 + kFkChunk,
+                       (J - c0 - kFkChunk) < kFkChunk ? (J - c0 - kFkChunk) : kFkChunk);
         if (active) {
             float *R = rot + lane * kRotPitch;
             float *P = pos + lane * kPosPitch;
-            for (int k = 0; k < nC; ++k) {
+            // unrolled: the window's LDS reads and the topology's scalar loads are
+            // issued together at the chunk head instead of once per chained joint
+#pragma unroll
+            for (int k = 0; k < kFkChunk; ++k) {
+                if (k >= nC) break;
                 const int j = c0 + k;
-                const int32_t sc = T.sched[j];
+                const int32_t sc = ld_const(T.sched + j);
                 Q lq = Q{R[4 * k], R[4 * k + 1], R[4 * k + 2], R[4 * k + 3]};
                 Q ng;
                 V nt;
                 if (j == 0) {   // root: global = local, unnormalised (kinematics.py:27-29)
                     ng = lq;
-                    nt = ld3(root_t + (f0 + lane) * 3);
+                    nt = root;
                 } else {
                     if ((sc & 0xFF) != kNoSlot) slot_get(slots, sc & 0xFF, g, t);
-                    if (STATE) lq = qmul_norm(T.tree_quat[j], lq);   // skeleton3d.py:412-418
-                    const V rv = qrotate(g, T.local_t[j]);
+                    if (STATE) lq = qmul_norm(ld_const(T.tree_quat + j), lq);   // skeleton3d.py:412-418
+                    const V rv = qrotate(g, ld_const(T.local_t + j));
                     ng = qmul_norm(g, lq);
                     nt = V{rv.x + t.x, rv.y + t.y, rv.z + t.z};
                 }
@@ -503,10 +572,10 @@ RTG_DEV void fk_stream_tile(const TopoView &T, const float *__restrict__ local_r
                 t = nt;
             }
         }
-        __syncthreads();
-        chunk_copy<4, false>(rot, kRotPitch, g_rot, f0, nfr, J, c0, nC);
-        chunk_copy<3, false>(pos, kPosPitch, g_pos, f0, nfr, J, c0, nC);
-        __syncthreads();
+        wave_sync();
+        chunk_store<4>(g_rot, rot, kRotPitch, f0, nfr, J, c0, nC);
+        chunk_store<3>(g_pos, pos, kPosPitch, f0, nfr, J, c0, nC);
+        wave_sync();
     }
 }
 
@@ -534,31 +603,38 @@ __global__ __launch_bounds__(kFkTile) void k_local_rotation_stream(TopoView T, c
     const int lane = threadIdx.x;
     Q prev = qident();
     V unused = V{0.0f, 0.0f, 0.0f};
+    ChunkRegs next;
+    chunk_load(next, g_rot, f0, nfr, J, 0, J < kFkChunk ? J : kFkChunk);
     for (int c0 = 0; c0 < J; c0 += kFkChunk) {
         const int nC = (J - c0) < kFkChunk ? (J - c0) : kFkChunk;
-        chunk_copy<4, true>(win, kRotPitch, const_cast<float *>(g_rot), f0, nfr, J, c0, nC);
-        __syncthreads();
+        chunk_to_lds(next, win, nfr, nC);
+        wave_sync();
+        if (c0 + kFkChunk < J)
+            chunk_load(next, g_rot, f0, nfr, J, c0 + kFkChunk,
+                       (J - c0 - kFkChunk) < kFkChunk ? (J - c0 - kFkChunk) : kFkChunk);
         if (lane < nfr) {
             float *W = win + lane * kRotPitch;
-            for (int k = 0; k < nC; ++k) {
+#pragma unroll
+            for (int k = 0; k < kFkChunk; ++k) {
+                if (k >= nC) break;
                 const int j = c0 + k;
-                const int32_t sc = T.sched[j];
+                const int32_t sc = ld_const(T.sched + j);
                 const Q gj = Q{W[4 * k], W[4 * k + 1], W[4 * k + 2], W[4 * k + 3]};
                 Q q = gj;   // root copied (kinematics.py:49)
                 if (j > 0) {
                     Q gp = prev;
                     if ((sc & 0xFF) != kNoSlot) slot_get(slots, sc & 0xFF, gp, unused);
                     q = qmul_norm(qconj(gp), gj);
-                    if (STATE) q = qmul_norm(qnormalize(qconj(T.tree_quat[j])), q);   // skeleton3d.py:470-478
+                    if (STATE) q = qmul_norm(qnormalize(qconj(ld_const(T.tree_quat + j))), q);   // skeleton3d.py:470-478
                 }
                 if (((sc >> 8) & 0xFF) != kNoSlot) slot_put(slots, (sc >> 8) & 0xFF, gj, unused);
                 W[4 * k] = q.x; W[4 * k + 1] = q.y; W[4 * k + 2] = q.z; W[4 * k + 3] = q.w;
                 prev = gj;
             }
         }
-        __syncthreads();
-        chunk_copy<4, false>(win, kRotPitch, local_rot, f0, nfr, J, c0, nC);
-        __syncthreads();
+        wave_sync();
+        chunk_store<4>(local_rot, win, kRotPitch, f0, nfr, J, c0, nC);
+        wave_sync();
     }
 }
 

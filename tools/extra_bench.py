@@ -82,6 +82,10 @@ def fk():
     ms = time_events(lambda: ops.forward_kinematics(T, lr, rt))
     res["hu_fk_262144"] = {"ms": ms, "frames_per_s": B / (ms * 1e-3),
                            "GBs_algorithmic": 1376 * B / (ms * 1e-3) / 1e9}
+    g = ops.forward_kinematics(T, lr, rt)[0]
+    ms = time_events(lambda: ops.local_rotation(T, g))
+    res["hu_inverse_fk_262144"] = {"ms": ms, "frames_per_s": B / (ms * 1e-3),
+                                   "GBs_algorithmic": 31 * 32 * B / (ms * 1e-3) / 1e9}
     segs = []
     nbytes = 0
     for i, n in enumerate(["hu_v5", "vtrdyn", "vtrdyn_full", "noitom"]):
