@@ -16,6 +16,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include "rtg_crmath.h"
+
 #pragma clang fp contract(off)
 
 namespace rtg {
@@ -30,6 +32,15 @@ RTG_DEV float cr_sqrt(float x) { return __builtin_sqrtf(x); }   // IEEE sqrt (co
 RTG_DEV float cr_acos(float x) { return (float)::acos((double)x); }
 RTG_DEV float cr_sin(float x) { return (float)::sin((double)x); }
 RTG_DEV float cr_cos(float x) { return (float)::cos((double)x); }
+// sin and cos of one argument, correctly rounded: fast shared-reduction path
+// (rtg_crmath.h, exhaustively checked against glibc) with the libm f64 call as
+// the exact fallback for the ~1-in-10^7 values the rounding test declines.
+struct SC { float s, c; };
+RTG_DEV SC cr_sincos(double x)
+{
+    const crm::SinCos r = crm::crm_sincos(x);
+    return SC{r.s_ok ? r.s : (float)::sin(x), r.c_ok ? r.c : (float)::cos(x)};
+}
 RTG_DEV float tsign(float v) { return v > 0.0f ? 1.0f : (v < 0.0f ? -1.0f : 0.0f); }
 RTG_DEV float clamp_lo(float v, float lo) { return v < lo ? lo : v; }          // NaN passes through
 RTG_DEV float clamp_lohi(float v, float lo, float hi) { return v < lo ? lo : (v > hi ? hi : v); }
@@ -111,6 +122,18 @@ RTG_DEV float g_atan2f(float y, float x)
     return (z - pi_lo) - pi;
 }
 
+// atan2f with the finite non-zero case branch-free (rtg_crmath.h); special
+// operands take the branchy restatement above.
+RTG_DEV float f_atan2f(float y, float x)
+{
+    return crm::crm_atan2f_regular(y, x) ? crm::crm_atan2f_sel(y, x) : g_atan2f(y, x);
+}
+RTG_DEV float normalize_angle(float a)   // rotation3d.py:582-584: atan2(sin a, cos a)
+{
+    const SC t = cr_sincos((double)a);
+    return f_atan2f(t.s, t.c);
+}
+
 // ------------------------------------------------ quaternion algebra (rotation3d.py)
 RTG_DEV Q qmul(Q a, Q b)   // :14-27, each component a left fold of four products
 {
@@ -159,7 +182,8 @@ RTG_DEV Q qfrom_angle_axis(float angle, V axis)  // :122-143
     float n = cr_sqrt((axis.x * axis.x + axis.y * axis.y) + axis.z * axis.z);
     n = clamp_lo(n, 1e-9f);
     const float ax = axis.x / n, ay = axis.y / n, az = axis.z / n;
-    const float s = cr_sin(theta), c = cr_cos(theta);
+    const SC t = cr_sincos((double)theta);
+    const float s = t.s, c = t.c;
     return qnormalize(Q{ax * s, ay * s, az * s, c});
 }
 
@@ -198,7 +222,7 @@ RTG_DEV V qexp_map(Q q)
 {
     const float sin_theta = cr_sqrt(1.0f - q.w * q.w);
     float angle = 2.0f * cr_acos(q.w);
-    angle = g_atan2f(cr_sin(angle), cr_cos(angle));   // normalize_angle :582-584
+    angle = normalize_angle(angle);   // normalize_angle :582-584
     const bool mask = fabsf(sin_theta) > 1e-5f;
     const float a = mask ? angle : 0.0f;
     const float ax = mask ? q.x / sin_theta : 0.0f;
@@ -211,7 +235,7 @@ RTG_DEV Q qangle_axis(Q q)
 {
     const float sin_theta = cr_sqrt(1.0f - q.w * q.w);
     float angle = 2.0f * cr_acos(q.w);
-    angle = g_atan2f(cr_sin(angle), cr_cos(angle));
+    angle = normalize_angle(angle);
     const bool mask = fabsf(sin_theta) > 1e-5f;
     return Q{mask ? angle : 0.0f, mask ? q.x / sin_theta : 0.0f, mask ? q.y / sin_theta : 0.0f,
              mask ? q.z / sin_theta : 1.0f};
@@ -519,7 +543,8 @@ RTG_DEV void scipy_as_euler(Q qf, int s0, int s1, int s2, bool extrinsic, double
 RTG_DEV Q elementary_quat(int axis, double angle)
 {
     const double h = angle / 2.0;
-    const float s = (float)::sin(h), c = (float)::cos(h);
+    const SC t = cr_sincos(h);
+    const float s = t.s, c = t.c;
     return Q{axis == 0 ? s : 0.0f, axis == 1 ? s : 0.0f, axis == 2 ? s : 0.0f, c};
 }
 
