@@ -41,6 +41,13 @@ RTG_DEV SC cr_sincos(double x)
     const crm::SinCos r = crm::crm_sincos(x);
     return SC{r.s_ok ? r.s : (float)::sin(x), r.c_ok ? r.c : (float)::cos(x)};
 }
+// k float divisions by one denominator n: RN(a/n) == (float)((double)a * RN(1/(double)n))
+// for all f32 a, n.  (An f32 quotient is never within 2^-50 relative of an f32
+// rounding midpoint, and the f64 product is within 2^-52; checked on 4.3e9
+// random pairs incl. subnormals / zeros / infinities, tests/test_oracle_golden.py.)
+// One f64 reciprocal replaces k correctly rounded f32 divide sequences.
+RTG_DEV double rcp64(float n) { return 1.0 / (double)n; }
+RTG_DEV float mulr(float a, double r) { return (float)((double)a * r); }
 RTG_DEV float tsign(float v) { return v > 0.0f ? 1.0f : (v < 0.0f ? -1.0f : 0.0f); }
 RTG_DEV float clamp_lo(float v, float lo) { return v < lo ? lo : v; }          // NaN passes through
 RTG_DEV float clamp_lohi(float v, float lo, float hi) { return v < lo ? lo : (v > hi ? hi : v); }
@@ -153,21 +160,24 @@ RTG_DEV Q qnormalize(Q q)  // quat_unit(quat_pos(q)) :30-56,92-98
     q.x = f * q.x; q.y = f * q.y; q.z = f * q.z; q.w = f * q.w;
     float n = cr_sqrt(((q.x * q.x + q.y * q.y) + q.z * q.z) + q.w * q.w);
     n = clamp_lo(n, 1e-9f);
-    return Q{q.x / n, q.y / n, q.z / n, q.w / n};
+    const double r = rcp64(n);
+    return Q{mulr(q.x, r), mulr(q.y, r), mulr(q.z, r), mulr(q.w, r)};
 }
 RTG_DEV Q qmul_norm(Q a, Q b) { return qnormalize(qmul(a, b)); }
 RTG_DEV float qabs(Q q) { return cr_sqrt(((q.x * q.x + q.y * q.y) + q.z * q.z) + q.w * q.w); }   // :41-47
 RTG_DEV Q qunit(Q q)                                                                                 // :50-56
 {
     const float n = clamp_lo(qabs(q), 1e-9f);
-    return Q{q.x / n, q.y / n, q.z / n, q.w / n};
+    const double r = rcp64(n);
+    return Q{mulr(q.x, r), mulr(q.y, r), mulr(q.z, r), mulr(q.w, r)};
 }
 // quat_angle_axis (:230-240): angle = acos(clamp(2 w^2 - 1)), axis = xyz / max(|xyz|, 1e-9)
 RTG_DEV Q qangle_axis_abs(Q q)
 {
     const float s = clamp_lohi(2.0f * (q.w * q.w) - 1.0f, -1.0f, 1.0f);
     const float n = clamp_lo(cr_sqrt((q.x * q.x + q.y * q.y) + q.z * q.z), 1e-9f);
-    return Q{cr_acos(s), q.x / n, q.y / n, q.z / n};
+    const double r = rcp64(n);
+    return Q{cr_acos(s), mulr(q.x, r), mulr(q.y, r), mulr(q.z, r)};
 }
 
 RTG_DEV V qrotate(Q q, V v)  // :205-211, two Hamilton products
@@ -181,7 +191,8 @@ RTG_DEV Q qfrom_angle_axis(float angle, V axis)  // :122-143
     const float theta = angle / 2.0f;
     float n = cr_sqrt((axis.x * axis.x + axis.y * axis.y) + axis.z * axis.z);
     n = clamp_lo(n, 1e-9f);
-    const float ax = axis.x / n, ay = axis.y / n, az = axis.z / n;
+    const double r = rcp64(n);
+    const float ax = mulr(axis.x, r), ay = mulr(axis.y, r), az = mulr(axis.z, r);
     const SC t = cr_sincos((double)theta);
     const float s = t.s, c = t.c;
     return qnormalize(Q{ax * s, ay * s, az * s, c});
@@ -237,8 +248,9 @@ RTG_DEV Q qangle_axis(Q q)
     float angle = 2.0f * cr_acos(q.w);
     angle = normalize_angle(angle);
     const bool mask = fabsf(sin_theta) > 1e-5f;
-    return Q{mask ? angle : 0.0f, mask ? q.x / sin_theta : 0.0f, mask ? q.y / sin_theta : 0.0f,
-             mask ? q.z / sin_theta : 1.0f};
+    const double r = rcp64(sin_theta);
+    return Q{mask ? angle : 0.0f, mask ? mulr(q.x, r) : 0.0f, mask ? mulr(q.y, r) : 0.0f,
+             mask ? mulr(q.z, r) : 1.0f};
 }
 RTG_DEV float qexp_component(Q q, int k)
 {
@@ -258,7 +270,11 @@ RTG_DEV V cross3(V a, V b)                                                      
              __builtin_fmaf(a.x, b.y, -(a.y * b.x))};
 }
 RTG_DEV V vsub(V a, V b) { return V{a.x - b.x, a.y - b.y, a.z - b.z}; }
-RTG_DEV V vdiv(V a, float s) { return V{a.x / s, a.y / s, a.z / s}; }
+RTG_DEV V vdiv(V a, float s)
+{
+    const double r = rcp64(s);
+    return V{mulr(a.x, r), mulr(a.y, r), mulr(a.z, r)};
+}
 RTG_DEV V vmul(V a, float s) { return V{s * a.x, s * a.y, s * a.z}; }
 
 RTG_DEV V proj_in_plane(V v, V n)  // :61-75

@@ -9,6 +9,8 @@
 //     path accepts, it must equal (float)sin((double)x) / (float)cos((double)x) (glibc).
 //  2. crm_sincos on 2^30 random doubles in [-pi/2, pi/2] (scipy from_euler half angles),
 //     plus the doubles nearest 0 and +-pi/2.
+//  4. shared-reciprocal division (rtg_math.cuh rcp64/mulr): (float)((double)a * (1.0 / n)) == a / n
+//     for 2^32 random f32 pairs (full bit patterns, clustered exponents, n near 1).
 //  3. crm_atan2f_sel vs the fdlibm restatement (glibc's own atan2f) for (sin a, cos a) of EVERY
 //     float a in [0, 2pi] (the exp-map's normalize_angle), and 2^30 random bit patterns.
 #include <math.h>
@@ -93,5 +95,25 @@ int main(int argc, char **argv)
         if (f2bits(got) != f2bits(ref)) { ++bad; if (bad < 10) printf("atan2 mismatch y=%a x=%a %a %a\n", y, x, got, ref); }
     }
     printf("[3] atan2f: %lld pairs, %lld mismatches\n", n, bad);
-    return (bad1 || bad2 || bad) ? 1 : 0;
+    long long bad3 = bad;
+    bad = 0; n = 0;
+#pragma omp parallel for reduction(+ : bad, n)
+    for (int64_t i = 0; i < (1ll << 32); i += stride) {
+        uint64_t h = (uint64_t)i * 0x9E3779B97F4A7C15ull;
+        h ^= h >> 29; h *= 0xBF58476D1CE4E5B9ull; h ^= h >> 32;
+        uint32_t ua = (uint32_t)h, un = (uint32_t)(h >> 32);
+        if (i & 1) {
+            ua = (ua & 0x807FFFFFu) | (((ua >> 23) % 40 + 107) << 23);
+            un = (un & 0x807FFFFFu) | (((un >> 23) % 40 + 107) << 23);
+        }
+        if ((i & 7) == 2) un = (un & 0x80FFFFFFu) | 0x3F000000u;
+        const float a = bits2f(ua), d = bits2f(un);
+        if (isnan(a) || isnan(d)) continue;
+        volatile float q = a / d;
+        const float p = (float)((double)a * (1.0 / (double)d));
+        ++n;
+        if (f2bits(p) != f2bits(q)) { ++bad; if (bad < 10) printf("rdiv mismatch a=%a n=%a\n", a, d); }
+    }
+    printf("[4] reciprocal division: %lld pairs, %lld mismatches\n", n, bad);
+    return (bad1 || bad2 || bad3 || bad) ? 1 : 0;
 }
