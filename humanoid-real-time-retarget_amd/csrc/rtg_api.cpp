@@ -25,6 +25,15 @@ struct rtg_topology_s {
     TopoView view() const { return TopoView{d_parents, d_local_t, d_tree_quat, d_sched, J, nslots}; }
 };
 
+// HuForwardModel: the topology is borrowed (it must outlive the model); axis / limits are owned.
+struct rtg_dof_model_s {
+    rtg_topology_t topo = nullptr;
+    int32_t *d_axis = nullptr;
+    float *d_lower = nullptr;
+    float *d_upper = nullptr;
+    bool has_limits = false;
+};
+
 struct rtg_solver_s {
     int kind = 0;
     int precise = 0;
@@ -217,6 +226,75 @@ int rtg_fk_multi_f32(const rtg_fk_segment *segs, int32_t n, rtg_stream_t stream)
         A.seg[i] = FkSeg{s.topo->view(), s.local_rot, s.root_t, s.g_rot, s.g_pos, s.B};
     }
     RTG_TRY(launch_fk_multi(A, as_stream(stream)), "k_fk_multi");
+    return RTG_OK;
+}
+
+// ---------------------------------------------------------------- joint-angle forward model
+int rtg_dof_model_create(rtg_topology_t topo, const int32_t *axis, const float *lower, const float *upper,
+                         rtg_dof_model_t *out)
+{
+    if (!out) return fail(RTG_ERR_INVALID_ARGUMENT, "rtg_dof_model_create: out is NULL");
+    *out = nullptr;
+    if (!topo) return fail(RTG_ERR_INVALID_ARGUMENT, "rtg_dof_model_create: NULL topology");
+    if (topo->nslots > kMaxFkSlots)
+        return fail(RTG_ERR_UNSUPPORTED, "rtg_dof_model_create: topology needs %d branch slots (max %d)", topo->nslots,
+                    kMaxFkSlots);
+    const int n = topo->J - 1;
+    if (n > 0 && !axis) return fail(RTG_ERR_INVALID_ARGUMENT, "rtg_dof_model_create: NULL axis");
+    for (int k = 0; k < n; ++k)
+        if (axis[k] < 0 || axis[k] > 2)
+            return fail(RTG_ERR_INVALID_ARGUMENT, "rtg_dof_model_create: axis[%d]=%d is not 0, 1 or 2", k, axis[k]);
+    if ((lower == nullptr) != (upper == nullptr))
+        return fail(RTG_ERR_INVALID_ARGUMENT, "rtg_dof_model_create: give both DOF limit arrays or neither");
+    rtg_dof_model_s *m = new (std::nothrow) rtg_dof_model_s();
+    if (!m) return fail(RTG_ERR_OUT_OF_MEMORY, "rtg_dof_model_create: host allocation failed");
+    m->topo = topo;
+    m->has_limits = lower != nullptr;
+    const size_t na = sizeof(int32_t) * (n > 0 ? n : 1), nf = sizeof(float) * (n > 0 ? n : 1);
+    int rc = hip_check(hipMalloc(&m->d_axis, na), "hipMalloc(axis)");
+    if (rc == RTG_OK && n > 0) rc = hip_check(hipMemcpy(m->d_axis, axis, sizeof(int32_t) * n, hipMemcpyHostToDevice), "hipMemcpy");
+    if (rc == RTG_OK && m->has_limits) {
+        rc = hip_check(hipMalloc(&m->d_lower, nf), "hipMalloc(lower)");
+        if (rc == RTG_OK) rc = hip_check(hipMalloc(&m->d_upper, nf), "hipMalloc(upper)");
+        if (rc == RTG_OK && n > 0)
+            rc = hip_check(hipMemcpy(m->d_lower, lower, sizeof(float) * n, hipMemcpyHostToDevice), "hipMemcpy");
+        if (rc == RTG_OK && n > 0)
+            rc = hip_check(hipMemcpy(m->d_upper, upper, sizeof(float) * n, hipMemcpyHostToDevice), "hipMemcpy");
+    }
+    if (rc != RTG_OK) {
+        (void)hipFree(m->d_axis);
+        (void)hipFree(m->d_lower);
+        (void)hipFree(m->d_upper);
+        delete m;
+        return rc;
+    }
+    *out = m;
+    return RTG_OK;
+}
+
+int rtg_dof_model_destroy(rtg_dof_model_t m)
+{
+    if (!m) return RTG_OK;
+    (void)hipFree(m->d_axis);
+    (void)hipFree(m->d_lower);
+    (void)hipFree(m->d_upper);
+    delete m;
+    return RTG_OK;
+}
+
+int rtg_dof_fk_f32(rtg_dof_model_t m, const float *dof, const float *root_rot, const float *root_t, int64_t B,
+                   int clip, float *g_rot, float *g_pos, rtg_stream_t stream)
+{
+    if (!m) return fail(RTG_ERR_INVALID_ARGUMENT, "rtg_dof_fk_f32: NULL model");
+    if (B < 0) return fail(RTG_ERR_INVALID_ARGUMENT, "rtg_dof_fk_f32: B=%lld < 0", (long long)B);
+    if (clip && !m->has_limits)
+        return fail(RTG_ERR_INVALID_ARGUMENT, "rtg_dof_fk_f32: clip_angles requested but the model has no DOF limits");
+    if (B == 0) return RTG_OK;
+    if ((m->topo->J > 1 && !dof) || !root_rot || !root_t || !g_rot || !g_pos)
+        return fail(RTG_ERR_INVALID_ARGUMENT, "rtg_dof_fk_f32: NULL buffer");
+    const DofView D{m->d_axis, m->d_lower, m->d_upper};
+    RTG_TRY(launch_dof_fk(m->topo->view(), D, clip != 0, dof, root_rot, root_t, B, g_rot, g_pos, as_stream(stream)),
+            "k_dof_fk");
     return RTG_OK;
 }
 

@@ -38,6 +38,13 @@ struct SolverConsts {
     int32_t par[4];   // BODY_ROT: parents of joints 18, 14, 19, 15
 };
 
+// Joint-angle forward model (HuForwardModel): per-DOF axis and optional limits, device memory.
+struct DofView {
+    const int32_t *axis;   // (J-1) 0/1/2
+    const float *lower;    // (J-1) or nullptr
+    const float *upper;    // (J-1) or nullptr
+};
+
 struct FkSeg {
     TopoView T;
     const float *local_rot;
@@ -60,6 +67,8 @@ hipError_t launch_fk(const TopoView &T, bool state, const float *lr, const float
                      hipStream_t s);
 hipError_t launch_local_rotation(const TopoView &T, bool state, const float *g, int64_t B, float *l, hipStream_t s);
 hipError_t launch_fk_multi(FkMultiArgs &A, hipStream_t s);
+hipError_t launch_dof_fk(const TopoView &T, const DofView &D, bool clip, const float *dof, const float *root_rot,
+                         const float *root_t, int64_t B, float *gr, float *gp, hipStream_t s);
 hipError_t launch_quat_op(int op, const float *a, const float *b, const float *c, int64_t n, float *out,
                           hipStream_t s);
 hipError_t launch_cal_joint_quat(const float *Z, const float *M, int npts, int64_t n, float *out, hipStream_t s);

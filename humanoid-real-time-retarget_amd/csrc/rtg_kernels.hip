@@ -710,6 +710,99 @@ __global__ __launch_bounds__(kFkTile) void k_fk_multi_stream(FkMultiArgs A)
                           S.g_rot, S.g_pos, fk_lds);
 }
 
+// Joint-angle FK (HuForwardModel.forward_kinematics, hu_forward_model.py:17-33): the streaming tile of
+// k_fk_stream, but joint j's local rotation is built in-lane from its DOF --
+// quat_from_angle_axis(a', e_axis) with a' = (clamp(a) - a) + a when clipping -- so no (B,J,4) local-rotation
+// tensor ever exists in HBM.  Each lane's next window of 8 angles is prefetched during the current window.
+struct DofRegs {
+    float a0, a1, a2, a3, a4, a5, a6, a7;
+};
+RTG_DEV void dof_load(DofRegs &r, const float *__restrict__ row, int J, int c0)
+{
+    // angles of joints c0..c0+7 are dof[c0-1 .. c0+6]; indices are clamped into the row (unused ones are dropped)
+    auto at = [&](int k) {
+        int i = c0 + k - 1;
+        i = i < 0 ? 0 : (i > J - 2 ? J - 2 : i);
+        return row[i];
+    };
+    r.a0 = at(0); r.a1 = at(1); r.a2 = at(2); r.a3 = at(3); r.a4 = at(4); r.a5 = at(5); r.a6 = at(6); r.a7 = at(7);
+}
+RTG_DEV float dof_get(const DofRegs &r, int k)
+{
+    return k == 0 ? r.a0 : k == 1 ? r.a1 : k == 2 ? r.a2 : k == 3 ? r.a3 : k == 4 ? r.a4 : k == 5 ? r.a5
+                                                                                           : k == 6 ? r.a6 : r.a7;
+}
+
+template <bool CLIP>
+__global__ __launch_bounds__(kFkTile) void k_dof_fk(TopoView T, DofView D, const float *__restrict__ dof,
+                                                    const float *__restrict__ root_rot,
+                                                    const float *__restrict__ root_t, int64_t B,
+                                                    float *__restrict__ g_rot, float *__restrict__ g_pos)
+{
+    extern __shared__ __attribute__((aligned(16))) float fk_lds[];
+    const int J = T.J;
+    const int64_t f0 = (int64_t)blockIdx.x * kFkTile;
+    const int nfr = (int)((B - f0) < kFkTile ? (B - f0) : kFkTile);
+    float *rot = fk_lds;
+    float *pos = fk_lds + kFkTile * kRotPitch;
+    float *slots = pos + kFkTile * kPosPitch;
+    const int lane = threadIdx.x;
+    const bool active = lane < nfr;
+    const int64_t f = f0 + (active ? lane : 0);
+    const float *drow = dof + f * (J - 1);
+    const Q rroot = ld4(root_rot + f * 4);
+    const V troot = ld3(root_t + f * 3);
+    DofRegs cur, next;
+    if (J > 1) dof_load(next, drow, J, 0);
+    Q g = qident();
+    V t = V{0.0f, 0.0f, 0.0f};
+    for (int c0 = 0; c0 < J; c0 += kFkChunk) {
+        const int nC = (J - c0) < kFkChunk ? (J - c0) : kFkChunk;
+        cur = next;
+        if (c0 + kFkChunk < J) dof_load(next, drow, J, c0 + kFkChunk);
+        if (active) {
+            float *R = rot + lane * kRotPitch;
+            float *P = pos + lane * kPosPitch;
+#pragma unroll
+            for (int k = 0; k < kFkChunk; ++k) {
+                if (k >= nC) break;
+                const int j = c0 + k;
+                const int32_t sc = ld_const(T.sched + j);
+                Q ng;
+                V nt;
+                if (j == 0) {   // root: global = local = the root rotation, unnormalised (:24, kinematics.py:27-29)
+                    ng = rroot;
+                    nt = troot;
+                } else {
+                    float a = dof_get(cur, k);
+                    if (CLIP) {   // torch.clamp (min then max; NaN passes), then the straight-through sum
+                        const float lo = ld_const(D.lower + (j - 1)), hi = ld_const(D.upper + (j - 1));
+                        float c = a < lo ? lo : a;
+                        c = c > hi ? hi : c;
+                        a = (c - a) + a;
+                    }
+                    const int ax = ld_const(D.axis + (j - 1));
+                    const Q lq = qfrom_angle_axis(a, V{ax == 0 ? 1.0f : 0.0f, ax == 1 ? 1.0f : 0.0f,
+                                                       ax == 2 ? 1.0f : 0.0f});
+                    if ((sc & 0xFF) != kNoSlot) slot_get(slots, sc & 0xFF, g, t);
+                    const V rv = qrotate(g, ld_const(T.local_t + j));
+                    ng = qmul_norm(g, lq);
+                    nt = V{rv.x + t.x, rv.y + t.y, rv.z + t.z};
+                }
+                R[4 * k] = ng.x; R[4 * k + 1] = ng.y; R[4 * k + 2] = ng.z; R[4 * k + 3] = ng.w;
+                P[3 * k] = nt.x; P[3 * k + 1] = nt.y; P[3 * k + 2] = nt.z;
+                if (((sc >> 8) & 0xFF) != kNoSlot) slot_put(slots, (sc >> 8) & 0xFF, ng, nt);
+                g = ng;
+                t = nt;
+            }
+        }
+        wave_sync();
+        chunk_store<4>(g_rot, rot, kRotPitch, f0, nfr, J, c0, nC);
+        chunk_store<3>(g_pos, pos, kPosPitch, f0, nfr, J, c0, nC);
+        wave_sync();
+    }
+}
+
 int32_t fk_schedule(const int32_t *parents, int32_t J, int32_t *sched)
 {
     // last non-consecutive child of every branch parent
@@ -1109,6 +1202,17 @@ hipError_t launch_fk_multi(FkMultiArgs &A, hipStream_t s)
         hipLaunchKernelGGL(k_fk_multi_stream, dim3((unsigned)blocks), dim3(kFkTile), fk_stream_lds_bytes(maxS), s, A);
     else
         hipLaunchKernelGGL(k_fk_multi, dim3((unsigned)blocks), dim3(256), 0, s, A);
+    return hipGetLastError();
+}
+
+hipError_t launch_dof_fk(const TopoView &T, const DofView &D, bool clip, const float *dof, const float *root_rot,
+                         const float *root_t, int64_t B, float *gr, float *gp, hipStream_t s)
+{
+    if (T.nslots > kMaxFkSlots) return hipErrorInvalidValue;   // rejected at rtg_dof_model_create
+    const dim3 g(grid_for(B, kFkTile)), b(kFkTile);
+    const size_t lds = fk_stream_lds_bytes(T.nslots);
+    if (clip) hipLaunchKernelGGL(k_dof_fk<true>, g, b, lds, s, T, D, dof, root_rot, root_t, B, gr, gp);
+    else hipLaunchKernelGGL(k_dof_fk<false>, g, b, lds, s, T, D, dof, root_rot, root_t, B, gr, gp);
     return hipGetLastError();
 }
 

@@ -3,3 +3,5 @@ from robot_kinematics_model.base_robot import RobotZeroPose
 from robot_kinematics_model.kinematics import cal_forward_kinematics, cal_local_rotation
 
 __all__ = ["RobotZeroPose", "cal_forward_kinematics", "cal_local_rotation"]
+# robot_kinematics_model.hu_forward_model.HuForwardModel / base_forward_model.BaseForwardModel are
+# imported by module path, as in the reference.

@@ -83,7 +83,7 @@ class RobotZeroPose:
 
     @classmethod
     def from_asset(cls, name: str):
-        """Zero pose from the package's converted assets ('hu_v5', 'vtrdyn_full', 'vtrdyn', 'noitom')."""
+        """Zero pose from the package's converted assets ('hu_v5', 'vtrdyn_full', 'vtrdyn', 'noitom', 'hu')."""
         from rtg import assets
         a = assets.load(name)
         tree = SkeletonTree([str(s) for s in a["node_names"]], torch.from_numpy(a["parent_indices"]),

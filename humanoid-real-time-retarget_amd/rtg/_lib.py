@@ -71,6 +71,10 @@ SIGNATURES = {
     "rtg_state_fk_f32": (c_int, [c_void_p, c_void_p, c_void_p, c_int64, c_void_p, c_void_p, c_void_p]),
     "rtg_state_local_rotation_f32": (c_int, [c_void_p, c_void_p, c_int64, c_void_p, c_void_p]),
     "rtg_fk_multi_f32": (c_int, [POINTER(FkSegment), c_int32, c_void_p]),
+    "rtg_dof_model_create": (c_int, [c_void_p, POINTER(c_int32), POINTER(c_float), POINTER(c_float),
+                                     POINTER(c_void_p)]),
+    "rtg_dof_model_destroy": (c_int, [c_void_p]),
+    "rtg_dof_fk_f32": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_int64, c_int, c_void_p, c_void_p, c_void_p]),
     "rtg_solver_create": (c_int, [c_int, POINTER(c_float), POINTER(c_float), POINTER(c_int32), c_int32, c_int,
                                   POINTER(c_void_p)]),
     "rtg_solver_destroy": (c_int, [c_void_p]),

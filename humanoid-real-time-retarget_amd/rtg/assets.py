@@ -9,7 +9,7 @@ from typing import Dict
 import numpy as np
 
 ASSET_DIR = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "assets")
-NAMES = ("hu_v5", "vtrdyn_full", "vtrdyn", "noitom")
+NAMES = ("hu_v5", "vtrdyn_full", "vtrdyn", "noitom", "hu")
 
 
 @lru_cache(maxsize=None)

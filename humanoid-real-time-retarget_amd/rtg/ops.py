@@ -228,6 +228,32 @@ def local_rotation(topo: Topology, g_rot, state: bool = False):
     return out
 
 
+def dof_forward_kinematics(model, dof, root_rot, root_t, clip: bool = False):
+    """HuForwardModel.forward_kinematics (hu_forward_model.py:17-33): joint angles (..., J-1) [or (..., J-1, 1)],
+    root rotation (..., 4) [or (..., 1, 4)], root translation (..., 3) -> g_rot (..., J, 4), g_pos (..., J, 3)."""
+    def _t(x):
+        return x if isinstance(x, torch.Tensor) else torch.as_tensor(x)
+
+    n = model.num_dofs
+    d = _t(dof)
+    if d.dim() >= 2 and d.shape[-1] == 1 and d.shape[-2] == n:
+        d = d[..., 0]
+    d = dev_f32(d, (n,), "motion_joint_angles")
+    lead = d.shape[:-1]
+    rr = _t(root_rot)
+    if rr.dim() >= 2 and rr.shape[-2] == 1 and rr.shape[-1] == 4:
+        rr = rr[..., 0, :]
+    rr = dev_f32(rr, (4,), "motion_root_rotation").expand(*lead, 4).contiguous()
+    rt = dev_f32(root_t, (3,), "motion_root_translation").expand(*lead, 3).contiguous()
+    B = int(torch.Size(lead).numel())
+    J = n + 1
+    g_rot = torch.empty(tuple(lead) + (J, 4), device=d.device, dtype=torch.float32)
+    g_pos = torch.empty(tuple(lead) + (J, 3), device=d.device, dtype=torch.float32)
+    check(lib().rtg_dof_fk_f32(model.handle, ptr(d), ptr(rr), ptr(rt), B, int(bool(clip)), ptr(g_rot), ptr(g_pos),
+                               stream_handle()))
+    return g_rot, g_pos
+
+
 def forward_kinematics_multi(segments: Sequence[tuple]):
     """One launch over several (topology, local_rot (B,J,4), root_t (B,3)) segments.
 

@@ -90,6 +90,44 @@ class Topology:
             self._h = None
 
 
+class DofModel:
+    """A joint-angle forward model (``rtg_dof_model_t``, HuForwardModel hu_forward_model.py:13-33):
+    a topology, one rotation axis per DOF (0/1/2) and optional DOF limits."""
+
+    def __init__(self, topo: Topology, axis, lower=None, upper=None):
+        require_gpu()
+        ax = _host_i32(axis)
+        n = topo.num_joints - 1
+        if ax.shape[0] != n:
+            raise ValueError(f"{ax.shape[0]} DOF axes for a {topo.num_joints}-joint topology (need {n})")
+        lo = hi = None
+        if (lower is None) != (upper is None):
+            raise ValueError("give both DOF limit tables or neither")
+        if lower is not None:
+            lo, hi = _host_f32(lower).reshape(-1), _host_f32(upper).reshape(-1)
+            if lo.shape[0] != n or hi.shape[0] != n:   # the reference's torch.clamp would fail to broadcast
+                raise ValueError(f"DOF limits hold {lo.shape[0]}/{hi.shape[0]} entries for {n} DOFs")
+        fp = ctypes.POINTER(ctypes.c_float)
+        h = ctypes.c_void_p()
+        check(lib().rtg_dof_model_create(topo.handle, ax.ctypes.data_as(ctypes.POINTER(ctypes.c_int32)),
+                                         None if lo is None else lo.ctypes.data_as(fp),
+                                         None if hi is None else hi.ctypes.data_as(fp), ctypes.byref(h)))
+        self._h = h
+        self.topo = topo   # borrowed by the handle: keep it alive
+        self.num_dofs = n
+        self.has_limits = lo is not None
+
+    @property
+    def handle(self) -> ctypes.c_void_p:
+        return self._h
+
+    def __del__(self):
+        h = getattr(self, "_h", None)
+        if h is not None and h.value and _lib._lib is not None:
+            _lib._lib.rtg_dof_model_destroy(h)
+            self._h = None
+
+
 class Solver:
     """A retarget solver (``rtg_solver_t``) of one of the four reference kinds."""
 

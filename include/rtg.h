@@ -92,6 +92,23 @@ typedef struct rtg_fk_segment {
 int rtg_fk_multi_f32(const rtg_fk_segment *segments, int32_t n_segments, rtg_stream_t stream);
 
 /* ------------------------------------------------------------------------
+ * Joint-angle forward model: HuForwardModel (robot_kinematics_model/
+ * hu_forward_model.py:13-33).  A topology plus one rotation axis per DOF
+ * (J-1 entries, 0=x 1=y 2=z: torch.eye(3)[Hu_DOF_AXIS], :16) and optional
+ * DOF limits (J-1 each; both NULL = none).  Host pointers, copied.
+ * ---------------------------------------------------------------------- */
+typedef struct rtg_dof_model_s *rtg_dof_model_t;
+int rtg_dof_model_create(rtg_topology_t topo, const int32_t *axis, const float *lower, const float *upper,
+                         rtg_dof_model_t *out);
+int rtg_dof_model_destroy(rtg_dof_model_t model);
+/* forward_kinematics(motion_joint_angles (B,J-1), motion_root_translation (B,3),
+ * motion_root_rotation (B,4), clip_angles) -> g_rot (B,J,4), g_pos (B,J,3).
+ * clip != 0 applies a' = (clamp(a, lower, upper) - a) + a (:27-33) and needs limits.
+ * local[j] = quat_from_angle_axis(a'[j-1], axis[j-1]) (:21-23), local[0] = root rotation (:24). */
+int rtg_dof_fk_f32(rtg_dof_model_t model, const float *dof, const float *root_rot, const float *root_t, int64_t B,
+                   int clip, float *g_rot, float *g_pos, rtg_stream_t stream);
+
+/* ------------------------------------------------------------------------
  * Retarget solvers (retarget/retarget_solver/__init__.py:9-14)
  * ---------------------------------------------------------------------- */
 typedef enum rtg_solver_kind {

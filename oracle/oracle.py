@@ -100,6 +100,21 @@ def fk(parents, zl, local_rot, root_t):
     return gr, gp
 
 
+def dof_fk(parents, zl, axis, dof, root_rot, root_t, lower=None, upper=None):
+    """HuForwardModel.forward_kinematics: dof (B, J-1), root_rot (B, 4), root_t (B, 3); optional clip limits."""
+    p, zl, ax = _i32(parents), _c32(zl), _i32(axis)
+    d, rr, rt = _c32(dof), _c32(root_rot), _c32(root_t)
+    B, J = d.shape[0], len(p)
+    lo = _c32(lower) if lower is not None else None
+    hi = _c32(upper) if upper is not None else None
+    gr = np.empty((B, J, 4), np.float32)
+    gp = np.empty((B, J, 3), np.float32)
+    lib().oracle_dof_fk(p.ctypes.data_as(_i), _fp(zl), ctypes.c_int32(J), ax.ctypes.data_as(_i),
+                        _fp(lo) if lo is not None else None, _fp(hi) if hi is not None else None,
+                        _fp(d), _fp(rr), _fp(rt), _i64(B), _fp(gr), _fp(gp))
+    return gr, gp
+
+
 def local_rotation(parents, g_rot):
     p, g = _i32(parents), _c32(g_rot)
     B, J = g.shape[:2]

@@ -167,3 +167,31 @@ def test_skeleton_motion_from_state(gpu):
     np.testing.assert_array_equal(mo.global_velocity.numpy(), m["global_velocity"])
     assert frame_stats(mo.global_angular_velocity.numpy(), m["global_angular_velocity"])["max"] <= 1e-6
     np.testing.assert_array_equal(mo.tensor.numpy()[:, :31 * 4 + 3], m["tensor"][:, :31 * 4 + 3])
+
+
+def test_hu_forward_model_dropin(gpu):
+    """robot_kinematics_model.hu_forward_model.HuForwardModel: reference shapes and clip semantics."""
+    import torch
+    import oracle as orc
+    from robot_kinematics_model.hu_forward_model import HuForwardModel
+    from rtg import assets
+    from retarget.robot_config import Hu
+    d = golden("dof_fk")
+    from robot_kinematics_model import RobotZeroPose
+    m = HuForwardModel(RobotZeroPose.from_asset("hu").skeleton_tree)
+    L = 128
+    ang = torch.from_numpy(d["hu_clip_dof"]).reshape(L, 32, 1).cuda()
+    rr = torch.from_numpy(d["hu_clip_root_rot"]).reshape(L, 1, 4).cuda()
+    rt = torch.from_numpy(d["hu_clip_root_t"]).cuda()
+    gr, gp = m.forward_kinematics(motion_joint_angles=ang, motion_root_translation=rt, motion_root_rotation=rr,
+                                  clip_angles=True)
+    assert gr.shape == (L, 33, 4) and gp.shape == (L, 33, 3) and gr.device.type == "cuda"
+    ogr, ogp = orc.dof_fk(assets.parents("hu"), assets.local_translation("hu"), Hu.Hu_DOF_AXIS, d["hu_clip_dof"],
+                          d["hu_clip_root_rot"], d["hu_clip_root_t"], Hu.Hu_DOF_LOWER.numpy(), Hu.Hu_DOF_UPPER.numpy())
+    np.testing.assert_array_equal(gr.cpu().numpy(), ogr)
+    np.testing.assert_array_equal(gp.cpu().numpy(), ogp)
+    c = m._clip_angles(ang)
+    assert c.shape == ang.shape and bool((c.cpu() <= Hu.Hu_DOF_UPPER.reshape(1, -1, 1) + 1e-6).all())
+    m5 = HuForwardModel(RobotZeroPose.from_asset("hu_v5").skeleton_tree)
+    with pytest.raises(ValueError):
+        m5.forward_kinematics(torch.zeros(2, 30, 1), torch.zeros(2, 3), torch.zeros(2, 1, 4), clip_angles=True)

@@ -133,6 +133,68 @@ def test_fk_random_topologies_vs_oracle(gpu, kind, J):
                                       orc.state_local_rotation(par, tq, ng))
 
 
+DOF_FK_CASES = [("hu_clip", "hu"), ("hu_noclip", "hu"), ("hu_v5_noclip", "hu_v5")]
+
+
+def _dof_model(d, tag, name):
+    from rtg.runtime import DofModel
+    lo = d[f"{tag}_lower"] if f"{tag}_lower" in d else None
+    hi = d[f"{tag}_upper"] if f"{tag}_upper" in d else None
+    return DofModel(_topo(name), d[f"{tag}_axis"], lo, hi), lo, hi
+
+
+@pytest.mark.parametrize("tag,name", DOF_FK_CASES)
+def test_dof_fk_vs_oracle_and_reference(gpu, tag, name):
+    """HuForwardModel.forward_kinematics (hu_forward_model.py:17-33) in one launch: bit-exact vs the oracle on
+    the golden inputs and on 20001 random frames (angles far outside the limits); vs the reference within the
+    VML sin/cos residual pinned in test_oracle_golden.py."""
+    import oracle as orc
+    from rtg import assets, ops
+    d = golden("dof_fk")
+    model, lo, hi = _dof_model(d, tag, name)
+    clip = lo is not None
+    par, lt = assets.parents(name), assets.local_translation(name)
+    gr, gp = ops.dof_forward_kinematics(model, d[f"{tag}_dof"], d[f"{tag}_root_rot"], d[f"{tag}_root_t"], clip=clip)
+    ogr, ogp = orc.dof_fk(par, lt, d[f"{tag}_axis"], d[f"{tag}_dof"], d[f"{tag}_root_rot"], d[f"{tag}_root_t"], lo, hi)
+    np.testing.assert_array_equal(_np(gr), ogr)
+    np.testing.assert_array_equal(_np(gp), ogp)
+    for got, want in ((_np(gr), d[f"{tag}_g_rot"]), (_np(gp), d[f"{tag}_g_pos"])):
+        assert np.abs(got - want).max() <= 2e-6
+    rng = np.random.default_rng(17)
+    B, n = 20001, model.num_dofs
+    dof = rng.uniform(-4, 4, (B, n)).astype(np.float32)
+    rr = rng.normal(size=(B, 4)).astype(np.float32)
+    rt = rng.normal(0, 0.3, (B, 3)).astype(np.float32)
+    gr, gp = ops.dof_forward_kinematics(model, dof, rr, rt, clip=clip)
+    ogr, ogp = orc.dof_fk(par, lt, d[f"{tag}_axis"], dof, rr, rt, lo, hi)
+    np.testing.assert_array_equal(_np(gr), ogr)
+    np.testing.assert_array_equal(_np(gp), ogp)
+
+
+def test_dof_fk_roundtrip_with_retargeted_dofs(gpu):
+    """Closing the loop: the retargeted Hu v5 DOFs of the golden frames, driven through the
+    joint-angle model, reproduce FK of the solver's own local rotations (identity root)."""
+    from rtg import _lib, assets, ops
+    from rtg.runtime import DofModel, Solver
+    from retarget.robot_config import Hu_v5
+    zp = golden("zero_pose")
+    g = golden("full_body_pos_precise")
+    S = Solver(_lib.SOLVER_FULL_BODY_POS, zp["vtrdyn_full_local_t"], zp["vtrdyn_full_global_t"],
+               assets.parents("vtrdyn_full"), True)
+    dof, lr, _ = S.retarget([torch.from_numpy(g[k]).cuda() for k in ("body", "lh", "rh")], want_local_rot=True)
+    T = _topo("hu_v5")
+    B = lr.shape[0]
+    root_rot = np.tile(np.array([0, 0, 0, 1], np.float32), (B, 1))
+    root_t = np.zeros((B, 3), np.float32)
+    gr, gp = ops.dof_forward_kinematics(DofModel(T, Hu_v5.Hu_DOF_AXIS), dof, root_rot, root_t)
+    lr = _np(lr).copy()
+    lr[:, 0] = root_rot
+    fr, fp = ops.forward_kinematics(T, lr, root_t)
+    # exp-map -> angle -> angle-axis is not an exact inverse in f32 (DOFs 18/19/27/28 are prismatic:
+    # the gripper links rotate by their metre value); compare the rotational chain's positions loosely
+    assert np.abs(_np(gp) - _np(fp))[:, :18].max() < 1e-4
+
+
 # ----------------------------------------------------------------- primitives
 def test_quaternion_algebra_bit_exact(gpu):
     from rtg import ops

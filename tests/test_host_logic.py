@@ -57,6 +57,17 @@ def test_solver_and_op_validation():
     assert lib.rtg_retarget_f32(None, None, None, None, None, 1, None, None, None, None) == 1
 
 
+def test_dof_model_validation():
+    from rtg import _lib
+    lib = _lib.lib()
+    h = ctypes.c_void_p()
+    ax = np.zeros(4, np.int32)
+    ip = ctypes.POINTER(ctypes.c_int32)
+    assert lib.rtg_dof_model_create(None, ax.ctypes.data_as(ip), None, None, ctypes.byref(h)) == 1
+    assert b"NULL topology" in lib.rtg_last_error()
+    assert lib.rtg_dof_fk_f32(None, None, None, None, 1, 0, None, None, None) == 1
+
+
 def test_empty_batches_are_noops():
     from rtg import _lib
     lib = _lib.lib()
@@ -71,6 +82,7 @@ def test_dropin_modules_import_without_gpu():
     import retarget.spatial_transform.transform3d  # noqa: F401
     import robot_kinematics_model  # noqa: F401
     from retarget.retarget_solver import VtrdynFullBodyPosRetargeter  # noqa: F401
+    from robot_kinematics_model.hu_forward_model import HuForwardModel  # noqa: F401
 
 
 @pytest.mark.skipif(__import__("torch").cuda.is_available(), reason="checks the no-GPU behaviour")

@@ -196,3 +196,50 @@ def test_fast_crmath_matches_glibc(tmp_path):
     r = subprocess.run([str(exe), "61"], capture_output=True, text=True, timeout=300)
     assert r.returncode == 0, r.stdout + r.stderr
     assert r.stdout.count(" 0 mismatches") == 4, r.stdout
+
+
+DOF_FK_CASES = [("hu_clip", "hu"), ("hu_noclip", "hu"), ("hu_v5_noclip", "hu_v5")]
+
+
+def _dof_fk_case(tag):
+    d = golden("dof_fk")
+    lo = d[f"{tag}_lower"] if f"{tag}_lower" in d else None
+    hi = d[f"{tag}_upper"] if f"{tag}_upper" in d else None
+    return d, lo, hi
+
+
+@pytest.mark.parametrize("tag,name", DOF_FK_CASES)
+def test_dof_fk_vs_reference(tag, name):
+    """HuForwardModel.forward_kinematics (hu_forward_model.py:17-33).  The only non-reproducible ops are
+    torch.sin/cos of the half angles (MKL VML on CPU, not always correctly rounded): <= 1-ulp-level
+    residual, and most elements bit-equal."""
+    from rtg import assets
+    d, lo, hi = _dof_fk_case(tag)
+    gr, gp = orc.dof_fk(assets.parents(name), assets.local_translation(name), d[f"{tag}_axis"], d[f"{tag}_dof"],
+                        d[f"{tag}_root_rot"], d[f"{tag}_root_t"], lo, hi)
+    for got, want in ((gr, d[f"{tag}_g_rot"]), (gp, d[f"{tag}_g_pos"])):
+        err = np.abs(got - want)
+        assert err.max() <= 2e-6 and (err == 0).mean() >= 0.75, (err.max(), (err == 0).mean())
+
+
+@pytest.mark.parametrize("tag,name", DOF_FK_CASES)
+def test_dof_fk_attribution_torch_sincos(tag, name):
+    """Build the local rotations with torch's own sin/cos (quat_from_angle_axis, rotation3d.py:122-143, after
+    the clip of :27-33) and run the oracle's FK: bit-exact.  So clip, axis selection, normalisation and FK
+    are reproduced exactly; the residual above is VML's sin/cos alone."""
+    import torch
+    from rtg import assets
+    d, lo, hi = _dof_fk_case(tag)
+    a = torch.from_numpy(d[f"{tag}_dof"])
+    if lo is not None:
+        c = torch.clamp(a, min=torch.from_numpy(lo), max=torch.from_numpy(hi))
+        a = (c - a) + a
+    axis = torch.eye(3)[torch.from_numpy(d[f"{tag}_axis"]).long()].expand(a.shape[0], -1, -1).reshape(-1, 3)
+    theta = (a.reshape(-1) / 2).unsqueeze(-1)
+    axis = axis / torch.clamp(axis.norm(p=2, dim=-1, keepdim=True), min=1e-9)
+    q = torch.cat([axis * theta.sin(), theta.cos()], dim=-1)
+    q = orc.quat_normalize(q.numpy()).reshape(a.shape[0], -1, 4)
+    lr = np.concatenate([d[f"{tag}_root_rot"][:, None], q], axis=1)
+    gr, gp = orc.fk(assets.parents(name), assets.local_translation(name), lr, d[f"{tag}_root_t"])
+    np.testing.assert_array_equal(gr, d[f"{tag}_g_rot"])
+    np.testing.assert_array_equal(gp, d[f"{tag}_g_pos"])

@@ -86,6 +86,17 @@ def fk():
     ms = time_events(lambda: ops.local_rotation(T, g))
     res["hu_inverse_fk_262144"] = {"ms": ms, "frames_per_s": B / (ms * 1e-3),
                                    "GBs_algorithmic": 31 * 32 * B / (ms * 1e-3) / 1e9}
+    # HuForwardModel: joint angles -> FK (33-link Hu, clip on): (J-1)*4 + 16 + 12 in, J*28 out per frame
+    from rtg.runtime import DofModel
+    import importlib
+    hu = importlib.import_module("retarget.robot_config.Hu")
+    Th = topo("hu")
+    M = DofModel(Th, hu.Hu_DOF_AXIS, hu.Hu_DOF_LOWER.numpy(), hu.Hu_DOF_UPPER.numpy())
+    dof = (torch.rand((B, 32), device="cuda") - 0.5) * 4
+    rr = torch.nn.functional.normalize(torch.randn((B, 4), device="cuda"), dim=-1)
+    ms = time_events(lambda: ops.dof_forward_kinematics(M, dof, rr, rt, clip=True))
+    res["hu_dof_fk_262144"] = {"ms": ms, "frames_per_s": B / (ms * 1e-3),
+                               "GBs_algorithmic": (32 * 4 + 28 + 33 * 28) * B / (ms * 1e-3) / 1e9}
     segs = []
     nbytes = 0
     for i, n in enumerate(["hu_v5", "vtrdyn", "vtrdyn_full", "noitom"]):

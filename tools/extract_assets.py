@@ -11,6 +11,7 @@ Output: ``humanoid-real-time-retarget_amd/assets/<name>.npz`` with
   vtrdyn_full  <- asset/zero_pose/vtrdyn_full_zero_pose.pkl (VTRDyn full body+hands, 59)
   vtrdyn       <- asset/zero_pose/vtrdyn_zero_pose.pkl      (VTRDyn body, 21)
   noitom       <- asset/zero_pose/noitom_zero_pose.pkl      (Noitom body, 21)
+  hu           <- asset/zero_pose/hu_zero_pose.pkl          (Hu, 33 links / 32 DOFs: HuForwardModel, robot_config/Hu.py)
 """
 import os
 import sys
@@ -29,6 +30,7 @@ ASSETS = {
     "vtrdyn_full": "asset/zero_pose/vtrdyn_full_zero_pose.pkl",
     "vtrdyn": "asset/zero_pose/vtrdyn_zero_pose.pkl",
     "noitom": "asset/zero_pose/noitom_zero_pose.pkl",
+    "hu": "asset/zero_pose/hu_zero_pose.pkl",
 }
 
 

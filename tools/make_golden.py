@@ -128,6 +128,50 @@ def gen_kinematics(ref, torch, n):
     return out
 
 
+def gen_dof_fk(ref, torch, n):
+    """HuForwardModel.forward_kinematics (robot_kinematics_model/hu_forward_model.py:17-33), evaluated step by
+    step with the reference's own functions: the module itself imports motion_convert.*, which the reference
+    does not ship.  hu (33 links, robot_config/Hu.py tables) with clip_angles=True and False; hu_v5 (31 links,
+    Hu_v5 axes; its 32-entry limit tables cannot broadcast against 30 DOFs) without clipping."""
+    import importlib
+    out = {}
+    cases = (("hu", "retarget.robot_config.Hu", True), ("hu", "retarget.robot_config.Hu", False),
+             ("hu_v5", "retarget.robot_config.Hu_v5", False))
+    for k, (name, mod, clip) in enumerate(cases):
+        cfg = importlib.import_module(mod)
+        tree = rh.ref_skeleton_state(ref, name).skeleton_tree
+        J = tree.num_joints
+        rng = np.random.default_rng(300 + k)
+        ang = rng.uniform(-3.5, 3.5, (n, J - 1, 1)).astype(np.float32)   # well beyond the limits: clip is exercised
+        ang[:4] = 0.0
+        root_rot = _rand_quats(rng, n).reshape(n, 1, 4)
+        root_t = rng.normal(0, 0.3, (n, 3)).astype(np.float32)
+        a = torch.from_numpy(ang)
+        if clip:   # HuForwardModel._clip_angles :27-33 (forward value of the straight-through form)
+            lo = cfg.Hu_DOF_LOWER.reshape(1, -1, 1)
+            hi = cfg.Hu_DOF_UPPER.reshape(1, -1, 1)
+            c = torch.clamp(a.clone(), min=lo, max=hi)
+            a = (c - a).detach() + a
+        axis = torch.eye(3)[cfg.Hu_DOF_AXIS].repeat(n, 1, 1).clone()                 # :16, :21
+        lr = ref.rotation3d.quat_from_angle_axis(a.reshape(-1), axis.reshape(-1, 3))  # :22
+        lr = lr.reshape(n, J - 1, 4)
+        lr = torch.concatenate([torch.from_numpy(root_rot), lr], dim=1)             # :24
+        gr, gp = ref.rkm.cal_forward_kinematics(motion_local_rotation=lr, motion_root_translation=torch.from_numpy(root_t),
+                                                parent_indices=tree.parent_indices,
+                                                zero_pose_local_translation=tree.local_translation)
+        tag = f"{name}_{'clip' if clip else 'noclip'}"
+        out[f"{tag}_dof"] = ang[..., 0]
+        out[f"{tag}_root_rot"] = root_rot[:, 0]
+        out[f"{tag}_root_t"] = root_t
+        out[f"{tag}_axis"] = np.asarray(cfg.Hu_DOF_AXIS, np.int32)
+        if clip:
+            out[f"{tag}_lower"] = t2n(cfg.Hu_DOF_LOWER)
+            out[f"{tag}_upper"] = t2n(cfg.Hu_DOF_UPPER)
+        out[f"{tag}_g_rot"] = t2n(gr)
+        out[f"{tag}_g_pos"] = t2n(gp)
+    return out
+
+
 def _rand_quats(rng, n):
     q = rng.normal(size=(n, 4))
     q /= np.linalg.norm(q, axis=-1, keepdims=True)
@@ -287,7 +331,7 @@ def main() -> None:
     ref = rh.load_reference()
     os.makedirs(OUT, exist_ok=True)
     zp = {}
-    for name in ["hu_v5", "vtrdyn", "vtrdyn_full", "noitom"]:
+    for name in ["hu_v5", "vtrdyn", "vtrdyn_full", "noitom", "hu"]:
         z = rh.ref_zero_pose(ref, name)
         zp[f"{name}_local_t"] = t2n(z.local_translation)
         zp[f"{name}_global_t"] = t2n(z.global_translation)
@@ -302,6 +346,7 @@ def main() -> None:
         "primitives": lambda: gen_primitives(ref, torch),
         "motion": lambda: gen_motion(ref, torch),
         "kat_rotation_test": lambda: gen_kat(ref, torch),
+        "dof_fk": lambda: gen_dof_fk(ref, torch, 128),
     }
     only = set(sys.argv[1:])
     for name, fn in jobs.items():
