@@ -298,6 +298,41 @@ int rtg_dof_fk_f32(rtg_dof_model_t m, const float *dof, const float *root_rot, c
     return RTG_OK;
 }
 
+// ---------------------------------------------------------------- motion-level prep (retarget/main.py)
+int rtg_rescale_motion_f32(rtg_topology_t topo, const float *motion, int64_t B, const float *dir, float *out,
+                           rtg_stream_t stream)
+{
+    if (!topo) return fail(RTG_ERR_INVALID_ARGUMENT, "rtg_rescale_motion_f32: NULL topology");
+    if (B < 0) return fail(RTG_ERR_INVALID_ARGUMENT, "rtg_rescale_motion_f32: B < 0");
+    if (B == 0) return RTG_OK;
+    if (!motion || !out) return fail(RTG_ERR_INVALID_ARGUMENT, "rtg_rescale_motion_f32: NULL buffer");
+    RTG_TRY(launch_rescale_motion(topo->view(), motion, B, dir, out, as_stream(stream)), "k_rescale_motion");
+    return RTG_OK;
+}
+
+int rtg_quat_between_f32(const float *v1, const float *v2, int64_t n, float *out, float *ws, rtg_stream_t stream)
+{
+    if (n < 0) return fail(RTG_ERR_INVALID_ARGUMENT, "rtg_quat_between_f32: n < 0");
+    if (n == 0) return RTG_OK;
+    if (!v1 || !v2 || !out || !ws) return fail(RTG_ERR_INVALID_ARGUMENT, "rtg_quat_between_f32: NULL buffer");
+    RTG_TRY(launch_quat_between(v1, v2, n, out, ws, as_stream(stream)), "k_quat_between");
+    return RTG_OK;
+}
+
+int rtg_rebuild_vtrdyn_f32(rtg_topology_t topo, const float *motion, int64_t B, float *g_rot, float *root_t,
+                           float *ws, rtg_stream_t stream)
+{
+    if (!topo) return fail(RTG_ERR_INVALID_ARGUMENT, "rtg_rebuild_vtrdyn_f32: NULL topology");
+    if (topo->J != 21)   // main.py:126-136 index the VTRDYN joints 0, 1, 4, 7, 10, 11, 13, 17
+        return fail(RTG_ERR_INVALID_ARGUMENT, "rtg_rebuild_vtrdyn_f32: expects the 21-joint VTRDYN zero pose, got %d",
+                    topo->J);
+    if (B < 0) return fail(RTG_ERR_INVALID_ARGUMENT, "rtg_rebuild_vtrdyn_f32: B < 0");
+    if (B == 0) return RTG_OK;
+    if (!motion || !g_rot || !root_t || !ws) return fail(RTG_ERR_INVALID_ARGUMENT, "rtg_rebuild_vtrdyn_f32: NULL buffer");
+    RTG_TRY(launch_rebuild_vtrdyn(topo->view(), motion, B, g_rot, root_t, ws, as_stream(stream)), "k_rebuild_vtrdyn");
+    return RTG_OK;
+}
+
 // ---------------------------------------------------------------- solvers
 int rtg_solver_create(int kind, const float *zl, const float *zg, const int32_t *parents, int32_t Js,
                       int precise_gripper, rtg_solver_t *out)

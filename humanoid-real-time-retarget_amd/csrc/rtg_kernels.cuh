@@ -69,6 +69,11 @@ hipError_t launch_local_rotation(const TopoView &T, bool state, const float *g, 
 hipError_t launch_fk_multi(FkMultiArgs &A, hipStream_t s);
 hipError_t launch_dof_fk(const TopoView &T, const DofView &D, bool clip, const float *dof, const float *root_rot,
                          const float *root_t, int64_t B, float *gr, float *gp, hipStream_t s);
+hipError_t launch_rescale_motion(const TopoView &T, const float *motion, int64_t B, const float *dir, float *out,
+                                 hipStream_t s);
+hipError_t launch_quat_between(const float *v1, const float *v2, int64_t n, float *out, float *ws, hipStream_t s);
+hipError_t launch_rebuild_vtrdyn(const TopoView &T, const float *motion, int64_t B, float *g_rot, float *root_t,
+                                 float *ws, hipStream_t s);
 hipError_t launch_quat_op(int op, const float *a, const float *b, const float *c, int64_t n, float *out,
                           hipStream_t s);
 hipError_t launch_cal_joint_quat(const float *Z, const float *M, int npts, int64_t n, float *out, hipStream_t s);

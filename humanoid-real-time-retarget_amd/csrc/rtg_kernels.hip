@@ -803,6 +803,150 @@ __global__ __launch_bounds__(kFkTile) void k_dof_fk(TopoView T, DofView D, const
     }
 }
 
+// ----------------------------------------------------------------------------
+// retarget/main.py motion-level prep, one frame per lane.
+// ----------------------------------------------------------------------------
+struct Dir3 {
+    float x, y, z;
+    int32_t on;
+};
+
+// Retarget.rescale_motion_to_standard_size (main.py:37-47) after coord_transform(dir) (:170).  A bone's parent
+// end is the parent's RESCALED position: re-read from this lane's own output row (program order).
+__global__ __launch_bounds__(256) void k_rescale_motion(TopoView T, const float *__restrict__ motion, int64_t B,
+                                                        Dir3 dir, float *__restrict__ out)
+{
+    const int64_t f = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (f >= B) return;
+    const int J = T.J;
+    const float *m = motion + f * J * 3;
+    float *o = out + f * J * 3;
+    auto mp = [&](int j) {
+        const V v = ld3(m + 3 * j);
+        return dir.on ? V{v.x * dir.x, v.y * dir.y, v.z * dir.z} : v;
+    };
+    for (int j = 0; j < J; ++j) {
+        const int p = ld_const(T.parents + j);
+        const V mj = mp(j);
+        if (p < 0) {
+            st3(o + 3 * j, mj);
+            continue;
+        }
+        const V d = vsub(mj, mp(p));
+        const float scale = lnorm3(d) / lnorm3(ld_const(T.local_t + j));
+        const V q = vdiv(d, scale);
+        const V op = ld3(o + 3 * p);
+        st3(o + 3 * j, V{op.x + q.x, op.y + q.y, op.z + q.z});
+    }
+}
+
+// torch.max over a batch of norms: every norm is >= 0 or NaN, so the float bits order as ints once NaN is
+// pinned to the largest pattern.  Wave-reduced, then one atomic per wave.
+RTG_DEV int32_t max_key(float v) { return v != v ? 0x7fffffff : __float_as_int(v); }
+RTG_DEV int32_t wave_max(int32_t v)
+{
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+        const int32_t w = __shfl_xor(v, o, 64);
+        v = w > v ? w : v;
+    }
+    return v;
+}
+RTG_DEV bool batch_small(const float *ws, int i)   // (max norm) <= 1e-6, false for NaN
+{
+    const int32_t k = reinterpret_cast<const int32_t *>(ws)[i];
+    return k != 0x7fffffff && __int_as_float(k) <= 1e-6f;
+}
+
+// quat_between_two_vecs (transform3d.py:8-21) for one pair; `ident`: the batch-level branch of :11-12
+RTG_DEV Q quat_between(V v1, V v2, bool ident)
+{
+    if (ident) return qident();
+    v1 = vdiv(v1, lnorm3(v1));
+    v2 = vdiv(v2, lnorm3(v2));
+    const V c = cross3(v1, v2);
+    return qnormalize(Q{c.x, c.y, c.z, 1.0f + dot3(v1, v2)});   // torch.sum(v1*v2): left fold (measured)
+}
+
+__global__ __launch_bounds__(256) void k_qbtv_norm_max(const float *__restrict__ v1, const float *__restrict__ v2,
+                                                       int64_t n, float *ws)
+{
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    int32_t a = 0, b = 0;
+    if (i < n) {
+        a = max_key(lnorm3(ld3(v1 + 3 * i)));   // torch.norm(dim=-1): the fma form (measured)
+        b = max_key(lnorm3(ld3(v2 + 3 * i)));
+    }
+    a = wave_max(a);
+    b = wave_max(b);
+    if ((threadIdx.x & 63) == 0) {
+        atomicMax(reinterpret_cast<int32_t *>(ws), a);
+        atomicMax(reinterpret_cast<int32_t *>(ws) + 1, b);
+    }
+}
+
+__global__ __launch_bounds__(256) void k_quat_between(const float *__restrict__ v1, const float *__restrict__ v2,
+                                                      int64_t n, const float *ws, float *__restrict__ out)
+{
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const bool ident = batch_small(ws, 0) || batch_small(ws, 1);
+    st4(out + 4 * i, quat_between(ld3(v1 + 3 * i), ld3(v2 + 3 * i), ident));
+}
+
+// _rebuild_with_vtrdyn_zero_pose (main.py:116-165): pass 1, per child joint j the batch max of |m_j - m_p|
+__global__ __launch_bounds__(256) void k_rebuild_norm_max(TopoView T, const float *__restrict__ motion, int64_t B,
+                                                          float *ws)
+{
+    const int64_t f = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const int J = T.J;
+    const float *m = motion + (f < B ? f : 0) * J * 3;
+    for (int j = 1; j < J; ++j) {
+        const int p = ld_const(T.parents + j);
+        if (p == 0 || p == 10) continue;
+        int32_t k = f < B ? max_key(lnorm3(vsub(ld3(m + 3 * j), ld3(m + 3 * p)))) : 0;
+        k = wave_max(k);
+        if ((threadIdx.x & 63) == 0) atomicMax(reinterpret_cast<int32_t *>(ws) + j, k);
+    }
+}
+
+// pass 2: rows 0 and 10 from the Kabsch fits (:126-136); every other row r takes quat_between_two_vecs of its
+// LAST child c (the loop :144-152 overwrites row r once per child, in index order), or stays identity; then
+// SkeletonState.from_rotation_and_root_translation normalises every row (skeleton3d.py:610).
+__global__ __launch_bounds__(256) void k_rebuild_vtrdyn(TopoView T, const float *__restrict__ motion, int64_t B,
+                                                        const float *ws, float *__restrict__ g_rot,
+                                                        float *__restrict__ root_t)
+{
+    const int64_t f = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (f >= B) return;
+    const int J = T.J;
+    const float *m = motion + f * J * 3;
+    float *gr = g_rot + f * J * 4;
+    auto zl = [&](int j) { return ld_const(T.local_t + j); };
+    const V m0 = ld3(m), m10 = ld3(m + 30);
+    {
+        const V Z[3] = {zl(4), zl(1), zl(7)};
+        const V M[3] = {vsub(ld3(m + 12), m0), vsub(ld3(m + 3), m0), vsub(ld3(m + 21), m0)};
+        st4(gr, qnormalize(cal_joint_quat<3>(Z, M)));
+    }
+    {
+        const V Z[3] = {zl(17), zl(13), zl(11)};
+        const V M[3] = {vsub(ld3(m + 51), m10), vsub(ld3(m + 39), m10), vsub(ld3(m + 33), m10)};
+        st4(gr + 40, qnormalize(cal_joint_quat<3>(Z, M)));
+    }
+    for (int r = 1; r < J; ++r) {
+        if (r == 10) continue;
+        int c = -1;   // uniform scalar search: last child of r
+        for (int k = r + 1; k < J; ++k)
+            if (ld_const(T.parents + k) == r) c = k;
+        Q q = qident();
+        if (c > 0)   // batch condition: max |vec1| = |zl_c| (one vector repeated), max |vec2| from pass 1
+            q = quat_between(zl(c), vsub(ld3(m + 3 * c), ld3(m + 3 * r)), lnorm3(zl(c)) <= 1e-6f || batch_small(ws, c));
+        st4(gr + 4 * r, qnormalize(q));
+    }
+    st3(root_t + f * 3, m0);
+}
+
 int32_t fk_schedule(const int32_t *parents, int32_t J, int32_t *sched)
 {
     // last non-consecutive child of every branch parent
@@ -1213,6 +1357,33 @@ hipError_t launch_dof_fk(const TopoView &T, const DofView &D, bool clip, const f
     const size_t lds = fk_stream_lds_bytes(T.nslots);
     if (clip) hipLaunchKernelGGL(k_dof_fk<true>, g, b, lds, s, T, D, dof, root_rot, root_t, B, gr, gp);
     else hipLaunchKernelGGL(k_dof_fk<false>, g, b, lds, s, T, D, dof, root_rot, root_t, B, gr, gp);
+    return hipGetLastError();
+}
+
+hipError_t launch_rescale_motion(const TopoView &T, const float *motion, int64_t B, const float *dir, float *out,
+                                 hipStream_t s)
+{
+    const Dir3 d = dir ? Dir3{dir[0], dir[1], dir[2], 1} : Dir3{1.0f, 1.0f, 1.0f, 0};
+    hipLaunchKernelGGL(k_rescale_motion, dim3(grid_for(B, 256)), dim3(256), 0, s, T, motion, B, d, out);
+    return hipGetLastError();
+}
+
+hipError_t launch_quat_between(const float *v1, const float *v2, int64_t n, float *out, float *ws, hipStream_t s)
+{
+    hipError_t e = hipMemsetAsync(ws, 0, 2 * sizeof(float), s);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(k_qbtv_norm_max, dim3(grid_for(n, 256)), dim3(256), 0, s, v1, v2, n, ws);
+    hipLaunchKernelGGL(k_quat_between, dim3(grid_for(n, 256)), dim3(256), 0, s, v1, v2, n, ws, out);
+    return hipGetLastError();
+}
+
+hipError_t launch_rebuild_vtrdyn(const TopoView &T, const float *motion, int64_t B, float *g_rot, float *root_t,
+                                 float *ws, hipStream_t s)
+{
+    hipError_t e = hipMemsetAsync(ws, 0, T.J * sizeof(float), s);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(k_rebuild_norm_max, dim3(grid_for(B, 256)), dim3(256), 0, s, T, motion, B, ws);
+    hipLaunchKernelGGL(k_rebuild_vtrdyn, dim3(grid_for(B, 256)), dim3(256), 0, s, T, motion, B, ws, g_rot, root_t);
     return hipGetLastError();
 }
 

@@ -254,6 +254,48 @@ def dof_forward_kinematics(model, dof, root_rot, root_t, clip: bool = False):
     return g_rot, g_pos
 
 
+def rescale_motion(topo: Topology, motion, dir=None):
+    """Retarget.rescale_motion_to_standard_size (retarget/main.py:37-47) after coord_transform(dir) (:170)."""
+    J = topo.num_joints
+    m = dev_f32(motion, (J, 3), "motion_global_translation")
+    B = int(torch.Size(m.shape[:-2]).numel())
+    out = torch.empty_like(m)
+    d = None
+    if dir is not None:
+        import numpy as np
+        dv = np.ascontiguousarray(np.asarray(dir.cpu() if isinstance(dir, torch.Tensor) else dir, np.float32).reshape(3))
+        d = dv.ctypes.data_as(ctypes.POINTER(ctypes.c_float))
+    check(lib().rtg_rescale_motion_f32(topo.handle, ptr(m), B, d, ptr(out), stream_handle()))
+    return out
+
+
+def quat_between_two_vecs(v1, v2):
+    """transform3d.py:8-21 (batch-level identity branch included): (..., 3) x (..., 3) -> (..., 4)."""
+    a = dev_f32(v1, (3,), "vec1")
+    b = dev_f32(v2, (3,), "vec2")
+    if a.shape != b.shape:
+        a, b = torch.broadcast_tensors(a, b)
+        a, b = a.contiguous(), b.contiguous()
+    n = int(torch.Size(a.shape[:-1]).numel())
+    out = torch.empty(tuple(a.shape[:-1]) + (4,), device=a.device, dtype=torch.float32)
+    ws = torch.empty(2, device=a.device, dtype=torch.float32)
+    check(lib().rtg_quat_between_f32(ptr(a), ptr(b), n, ptr(out), ptr(ws), stream_handle()))
+    return out
+
+
+def rebuild_vtrdyn(topo: Topology, motion):
+    """RetargetHuV5fromMocap._rebuild_with_vtrdyn_zero_pose (retarget/main.py:116-165) up to its SkeletonState:
+    (B, 21, 3) rescaled positions -> (global rotations (B, 21, 4), root translation (B, 3))."""
+    J = topo.num_joints
+    m = dev_f32(motion, (J, 3), "motion_global_translation")
+    B = int(m.shape[0])
+    g_rot = torch.empty((B, J, 4), device=m.device, dtype=torch.float32)
+    root = torch.empty((B, 3), device=m.device, dtype=torch.float32)
+    ws = torch.empty(J, device=m.device, dtype=torch.float32)
+    check(lib().rtg_rebuild_vtrdyn_f32(topo.handle, ptr(m), B, ptr(g_rot), ptr(root), ptr(ws), stream_handle()))
+    return g_rot, root
+
+
 def forward_kinematics_multi(segments: Sequence[tuple]):
     """One launch over several (topology, local_rot (B,J,4), root_t (B,3)) segments.
 

@@ -109,6 +109,24 @@ int rtg_dof_fk_f32(rtg_dof_model_t model, const float *dof, const float *root_ro
                    int clip, float *g_rot, float *g_pos, rtg_stream_t stream);
 
 /* ------------------------------------------------------------------------
+ * Motion-level prep of the legacy motion path (retarget/main.py)
+ * ---------------------------------------------------------------------- */
+/* Retarget.rescale_motion_to_standard_size (main.py:37-47) after coord_transform(p, dir=dir) (:170;
+ * transform3d.py:24-29).  motion (B,J,3) -> out (B,J,3): every bone scaled to its zero-pose length and hung
+ * from the parent's rescaled position.  dir: 3 floats (host) or NULL. */
+int rtg_rescale_motion_f32(rtg_topology_t topo, const float *motion, int64_t B, const float *dir, float *out,
+                           rtg_stream_t stream);
+/* quat_between_two_vecs (transform3d.py:8-21): v1, v2 (n,3) -> (n,4).  The identity branch is decided over the
+ * whole batch (max norm <= 1e-6, :11-12), as the reference does.  workspace: 2 floats of device memory. */
+int rtg_quat_between_f32(const float *v1, const float *v2, int64_t n, float *out, float *workspace,
+                         rtg_stream_t stream);
+/* RetargetHuV5fromMocap._rebuild_with_vtrdyn_zero_pose (main.py:116-165) up to the SkeletonState it builds
+ * (rotations normalised, skeleton3d.py:610).  topo: the 21-joint VTRDYN zero pose; motion (B,21,3) rescaled
+ * positions -> g_rot (B,21,4) global rotations, root_t (B,3).  workspace: J floats of device memory. */
+int rtg_rebuild_vtrdyn_f32(rtg_topology_t topo, const float *motion, int64_t B, float *g_rot, float *root_t,
+                           float *workspace, rtg_stream_t stream);
+
+/* ------------------------------------------------------------------------
  * Retarget solvers (retarget/retarget_solver/__init__.py:9-14)
  * ---------------------------------------------------------------------- */
 typedef enum rtg_solver_kind {

@@ -115,6 +115,35 @@ def dof_fk(parents, zl, axis, dof, root_rot, root_t, lower=None, upper=None):
     return gr, gp
 
 
+def rescale_motion(parents, zl, motion, dir=None):
+    """retarget/main.py:37-47 after coord_transform(dir) (:170): motion (B, J, 3) -> (B, J, 3)."""
+    p, zl, m = _i32(parents), _c32(zl), _c32(motion)
+    B, J = m.shape[0], len(p)
+    dv = None if dir is None else _c32(np.asarray(dir, np.float32).reshape(3))
+    out = np.empty_like(m)
+    lib().oracle_rescale_motion(p.ctypes.data_as(_i), _fp(zl), ctypes.c_int32(J), _fp(m), _i64(B),
+                                None if dv is None else _fp(dv), _fp(out))
+    return out
+
+
+def quat_between(v1, v2):
+    """quat_between_two_vecs (transform3d.py:8-21), batch-level identity condition included."""
+    a, b = _c32(v1).reshape(-1, 3), _c32(v2).reshape(-1, 3)
+    out = np.empty((a.shape[0], 4), np.float32)
+    lib().oracle_quat_between(_fp(a), _fp(b), _i64(a.shape[0]), _fp(out))
+    return out
+
+
+def rebuild_vtrdyn(parents, zl, motion):
+    """retarget/main.py:116-165 through SkeletonState's normalisation: (B, 21, 3) -> g_rot (B, 21, 4), root (B, 3)."""
+    p, zl, m = _i32(parents), _c32(zl), _c32(motion)
+    B, J = m.shape[0], len(p)
+    gr = np.empty((B, J, 4), np.float32)
+    rt = np.empty((B, 3), np.float32)
+    lib().oracle_rebuild_vtrdyn(p.ctypes.data_as(_i), _fp(zl), ctypes.c_int32(J), _fp(m), _i64(B), _fp(gr), _fp(rt))
+    return gr, rt
+
+
 def local_rotation(parents, g_rot):
     p, g = _i32(parents), _c32(g_rot)
     B, J = g.shape[:2]

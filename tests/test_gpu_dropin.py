@@ -195,3 +195,22 @@ def test_hu_forward_model_dropin(gpu):
     m5 = HuForwardModel(RobotZeroPose.from_asset("hu_v5").skeleton_tree)
     with pytest.raises(ValueError):
         m5.forward_kinematics(torch.zeros(2, 30, 1), torch.zeros(2, 3), torch.zeros(2, 1, 4), clip_angles=True)
+
+
+def test_main_motion_prep_dropin(gpu):
+    """retarget.main (legacy motion path): rescale + rebuild through the drop-in classes."""
+    import oracle as orc
+    from retarget.main import Retarget, RetargetHuV5fromMocap
+    from robot_kinematics_model import RobotZeroPose
+    from rtg import assets
+    d = golden("motion_prep")
+    zp = RobotZeroPose.from_asset("vtrdyn")
+    m = torch.from_numpy(d["raw"]) * torch.tensor([-1.0, -1.0, 1.0])
+    r = Retarget.rescale_motion_to_standard_size(m, zp)
+    assert r.device.type == "cpu"
+    np.testing.assert_array_equal(r.numpy(), d["rescaled"])
+    motion = RetargetHuV5fromMocap(zp, zp)._rebuild_with_vtrdyn_zero_pose(r)
+    ogr, ort = orc.rebuild_vtrdyn(assets.parents("vtrdyn"), golden("zero_pose")["vtrdyn_local_t"], d["rescaled"])
+    np.testing.assert_array_equal(motion.global_rotation.cpu().numpy(), ogr)
+    np.testing.assert_array_equal(motion.root_translation.cpu().numpy(), ort)
+    assert motion.global_velocity.shape == (len(ogr), 21, 3)

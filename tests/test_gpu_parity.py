@@ -195,6 +195,43 @@ def test_dof_fk_roundtrip_with_retargeted_dofs(gpu):
     assert np.abs(_np(gp) - _np(fp))[:, :18].max() < 1e-4
 
 
+def test_motion_prep_vs_oracle_and_reference(gpu):
+    """retarget/main.py prep: rescale + quat_between_two_vecs + rebuild, bit-exact vs the
+    oracle (golden motion and 50000 random frames); rescale / quat_between bit-exact vs the reference."""
+    import oracle as orc
+    from rtg import assets, ops
+    d = golden("motion_prep")
+    zl = golden("zero_pose")["vtrdyn_local_t"]
+    par = assets.parents("vtrdyn")
+    T = _topo("vtrdyn")
+    r = _np(ops.rescale_motion(T, d["raw"], dir=[-1.0, -1.0, 1.0]))
+    np.testing.assert_array_equal(r, d["rescaled"])
+    np.testing.assert_array_equal(_np(ops.quat_between_two_vecs(d["qb_v1"], d["qb_v2"])), d["qb"])
+    np.testing.assert_array_equal(_np(ops.quat_between_two_vecs(d["qb_v1"][:4], np.zeros((4, 3), np.float32))),
+                                  d["qb_zero"])
+    gr, rt = ops.rebuild_vtrdyn(T, d["rescaled"])
+    ogr, ort = orc.rebuild_vtrdyn(par, zl, d["rescaled"])
+    np.testing.assert_array_equal(_np(gr), ogr)
+    np.testing.assert_array_equal(_np(rt), ort)
+    rng = np.random.default_rng(5)
+    x = (d["raw"][rng.integers(0, len(d["raw"]), 50000)] * rng.uniform(0.7, 1.3, (50000, 1, 1))
+         + rng.normal(0, 0.02, (50000, 21, 3))).astype(np.float32)
+    x[7, 12] = x[7, 11]                       # a zero-length bone in one frame: NaN quat there, as the reference
+    r = _np(ops.rescale_motion(T, x, dir=[-1.0, -1.0, 1.0]))
+    orr = orc.rescale_motion(par, zl, x, dir=[-1.0, -1.0, 1.0])
+    np.testing.assert_array_equal(r, orr)
+    gr, rt = ops.rebuild_vtrdyn(T, orr)
+    ogr, ort = orc.rebuild_vtrdyn(par, zl, orr)
+    np.testing.assert_array_equal(_np(gr), ogr)
+    np.testing.assert_array_equal(_np(rt), ort)
+    y = x.copy()
+    y[:, 12] = y[:, 11]                       # degenerate for EVERY frame: the batch-level identity branch
+    gr, _ = ops.rebuild_vtrdyn(T, y)
+    ogr, _ = orc.rebuild_vtrdyn(par, zl, y)
+    np.testing.assert_array_equal(_np(gr), ogr)
+    assert (ogr[:, 11] == np.array([0, 0, 0, 1], np.float32)).all()
+
+
 # ----------------------------------------------------------------- primitives
 def test_quaternion_algebra_bit_exact(gpu):
     from rtg import ops

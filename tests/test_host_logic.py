@@ -83,6 +83,7 @@ def test_dropin_modules_import_without_gpu():
     import robot_kinematics_model  # noqa: F401
     from retarget.retarget_solver import VtrdynFullBodyPosRetargeter  # noqa: F401
     from robot_kinematics_model.hu_forward_model import HuForwardModel  # noqa: F401
+    from retarget.main import Retarget, RetargetHuV5fromMocap  # noqa: F401
 
 
 @pytest.mark.skipif(__import__("torch").cuda.is_available(), reason="checks the no-GPU behaviour")

@@ -243,3 +243,23 @@ def test_dof_fk_attribution_torch_sincos(tag, name):
     gr, gp = orc.fk(assets.parents(name), assets.local_translation(name), lr, d[f"{tag}_root_t"])
     np.testing.assert_array_equal(gr, d[f"{tag}_g_rot"])
     np.testing.assert_array_equal(gp, d[f"{tag}_g_pos"])
+
+
+def test_motion_prep_vs_reference():
+    """retarget/main.py prep, pinned to the reference's own functions:
+    coord_transform + rescale_motion_to_standard_size bit-exact; quat_between_two_vecs bit-exact (incl. the
+    batch-level identity branch); _rebuild_with_vtrdyn_zero_pose's rotations bit-exact except the two Kabsch
+    rows (0, 10: MKL sgesdd, the residual bound of the solvers)."""
+    from rtg import assets
+    d = golden("motion_prep")
+    par, zl = assets.parents("vtrdyn"), golden("zero_pose")["vtrdyn_local_t"]
+    r = orc.rescale_motion(par, zl, d["raw"], dir=[-1.0, -1.0, 1.0])
+    np.testing.assert_array_equal(r, d["rescaled"])
+    np.testing.assert_array_equal(orc.quat_between(d["qb_v1"], d["qb_v2"]), d["qb"])
+    np.testing.assert_array_equal(orc.quat_between(d["qb_v1"][:4], np.zeros((4, 3), np.float32)), d["qb_zero"])
+    gr, rt = orc.rebuild_vtrdyn(par, zl, d["rescaled"])
+    np.testing.assert_array_equal(rt, d["root_t"])
+    other = [j for j in range(21) if j not in (0, 10)]
+    np.testing.assert_array_equal(gr[:, other], d["g_rot"][:, other])
+    e = np.abs(gr[:, [0, 10]] - d["g_rot"][:, [0, 10]]).reshape(len(gr), -1).max(1)   # per-frame max
+    assert e.max() <= 5e-4 and np.median(e) <= 5e-6 and (e > 1e-5).mean() <= 0.2, (e.max(), np.median(e))

@@ -172,6 +172,36 @@ def gen_dof_fk(ref, torch, n):
     return out
 
 
+def gen_motion_prep(ref, torch, L=64):
+    """retarget/main.py motion-level prep, called on the reference's own code:
+    coord_transform (:170) -> Retarget.rescale_motion_to_standard_size (:37-47) ->
+    RetargetHuV5fromMocap._rebuild_with_vtrdyn_zero_pose (:116-165, its SkeletonMotion's global rotations).
+    Inputs: smooth synthetic VTRDyn body motion (21 joints, raw mocap frame).  Also quat_between_two_vecs
+    (transform3d.py:8-21) on random pairs and on an all-degenerate batch (the batch-level identity branch)."""
+    main = rh.load_main_module(ref)
+    zp = rh.ref_zero_pose(ref, "vtrdyn")
+    x = synth.synth_upper_body_inputs(L, 4242)                     # raw VTRDyn positions (B, 21, 3)
+    g = np.random.default_rng(4243)                                  # other body sizes + marker jitter:
+    x = (x * g.uniform(0.8, 1.25, (L, 1, 1)) + g.normal(0, 0.01, x.shape)).astype(np.float32)   # rescale has work
+    xt = torch.from_numpy(x)
+    m = ref.transform3d.coord_transform(xt, dir=torch.Tensor([-1, -1, 1]))
+    rescaled = main.Retarget.rescale_motion_to_standard_size(m, zp)
+    rt = main.RetargetHuV5fromMocap(zp, zp)
+    import contextlib
+    import io
+    with contextlib.redirect_stdout(io.StringIO()):               # it prints the rebuild error
+        motion = rt._rebuild_with_vtrdyn_zero_pose(rescaled)
+    rng = np.random.default_rng(77)
+    v1 = rng.normal(size=(512, 3)).astype(np.float32)
+    v2 = rng.normal(size=(512, 3)).astype(np.float32)
+    v2[:8] = -v1[:8]                                                 # antiparallel: real part 1 + dot ~ 0
+    v2[8:16] = v1[8:16] * 3.0                                         # parallel
+    qb = ref.transform3d.quat_between_two_vecs(torch.from_numpy(v1), torch.from_numpy(v2))
+    qb0 = ref.transform3d.quat_between_two_vecs(torch.from_numpy(v1[:4]), torch.zeros(4, 3))
+    return {"raw": x, "rescaled": t2n(rescaled), "g_rot": t2n(motion.global_rotation),
+            "root_t": t2n(motion.root_translation), "qb_v1": v1, "qb_v2": v2, "qb": t2n(qb), "qb_zero": t2n(qb0)}
+
+
 def _rand_quats(rng, n):
     q = rng.normal(size=(n, 4))
     q /= np.linalg.norm(q, axis=-1, keepdims=True)
@@ -347,6 +377,7 @@ def main() -> None:
         "motion": lambda: gen_motion(ref, torch),
         "kat_rotation_test": lambda: gen_kat(ref, torch),
         "dof_fk": lambda: gen_dof_fk(ref, torch, 128),
+        "motion_prep": lambda: gen_motion_prep(ref, torch),
     }
     only = set(sys.argv[1:])
     for name, fn in jobs.items():

@@ -118,3 +118,21 @@ def load_body_retargeter_module(ref):
     """``body_retargeter`` imports vedo_visualizer at module level; stubs cover it."""
     from retarget.retarget_solver import body_retargeter
     return body_retargeter
+
+
+def load_main_module(ref):
+    """retarget/main.py (the legacy motion-level path) needs three names the reference does not provide
+    (SURVEY §8c): the alias retarget.robot_kinematics_model -> robot_kinematics_model,
+    retarget.utils.get_mocap_translation (CSV reader, unused here) and body_visualizer.common (viewer)."""
+    import importlib
+    import robot_kinematics_model
+    sys.modules.setdefault("retarget.robot_kinematics_model", robot_kinematics_model)
+    import retarget.utils as ru
+    if not hasattr(ru, "get_mocap_translation"):
+        ru.get_mocap_translation = lambda *a, **k: None
+    if "body_visualizer" not in sys.modules:
+        bv = _stub("body_visualizer")
+        bv.common = _stub("body_visualizer.common", vis_vtrdyn=lambda *a, **k: None)
+    if "poselib.poselib.visualization.common" not in sys.modules:
+        _stub("poselib.poselib.visualization.common", plot_skeleton_H=lambda *a, **k: None)
+    return importlib.import_module("retarget.main")
