@@ -298,6 +298,18 @@ int rtg_dof_fk_f32(rtg_dof_model_t m, const float *dof, const float *root_rot, c
     return RTG_OK;
 }
 
+// ---------------------------------------------------------------- VTRDyn ingest
+int rtg_ingest_vtrdyn_f32(const float *bp, const float *lhp, const float *rhp, int64_t B, float *body, float *lh,
+                          float *rh, uint8_t *valid, rtg_stream_t stream)
+{
+    if (B < 0) return fail(RTG_ERR_INVALID_ARGUMENT, "rtg_ingest_vtrdyn_f32: B < 0");
+    if (B == 0) return RTG_OK;
+    if (!bp || !lhp || !rhp || !body || !lh || !rh || !valid)
+        return fail(RTG_ERR_INVALID_ARGUMENT, "rtg_ingest_vtrdyn_f32: NULL buffer");
+    RTG_TRY(launch_ingest_vtrdyn(bp, lhp, rhp, B, body, lh, rh, valid, as_stream(stream)), "k_ingest_vtrdyn");
+    return RTG_OK;
+}
+
 // ---------------------------------------------------------------- motion-level prep (retarget/main.py)
 int rtg_rescale_motion_f32(rtg_topology_t topo, const float *motion, int64_t B, const float *dir, float *out,
                            rtg_stream_t stream)

@@ -74,6 +74,8 @@ hipError_t launch_rescale_motion(const TopoView &T, const float *motion, int64_t
 hipError_t launch_quat_between(const float *v1, const float *v2, int64_t n, float *out, float *ws, hipStream_t s);
 hipError_t launch_rebuild_vtrdyn(const TopoView &T, const float *motion, int64_t B, float *g_rot, float *root_t,
                                  float *ws, hipStream_t s);
+hipError_t launch_ingest_vtrdyn(const float *bp, const float *lhp, const float *rhp, int64_t B, float *body,
+                                float *lh, float *rh, uint8_t *valid, hipStream_t s);
 hipError_t launch_quat_op(int op, const float *a, const float *b, const float *c, int64_t n, float *out,
                           hipStream_t s);
 hipError_t launch_cal_joint_quat(const float *Z, const float *M, int npts, int64_t n, float *out, hipStream_t s);

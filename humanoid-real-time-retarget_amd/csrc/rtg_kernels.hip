@@ -947,6 +947,30 @@ __global__ __launch_bounds__(256) void k_rebuild_vtrdyn(TopoView T, const float 
     st3(root_t + f * 3, m0);
 }
 
+// ----------------------------------------------------------------------------
+// VTRDyn ingest: sim_full_body_teleop.py:109 (body 23 -> 21), :111-112 (hand order), :92 (skip all-zero frames)
+// ----------------------------------------------------------------------------
+__constant__ int8_t c_body23_to_21[21] = {0, 1, 2, 3, 5, 6, 7, 9, 10, 11, 12, 13, 14, 15, 16, 17, 18, 19, 20, 21, 22};
+__constant__ int8_t c_hand_order[20] = {0, 4, 5, 6, 7, 8, 9, 10, 11, 16, 17, 18, 19, 12, 13, 14, 15, 1, 2, 3};
+
+__global__ __launch_bounds__(256) void k_ingest_vtrdyn(const float *__restrict__ bp, const float *__restrict__ lhp,
+                                                       const float *__restrict__ rhp, int64_t B,
+                                                       float *__restrict__ body, float *__restrict__ lh,
+                                                       float *__restrict__ rh, uint8_t *__restrict__ valid)
+{
+    const int64_t f = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (f >= B) return;
+    const float *b = bp + f * 69;
+    bool close = true;   // np.allclose(body_pos, 0): |x| <= 1e-8 everywhere (a NaN is never close)
+    for (int i = 0; i < 69; ++i) close = close && (fabsf(b[i]) <= 1e-8f);
+    valid[f] = close ? 0 : 1;
+    for (int j = 0; j < 21; ++j) st3(body + f * 63 + 3 * j, ld3(b + 3 * c_body23_to_21[j]));
+    for (int j = 0; j < 20; ++j) {
+        st3(lh + f * 60 + 3 * j, ld3(lhp + f * 60 + 3 * c_hand_order[j]));
+        st3(rh + f * 60 + 3 * j, ld3(rhp + f * 60 + 3 * c_hand_order[j]));
+    }
+}
+
 int32_t fk_schedule(const int32_t *parents, int32_t J, int32_t *sched)
 {
     // last non-consecutive child of every branch parent
@@ -1384,6 +1408,13 @@ hipError_t launch_rebuild_vtrdyn(const TopoView &T, const float *motion, int64_t
     if (e != hipSuccess) return e;
     hipLaunchKernelGGL(k_rebuild_norm_max, dim3(grid_for(B, 256)), dim3(256), 0, s, T, motion, B, ws);
     hipLaunchKernelGGL(k_rebuild_vtrdyn, dim3(grid_for(B, 256)), dim3(256), 0, s, T, motion, B, ws, g_rot, root_t);
+    return hipGetLastError();
+}
+
+hipError_t launch_ingest_vtrdyn(const float *bp, const float *lhp, const float *rhp, int64_t B, float *body,
+                                float *lh, float *rh, uint8_t *valid, hipStream_t s)
+{
+    hipLaunchKernelGGL(k_ingest_vtrdyn, dim3(grid_for(B, 256)), dim3(256), 0, s, bp, lhp, rhp, B, body, lh, rh, valid);
     return hipGetLastError();
 }
 

@@ -74,6 +74,8 @@ SIGNATURES = {
     "rtg_dof_model_create": (c_int, [c_void_p, POINTER(c_int32), POINTER(c_float), POINTER(c_float),
                                      POINTER(c_void_p)]),
     "rtg_dof_model_destroy": (c_int, [c_void_p]),
+    "rtg_ingest_vtrdyn_f32": (c_int, [c_void_p, c_void_p, c_void_p, c_int64, c_void_p, c_void_p, c_void_p, c_void_p,
+                                      c_void_p]),
     "rtg_rescale_motion_f32": (c_int, [c_void_p, c_void_p, c_int64, POINTER(c_float), c_void_p, c_void_p]),
     "rtg_quat_between_f32": (c_int, [c_void_p, c_void_p, c_int64, c_void_p, c_void_p, c_void_p]),
     "rtg_rebuild_vtrdyn_f32": (c_int, [c_void_p, c_void_p, c_int64, c_void_p, c_void_p, c_void_p, c_void_p]),

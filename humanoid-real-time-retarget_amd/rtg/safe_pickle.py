@@ -39,6 +39,7 @@ class Global:
 class Call:
     func: Any
     args: Any
+    state: Any = None   # BUILD applied to the call's result (numpy arrays: __setstate__ tuple)
 
 
 @dataclass
@@ -89,7 +90,7 @@ def _run_vm(stream: io.BytesIO) -> Any:
             pop_mark()
         elif n in ("SHORT_BINUNICODE", "BINUNICODE", "BINUNICODE8", "UNICODE",
                    "SHORT_BINSTRING", "BINSTRING", "STRING",
-                   "BINBYTES", "SHORT_BINBYTES", "BINBYTES8",
+                   "BINBYTES", "SHORT_BINBYTES", "BINBYTES8", "BYTEARRAY8",
                    "BININT", "BININT1", "BININT2", "LONG1", "LONG4", "INT", "LONG",
                    "BINFLOAT", "FLOAT"):
             stack.append(arg)
@@ -157,7 +158,7 @@ def _run_vm(stream: io.BytesIO) -> Any:
         elif n == "BUILD":
             state = stack.pop()
             target = stack[-1]
-            if isinstance(target, Obj):
+            if isinstance(target, (Obj, Call)):
                 target.state = state
             else:
                 raise ValueError(f"BUILD on unsupported target {type(target)}")

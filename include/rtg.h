@@ -109,6 +109,15 @@ int rtg_dof_fk_f32(rtg_dof_model_t model, const float *dof, const float *root_ro
                    int clip, float *g_rot, float *g_pos, rtg_stream_t stream);
 
 /* ------------------------------------------------------------------------
+ * VTRDyn ingest (sim_full_body_teleop.py:92, :109-112)
+ * ---------------------------------------------------------------------- */
+/* Raw broadcast frames body_pos (B,23,3), left/right_hand_pos (B,20,3) -> solver inputs body (B,21,3)
+ * (23 -> 21 joint reindex), hands (B,20,3) (point reorder), and valid (B) uint8: 0 where every body value
+ * is within 1e-8 of 0 (np.allclose(body_pos, 0): the teleop loop keeps the previous DOFs), else 1. */
+int rtg_ingest_vtrdyn_f32(const float *body_pos, const float *left_hand, const float *right_hand, int64_t B,
+                          float *body, float *lh, float *rh, uint8_t *valid, rtg_stream_t stream);
+
+/* ------------------------------------------------------------------------
  * Motion-level prep of the legacy motion path (retarget/main.py)
  * ---------------------------------------------------------------------- */
 /* Retarget.rescale_motion_to_standard_size (main.py:37-47) after coord_transform(p, dir=dir) (:170;
