@@ -98,6 +98,61 @@ def pmc_traffic(B):
     return rec["traffic_bytes"]
 
 
+def secondary_configs(solver, sets, stream):
+    """BASELINE configs 2 and 5 on the same GPU (reported beside the headline line, not as `value`):
+    config 2 = 4096 frames per launch (latency-bound regime), kernel-only and PCIe-inclusive (pinned host
+    frames in, DOFs back); config 5 = FK of 4 robot_config skeletons x 65536 frames in one launch."""
+    import torch
+    from rtg import assets, ops, synth
+    from rtg.runtime import Topology
+    out = {}
+    b, l, r_, _ = sets[0]
+    n = 4096
+    xb, xl, xr = b[:n].contiguous(), l[:n].contiguous(), r_[:n].contiguous()
+    d = torch.empty((n, 30), device=b.device)
+    for _ in range(10):
+        solver.retarget([xb, xl, xr], out_dof=d)
+    reps = 200
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record(stream)
+    for _ in range(reps):
+        solver.retarget([xb, xl, xr], out_dof=d)
+    e1.record(stream)
+    e1.synchronize()
+    k_ms = e0.elapsed_time(e1) / reps
+    hb, hl, hr = (t.cpu().pin_memory() for t in (xb, xl, xr))
+    hd = torch.empty((n, 30)).pin_memory()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(50):
+        xb.copy_(hb, non_blocking=True); xl.copy_(hl, non_blocking=True); xr.copy_(hr, non_blocking=True)
+        solver.retarget([xb, xl, xr], out_dof=d)
+        hd.copy_(d, non_blocking=True)
+        torch.cuda.synchronize()
+    e2e_ms = (time.perf_counter() - t0) * 1e3 / 50
+    out["config2_batch4096"] = {"kernel_ms": k_ms, "frames_per_s": n / (k_ms * 1e-3), "e2e_pcie_ms": e2e_ms,
+                                "e2e_pcie_frames_per_s": n / (e2e_ms * 1e-3)}
+    segs, nbytes = [], 0
+    for i, name in enumerate(["hu_v5", "vtrdyn", "vtrdyn_full", "noitom"]):
+        t = Topology(assets.parents(name), assets.local_translation(name), assets.tree_quat(name))
+        J = t.num_joints
+        segs.append((t, torch.from_numpy(synth.random_local_quats(65536, J, 10 + i)).cuda(),
+                     torch.zeros((65536, 3), device="cuda")))
+        nbytes += 65536 * (J * 16 + 12 + J * 28)
+    for _ in range(5):
+        ops.forward_kinematics_multi(segs)
+    e0.record(stream)
+    for _ in range(50):
+        ops.forward_kinematics_multi(segs)
+    e1.record(stream)
+    e1.synchronize()
+    ms = e0.elapsed_time(e1) / 50
+    out["config5_mixed_fk_4x65536"] = {"kernel_ms": ms, "frames_per_s": 4 * 65536 / (ms * 1e-3),
+                                       "GBs_algorithmic": nbytes / (ms * 1e-3) / 1e9,
+                                       "hbm_frac": nbytes / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS}
+    return out
+
+
 def parity_vs_reference():
     """max / p99 |dof_gpu - dof_ref| on the committed reference golden vectors."""
     import torch
@@ -194,6 +249,11 @@ def main():
         }
         if gather_ms is not None:
             line["gather_ms"] = gather_ms
+        if world == 1:
+            try:
+                line["secondary"] = secondary_configs(solver, sets, stream)
+            except Exception as e:  # noqa: BLE001
+                line["secondary"] = {"error": repr(e)}
         try:
             line["parity_vs_reference"] = parity_vs_reference()
         except Exception as e:  # noqa: BLE001

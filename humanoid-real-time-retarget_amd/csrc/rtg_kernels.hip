@@ -483,8 +483,12 @@ __global__ __launch_bounds__(256) void k_local_rotation(TopoView T, const float 
 // conflict-free) + 6.4 KiB position window (odd pitch 25) + 1.8 KiB per slot,
 // ~19 KiB for every shipped skeleton, i.e. 8 waves per CU whatever J is.
 // ----------------------------------------------------------------------------
+#ifndef RTG_FK_CHUNK
+#define RTG_FK_CHUNK 8
+#endif
 constexpr int kFkTile = 64;
-constexpr int kFkChunk = 8;
+constexpr int kFkChunk = RTG_FK_CHUNK;   // joints per LDS window (4 or 8)
+static_assert(kFkChunk == 4 || kFkChunk == 8, "window of 4 or 8 joints");
 constexpr int kRotPitch = 4 * (kFkChunk + 1);   // floats per frame row (LDS)
 constexpr int kPosPitch = 3 * kFkChunk + 1;
 
@@ -518,7 +522,7 @@ RTG_DEV void chunk_load(ChunkRegs &r, const float *__restrict__ g, int64_t f0, i
     // unconditional loads (lanes past the tile re-read the tile's first element)
     // keep the prefetch registers fully defined across the chunk loop
 #define RTG_LD(I)                                                                          \
-    {                                                                                      \
+    if ((I) < kFkChunk) {                                                                  \
         const int v = (I) * kFkTile + (int)threadIdx.x;                                    \
         const int fr = v / kFkChunk, k = v % kFkChunk;                                     \
         const int64_t e = (fr < nfr && k < nC) ? (f0 + fr) * J + c0 + k : f0 * J;         \
@@ -531,7 +535,7 @@ RTG_DEV void chunk_to_lds(const ChunkRegs &r, float *lds, int nfr, int nC)
 {
     const bool full = nfr == kFkTile && nC == kFkChunk;   // unpredicated: the writes issue back to back
 #define RTG_ST(I)                                                                          \
-    {                                                                                      \
+    if ((I) < kFkChunk) {                                                                  \
         const int v = (I) * kFkTile + (int)threadIdx.x;                                    \
         const int fr = v / kFkChunk, k = v % kFkChunk;                                     \
         if (full || (fr < nfr && k < nC)) st4(lds + fr * kRotPitch + k * 4, r.v##I);       \
