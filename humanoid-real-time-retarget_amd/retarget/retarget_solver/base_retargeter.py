@@ -29,6 +29,7 @@ class BaseHumanoidRetargeter(ABC):
         self._motion_dof_pos = []
         self._solver = None
         self._precise = bool(precise_gripper)
+        self._frame_graphs = {}
 
     # -- device solver (built lazily so construction works before a GPU is touched)
     @property
@@ -43,8 +44,15 @@ class BaseHumanoidRetargeter(ABC):
         return self._solver
 
     def _solve(self, inputs: Sequence, batched: bool, want_body_rot=False):
-        """Run the device solver on (B, ...) or single-frame inputs; returns (local_rot, dof, body_rot)."""
+        """Run the device solver on (B, ...) or single-frame inputs; returns (local_rot, dof, body_rot).
+        A single frame of host inputs (the live teleop loop) replays a captured HIP graph (rtg.realtime)."""
         dev = home_device(*inputs)
+        if not batched and dev.type == "cpu":
+            g = self._frame_graphs.get(bool(want_body_rot))
+            if g is None:
+                from rtg.realtime import FrameGraph
+                g = self._frame_graphs[bool(want_body_rot)] = FrameGraph(self.solver, want_body_rot)
+            return g(*inputs)
         tails = [tuple(as_tensor(x).shape[-2:]) for x in inputs]
         xs = [dev_f32(as_tensor(x).reshape(-1, *t)) for x, t in zip(inputs, tails)]
         dof, lr, br = self.solver.retarget(xs, want_local_rot=True, want_body_rot=want_body_rot)

@@ -148,6 +148,10 @@ class Solver:
         self.kind = int(kind)
         self.precise_gripper = bool(precise_gripper)
 
+    @property
+    def handle(self) -> ctypes.c_void_p:
+        return self._h
+
     def retarget(self, inputs: Sequence[torch.Tensor], want_local_rot=False, want_body_rot=False,
                  out_dof: Optional[torch.Tensor] = None, stream=None):
         """Batched solve.  ``inputs``: device float32 tensors in the order of rtg.h.

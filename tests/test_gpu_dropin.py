@@ -214,3 +214,24 @@ def test_main_motion_prep_dropin(gpu):
     np.testing.assert_array_equal(motion.global_rotation.cpu().numpy(), ogr)
     np.testing.assert_array_equal(motion.root_translation.cpu().numpy(), ort)
     assert motion.global_velocity.shape == (len(ogr), 21, 3)
+
+
+def test_per_frame_graph_matches_batched(gpu):
+    """The teleop per-frame call (host tensors -> captured HIP graph, rtg.realtime.FrameGraph) returns exactly
+    the batched solve's rows, frame after frame."""
+    from retarget.retarget_solver import VtrdynFullBodyPosRetargeter
+    from robot_kinematics_model import RobotZeroPose
+    g = golden("full_body_pos_precise")
+    hu = VtrdynFullBodyPosRetargeter(RobotZeroPose.from_asset("vtrdyn_full"), RobotZeroPose.from_asset("hu_v5"),
+                                     precise_gripper=True)
+    n = 40
+    lr_b, dof_b, br_b = hu.retarget_batch(torch.from_numpy(g["body"][:n]), torch.from_numpy(g["lh"][:n]),
+                                          torch.from_numpy(g["rh"][:n]), want_body_rot=True)
+    for i in range(n):
+        lr, dof, br = hu.retarget(torch.from_numpy(g["body"][i]), torch.from_numpy(g["lh"][i]),
+                                  torch.from_numpy(g["rh"][i]))
+        assert lr.device.type == "cpu" and dof.shape == (30,) and br.shape == (59, 4)
+        np.testing.assert_array_equal(dof.numpy(), dof_b[i].numpy())
+        np.testing.assert_array_equal(lr.numpy(), lr_b[i].numpy())
+        np.testing.assert_array_equal(br.numpy(), br_b[i].numpy())
+    assert hu.motion_length == n

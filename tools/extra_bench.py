@@ -70,6 +70,27 @@ def latency():
             ts.append(time.perf_counter() - t0)
         out[str(B)] = {"kernel_us": k_ms * 1e3, "e2e_median_us": float(np.median(ts) * 1e6),
                        "e2e_p99_us": float(np.quantile(ts, 0.99) * 1e6)}
+    # the drop-in per-frame call of the teleop loop (host tensors in/out; captured HIP graph, rtg.realtime)
+    from rtg.realtime import FrameGraph
+    sys.path.insert(0, os.path.join(REPO, "humanoid-real-time-retarget_amd"))
+    from retarget.retarget_solver import VtrdynFullBodyPosRetargeter
+    from robot_kinematics_model import RobotZeroPose
+    hu = VtrdynFullBodyPosRetargeter(RobotZeroPose.from_asset("vtrdyn_full"), RobotZeroPose.from_asset("hu_v5"),
+                                     precise_gripper=True)
+    fb, fl, fr = (torch.from_numpy(np.ascontiguousarray(g[k][0])) for k in ("body", "lh", "rh"))
+    fg = FrameGraph(S, want_body_rot=False)
+    for name, fn in (("dropin_retarget_per_frame", lambda: hu.retarget(fb, fl, fr)),
+                     ("dropin_batch_of_one_no_graph",
+                      lambda: hu.retarget_batch(fb[None], fl[None], fr[None], want_body_rot=True)),
+                     ("frame_graph_dof_local_rot", lambda: fg(fb, fl, fr))):
+        for _ in range(20):
+            fn()
+        ts = []
+        for _ in range(500):
+            t0 = time.perf_counter()
+            fn()
+            ts.append(time.perf_counter() - t0)
+        out[name] = {"median_us": float(np.median(ts) * 1e6), "p99_us": float(np.quantile(ts, 0.99) * 1e6)}
     return out
 
 
