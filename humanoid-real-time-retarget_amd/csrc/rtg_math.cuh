@@ -28,7 +28,27 @@ struct V { float x, y, z; };
 #define RTG_DEV __device__ __forceinline__
 
 // ---------------------------------------------------------------- helpers
-RTG_DEV float cr_sqrt(float x) { return __builtin_sqrtf(x); }   // IEEE sqrt (correctly rounded build)
+RTG_DEV float ieee_sqrtf(float x) { return __builtin_sqrtf(x); }   // IEEE sqrt (correctly rounded build)
+#ifndef RTG_FAST_EXACT
+#define RTG_FAST_EXACT 1
+#endif
+// Correctly rounded f32 sqrt in 6 instructions: v_sqrt_f64 (not accurate enough alone: it misses on 4 % of
+// inputs) plus one Newton correction gives ~2^-100, and sqrt of an f32 is never within 2^-51 of an f32
+// midpoint, so the single rounding is exact.  0 / inf / NaN / negative: the residual is 0 or NaN and the raw
+// v_sqrt_f64 value (IEEE for those) is kept.  Proven equal to __builtin_sqrtf on all 2^32 inputs by
+// tools/check_fastmath.hip (run by tests/test_gpu_parity.py).
+RTG_DEV float cr_sqrt(float x)
+{
+#if RTG_FAST_EXACT
+    const double d = (double)x;
+    const double y = __builtin_amdgcn_sqrt(d);
+    const double r = __builtin_fma(-y, y, d);
+    const double y1 = __builtin_fma(r, 0.5 * __builtin_amdgcn_rcp(y), y);
+    return (float)((r == 0.0 || r != r) ? y : y1);
+#else
+    return __builtin_sqrtf(x);
+#endif
+}
 RTG_DEV float cr_acos(float x) { return (float)::acos((double)x); }
 RTG_DEV float cr_sin(float x) { return (float)::sin((double)x); }
 RTG_DEV float cr_cos(float x) { return (float)::cos((double)x); }
@@ -46,8 +66,37 @@ RTG_DEV SC cr_sincos(double x)
 // rounding midpoint, and the f64 product is within 2^-52; checked on 4.3e9
 // random pairs incl. subnormals / zeros / infinities, tests/test_oracle_golden.py.)
 // One f64 reciprocal replaces k correctly rounded f32 divide sequences.
-RTG_DEV double rcp64(float n) { return 1.0 / (double)n; }
-RTG_DEV float mulr(float a, double r) { return (float)((double)a * r); }
+// 1/n for k divisions by one denominator: v_rcp_f64 + two Newton steps, i.e. RN(1/n) to within an ulp even
+// from a 14-bit estimate (the IEEE f64 divide sequence is twice as long).  0 / inf / NaN make the residual NaN;
+// the raw v_rcp_f64 value (inf, 0, NaN) is then the IEEE answer.
+struct Rcp {
+    double r;
+    float n;
+};
+RTG_DEV Rcp rcp64(float n)
+{
+#if RTG_FAST_EXACT
+    const double d = (double)n;
+    const double r0 = __builtin_amdgcn_rcp(d);
+    const double e0 = __builtin_fma(-d, r0, 1.0);
+    const double r1 = __builtin_fma(r0, e0, r0);
+    const double e1 = __builtin_fma(-d, r1, 1.0);
+    return Rcp{e0 == e0 ? __builtin_fma(r1, e1, r1) : r0, n};
+#else
+    return Rcp{1.0 / (double)n, n};
+#endif
+}
+// RN(a/n) == (float)((double)a * 1/n) whenever the quotient is a normal f32: an f32 quotient is never within
+// 2^-50 (relative) of an f32 midpoint and the f64 product is within 2^-52.  A subnormal quotient (absolute
+// grid) takes the IEEE division; that branch is rare and divergent.  tools/check_fastmath.hip: 2^32 random
+// pairs + all special-value pairs, 0 mismatches.
+RTG_DEV float mulr(float a, const Rcp &r)
+{
+    const double p = (double)a * r.r;
+    float q = (float)p;
+    if (__builtin_expect(__builtin_fabs(p) < 0x1p-126 && p != 0.0, 0)) q = a / r.n;
+    return q;
+}
 RTG_DEV float tsign(float v) { return v > 0.0f ? 1.0f : (v < 0.0f ? -1.0f : 0.0f); }
 RTG_DEV float clamp_lo(float v, float lo) { return v < lo ? lo : v; }          // NaN passes through
 RTG_DEV float clamp_lohi(float v, float lo, float hi) { return v < lo ? lo : (v > hi ? hi : v); }
@@ -160,7 +209,7 @@ RTG_DEV Q qnormalize(Q q)  // quat_unit(quat_pos(q)) :30-56,92-98
     q.x = f * q.x; q.y = f * q.y; q.z = f * q.z; q.w = f * q.w;
     float n = cr_sqrt(((q.x * q.x + q.y * q.y) + q.z * q.z) + q.w * q.w);
     n = clamp_lo(n, 1e-9f);
-    const double r = rcp64(n);
+    const Rcp r = rcp64(n);
     return Q{mulr(q.x, r), mulr(q.y, r), mulr(q.z, r), mulr(q.w, r)};
 }
 RTG_DEV Q qmul_norm(Q a, Q b) { return qnormalize(qmul(a, b)); }
@@ -168,7 +217,7 @@ RTG_DEV float qabs(Q q) { return cr_sqrt(((q.x * q.x + q.y * q.y) + q.z * q.z) +
 RTG_DEV Q qunit(Q q)                                                                                 // :50-56
 {
     const float n = clamp_lo(qabs(q), 1e-9f);
-    const double r = rcp64(n);
+    const Rcp r = rcp64(n);
     return Q{mulr(q.x, r), mulr(q.y, r), mulr(q.z, r), mulr(q.w, r)};
 }
 // quat_angle_axis (:230-240): angle = acos(clamp(2 w^2 - 1)), axis = xyz / max(|xyz|, 1e-9)
@@ -176,7 +225,7 @@ RTG_DEV Q qangle_axis_abs(Q q)
 {
     const float s = clamp_lohi(2.0f * (q.w * q.w) - 1.0f, -1.0f, 1.0f);
     const float n = clamp_lo(cr_sqrt((q.x * q.x + q.y * q.y) + q.z * q.z), 1e-9f);
-    const double r = rcp64(n);
+    const Rcp r = rcp64(n);
     return Q{cr_acos(s), mulr(q.x, r), mulr(q.y, r), mulr(q.z, r)};
 }
 
@@ -191,7 +240,7 @@ RTG_DEV Q qfrom_angle_axis(float angle, V axis)  // :122-143
     const float theta = angle / 2.0f;
     float n = cr_sqrt((axis.x * axis.x + axis.y * axis.y) + axis.z * axis.z);
     n = clamp_lo(n, 1e-9f);
-    const double r = rcp64(n);
+    const Rcp r = rcp64(n);
     const float ax = mulr(axis.x, r), ay = mulr(axis.y, r), az = mulr(axis.z, r);
     const SC t = cr_sincos((double)theta);
     const float s = t.s, c = t.c;
@@ -248,7 +297,7 @@ RTG_DEV Q qangle_axis(Q q)
     float angle = 2.0f * cr_acos(q.w);
     angle = normalize_angle(angle);
     const bool mask = fabsf(sin_theta) > 1e-5f;
-    const double r = rcp64(sin_theta);
+    const Rcp r = rcp64(sin_theta);
     return Q{mask ? angle : 0.0f, mask ? mulr(q.x, r) : 0.0f, mask ? mulr(q.y, r) : 0.0f,
              mask ? mulr(q.z, r) : 1.0f};
 }
@@ -272,7 +321,7 @@ RTG_DEV V cross3(V a, V b)                                                      
 RTG_DEV V vsub(V a, V b) { return V{a.x - b.x, a.y - b.y, a.z - b.z}; }
 RTG_DEV V vdiv(V a, float s)
 {
-    const double r = rcp64(s);
+    const Rcp r = rcp64(s);
     return V{mulr(a.x, r), mulr(a.y, r), mulr(a.z, r)};
 }
 RTG_DEV V vmul(V a, float s) { return V{s * a.x, s * a.y, s * a.z}; }

@@ -2,6 +2,8 @@
 golden vectors (the reference-noise-bounded statistics of test_oracle_golden.py).
 
 All calls go through the C ABI (rtg._lib via rtg.runtime / rtg.ops)."""
+import os
+
 import numpy as np
 import pytest
 import torch
@@ -230,6 +232,19 @@ def test_motion_prep_vs_oracle_and_reference(gpu):
     ogr, _ = orc.rebuild_vtrdyn(par, zl, y)
     np.testing.assert_array_equal(_np(gr), ogr)
     assert (ogr[:, 11] == np.array([0, 0, 0, 1], np.float32)).all()
+
+
+def test_fast_exact_sqrt_and_reciprocal_exhaustive(gpu):
+    """csrc/rtg_math.cuh's cr_sqrt (v_sqrt_f64 + Newton) and rcp64/mulr (v_rcp_f64 + Newton, subnormal
+    quotients via IEEE division) against IEEE f32 sqrt / division on the device: all 2^32 sqrt inputs,
+    2^32 random division pairs and all special-value pairs (tools/check_fastmath.hip)."""
+    import subprocess
+    import __graft_entry__ as ge
+    exe = ge.FASTMATH_BIN
+    if not os.path.exists(exe) or os.path.getmtime(exe) < os.path.getmtime(ge.FASTMATH_SRC):
+        ge.build_fastmath_check()
+    r = subprocess.run([exe], capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0 and r.stdout.count(" 0 mismatches") == 3, r.stdout + r.stderr
 
 
 # ----------------------------------------------------------------- primitives
