@@ -64,11 +64,7 @@ struct Emit {
     template <int LINK>
     RTG_DEV void link(Q q) const
     {
-#if defined(RTG_SKIP) && (RTG_SKIP & 1)
-        row[LINK - 1] = q.x + q.y;
-#else
         row[LINK - 1] = qexp_component(q, hu_dof_axis(LINK - 1));
-#endif
         if (lr) st4(lr + 4 * LINK, q);
     }
     template <int LINK>
@@ -199,101 +195,6 @@ RTG_DEV void solve_full_body_pos(const SolverConsts &C, const FbpIn &I, const Em
     }
 }
 
-#ifndef RTG_SOLVE_ORDER
-#define RTG_SOLVE_ORDER 0
-#endif
-#ifndef RTG_STAGE_BARRIER
-#define RTG_STAGE_BARRIER 0
-#endif
-#ifndef RTG_SKIP
-#define RTG_SKIP 0   // timing attribution only: 1 exp-maps, 2 Euler, 4 wrist fits, 8 arms, 16 gripper, 32 torso fit
-#endif
-#ifndef RTG_SOLVER_WAVES
-#define RTG_SOLVER_WAVES 1
-#endif
-RTG_DEV void stage_barrier()
-{
-#if RTG_STAGE_BARRIER
-    __builtin_amdgcn_sched_barrier(0);
-#endif
-}
-
-// One side (arm -> wrist fit -> wrist Euler -> gripper), loading its points
-// when the stage needs them, so only that side's values are live.
-template <bool PRECISE, int L0, int E0, int D0>
-RTG_DEV Q solve_side_pos(const SolverConsts &C, const float *__restrict__ b, int sh, int el, int wr,
-                         const float *__restrict__ H, const V (&Zw)[5], ArmZero zs, ArmZero ze, Q R10, const Emit &E)
-{
-    const V bel = ld3(b + 3 * el);
-#if RTG_SKIP & 8
-    const V u = vsub(bel, ld3(b + 3 * sh)), w = vsub(ld3(b + 3 * wr), bel);
-    const Q chain = qnormalize(Q{u.x, u.y, w.z, 1.0f});
-    E.link<L0>(chain); E.link<L0 + 1>(qconj(chain)); E.link<L0 + 2>(Q{chain.y, chain.x, chain.z, chain.w});
-    E.link<L0 + 3>(Q{chain.z, chain.y, chain.x, chain.w});
-#else
-    const Q chain = solve_arm<L0>(E, vsub(bel, ld3(b + 3 * sh)), vsub(ld3(b + 3 * wr), bel), zs, ze, R10);
-#endif
-    stage_barrier();
-    Q W;
-    {
-        const V h0 = ld3(H);
-        const V M[5] = {vsub(ld3(H + 6), h0), vsub(ld3(H + 18), h0), vsub(ld3(H + 30), h0), vsub(ld3(H + 42), h0),
-                        vsub(ld3(H + 51), h0)};
-#if RTG_SKIP & 4
-        W = qnormalize(Q{M[0].x + M[3].x, M[1].y + M[4].y, M[2].z, 1.0f});
-#else
-        W = cal_joint_quat<5>(Zw, M);
-#endif
-    }
-    stage_barrier();
-#if RTG_SKIP & 2
-    {
-        const Q lq = qmul_norm(qconj(qmul_norm(R10, chain)), W);
-        E.link<E0>(lq); E.link<E0 + 1>(qconj(lq)); E.link<E0 + 2>(Q{lq.y, lq.x, lq.z, lq.w});
-    }
-#else
-    emit_euler_xyz<E0>(E, qmul_norm(qconj(qmul_norm(R10, chain)), W));
-#endif
-    stage_barrier();
-    constexpr int tips[5] = {4, 8, 12, 16, 19};
-#if RTG_SKIP & 16
-    const float a = W.x + ld3(H + 12).x;
-#else
-    const float a = hand_x_mean(qconj(W), H, tips);
-#endif
-    if (PRECISE) {
-        const float sc = clamp_lohi(a / C.orig - 0.5f, 0.0f, 0.5f) / 0.5f;
-        E.row[D0] = sc * 0.044f; E.row[D0 + 1] = sc * -0.044f;
-    } else {
-        const bool closed = a / C.orig < 0.7f;
-        E.row[D0] = closed ? 0.0f : 0.044f; E.row[D0 + 1] = closed ? 0.0f : -0.044f;
-    }
-    stage_barrier();
-    return W;
-}
-
-template <bool PRECISE>
-RTG_DEV void solve_full_body_pos_sides(const SolverConsts &C, const float *__restrict__ b, const float *__restrict__ L,
-                                       const float *__restrict__ R, const Emit &E, float *__restrict__ body_rot)
-{
-    Q R10;
-    {
-        const V b10 = ld3(b + 30);
-        const V Mt[3] = {vsub(ld3(b + 51), b10), vsub(ld3(b + 39), b10), vsub(ld3(b + 33), b10)};
-#if RTG_SKIP & 32
-        R10 = qnormalize(Q{Mt[0].x, Mt[1].y, Mt[2].z, 1.0f});
-#else
-        R10 = cal_joint_quat<3>(C.Zt, Mt);
-#endif
-    }
-    stage_barrier();
-    const Q WL = solve_side_pos<PRECISE, 12, 16, 18>(C, b, 18, 19, 20, L, C.Zl, C.lsh, C.lel, R10, E);
-    const Q WR = solve_side_pos<PRECISE, 21, 25, 27>(C, b, 14, 15, 16, R, C.Zr, C.rsh, C.rel, R10, E);
-    if (body_rot) {
-        for (int j = 0; j < 59; ++j) st4(body_rot + 4 * j, j == 10 ? R10 : (j == 14 ? WL : (j == 39 ? WR : qident())));
-    }
-}
-
 // HuUpperBodyFromMocapRetarget.retarget_from_global_translation  retarget_solver.py:40-99
 RTG_DEV void solve_upper_body(const SolverConsts &C, const float *__restrict__ x, const Emit &E)
 {
@@ -363,7 +264,7 @@ constexpr int kSolverBlock = 256;
 constexpr int kDofStride = 31;   // LDS row pitch (dwords): odd -> conflict-free ds_write_b32
 
 template <int KIND, bool PRECISE>
-__global__ __launch_bounds__(kSolverBlock, RTG_SOLVER_WAVES) void k_retarget(SolverConsts C, const float *__restrict__ in0,
+__global__ __launch_bounds__(kSolverBlock) void k_retarget(SolverConsts C, const float *__restrict__ in0,
                                                            const float *__restrict__ in1,
                                                            const float *__restrict__ in2,
                                                            const float *__restrict__ in3, int64_t B,
@@ -375,10 +276,7 @@ __global__ __launch_bounds__(kSolverBlock, RTG_SOLVER_WAVES) void k_retarget(Sol
     if (f < B) {
         const Emit E{sdof + threadIdx.x * kDofStride, local_rot ? local_rot + f * 124 : nullptr};
         emit_fixed_links(E);
-        if (KIND == RTG_SOLVER_FULL_BODY_POS && RTG_SOLVE_ORDER == 1)
-            solve_full_body_pos_sides<PRECISE>(C, in0 + f * 63, in1 + f * 60, in2 + f * 60, E,
-                                               body_rot ? body_rot + f * 236 : nullptr);
-        else if (KIND == RTG_SOLVER_FULL_BODY_POS)
+        if (KIND == RTG_SOLVER_FULL_BODY_POS)
             solve_full_body_pos<PRECISE>(C, load_fbp(in0 + f * 63, in1 + f * 60, in2 + f * 60), E,
                                          body_rot ? body_rot + f * 236 : nullptr);
         else if (KIND == RTG_SOLVER_UPPER_BODY)
