@@ -133,12 +133,12 @@ def fk():
 
 def solvers():
     zp = np.load(os.path.join(G, "zero_pose.npz"))
-    B = 262144
+    B = int(os.environ.get("RTG_BENCH_B", "262144"))
     res = {}
     Tf = topo("vtrdyn_full")
     body, lh, rh, brot = ops.synth_full_body(Tf, B, seed=7, want_rot=True)
-    x = torch.from_numpy(synth.synth_upper_body_inputs(4096, 3)).cuda().repeat(64, 1, 1).contiguous()
-    g21 = torch.from_numpy(synth.synth_body21_pose(4096, 4)[1]).cuda().repeat(64, 1, 1).contiguous()
+    x = torch.from_numpy(synth.synth_upper_body_inputs(4096, 3)).cuda().repeat(B // 4096, 1, 1).contiguous()
+    g21 = torch.from_numpy(synth.synth_body21_pose(4096, 4)[1]).cuda().repeat(B // 4096, 1, 1).contiguous()
     cfg = {
         "full_body_pos": (Solver(_lib.SOLVER_FULL_BODY_POS, zp["vtrdyn_full_local_t"], zp["vtrdyn_full_global_t"],
                                  assets.parents("vtrdyn_full"), True), [body, lh, rh]),
