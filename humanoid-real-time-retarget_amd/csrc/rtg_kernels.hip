@@ -261,6 +261,9 @@ RTG_DEV void solve_body_rot(const SolverConsts &C, const float *__restrict__ g, 
 // solver kernel: per-frame body + coalesced DOF tile store
 // ----------------------------------------------------------------------------
 constexpr int kSolverBlock = 256;
+#ifndef RTG_FBP_SIDES
+#define RTG_FBP_SIDES 1
+#endif
 constexpr int kDofStride = 31;   // LDS row pitch (dwords): odd -> conflict-free ds_write_b32
 
 template <int KIND, bool PRECISE>
@@ -303,6 +306,91 @@ __global__ __launch_bounds__(kSolverBlock) void k_retarget(SolverConsts C, const
         *reinterpret_cast<float4 *>(dst + i) = make_float4(lds_at(i), lds_at(i + 1), lds_at(i + 2), lds_at(i + 3));
     }
     for (int i = (nvec << 2) + threadIdx.x; i < nvals; i += kSolverBlock) dst[i] = lds_at(i);
+}
+
+// ----------------------------------------------------------------------------
+// FULL_BODY_POS, two waves per frame tile.  After the torso fit the two sides are independent
+// (full_body_pos_retargeter.py:70-175), so waves 2k and 2k+1 of a block take the left and the right side of
+// the same 64 frames.  The side is wave-uniform: its constants stay scalar, the branch never diverges, and each
+// wave runs the torso fit plus half the frame program -- twice the waves in flight, about half the per-frame
+// latency, the same arithmetic per value (so the same bits as the fused body).
+// ----------------------------------------------------------------------------
+constexpr int kSideFrames = 128;   // frames per 256-thread block
+
+template <bool PRECISE, int SIDE>
+RTG_DEV void solve_fbp_side(const SolverConsts &C, const float *__restrict__ b, const float *__restrict__ H,
+                            Q R10, const Emit &E, float *__restrict__ brow)
+{
+    constexpr int L0 = SIDE ? 21 : 12, E0 = SIDE ? 25 : 16, D0 = SIDE ? 27 : 18, WROW = SIDE ? 39 : 14;
+    constexpr int SH = SIDE ? 14 : 18, EL = SIDE ? 15 : 19, WR = SIDE ? 16 : 20;
+    const V bel = ld3(b + 3 * EL);
+    const Q chain = solve_arm<L0>(E, vsub(bel, ld3(b + 3 * SH)), vsub(ld3(b + 3 * WR), bel), SIDE ? C.rsh : C.lsh,
+                                  SIDE ? C.rel : C.lel, R10);
+    Q W;
+    {
+        const V h0 = ld3(H);
+        const V M[5] = {vsub(ld3(H + 6), h0), vsub(ld3(H + 18), h0), vsub(ld3(H + 30), h0), vsub(ld3(H + 42), h0),
+                        vsub(ld3(H + 51), h0)};
+        W = cal_joint_quat<5>(SIDE ? C.Zr : C.Zl, M);
+    }
+    emit_euler_xyz<E0>(E, qmul_norm(qconj(qmul_norm(R10, chain)), W));
+    constexpr int tips[5] = {4, 8, 12, 16, 19};
+    const float a = hand_x_mean(qconj(W), H, tips);
+    if (PRECISE) {
+        const float sc = clamp_lohi(a / C.orig - 0.5f, 0.0f, 0.5f) / 0.5f;
+        E.row[D0] = sc * 0.044f;
+        E.row[D0 + 1] = sc * -0.044f;
+    } else {
+        const bool closed = a / C.orig < 0.7f;
+        E.row[D0] = closed ? 0.0f : 0.044f;
+        E.row[D0 + 1] = closed ? 0.0f : -0.044f;
+    }
+    if (brow) {   // body_global_rotation rows (:116, :172-173): the left wave also writes row 10 and the identities
+        st4(brow + 4 * WROW, W);
+        if (!SIDE)
+            for (int j = 0; j < 59; ++j)
+                if (j != 14 && j != 39) st4(brow + 4 * j, j == 10 ? R10 : qident());
+    }
+}
+
+template <bool PRECISE>
+__global__ __launch_bounds__(256) void k_fbp_sides(SolverConsts C, const float *__restrict__ body,
+                                                   const float *__restrict__ lh, const float *__restrict__ rh,
+                                                   int64_t B, float *__restrict__ dof, float *__restrict__ local_rot,
+                                                   float *__restrict__ body_rot)
+{
+    __shared__ float sdof[kSideFrames * kDofStride];
+    const int w = threadIdx.x >> 6, side = w & 1;
+    const int r = (w >> 1) * 64 + (threadIdx.x & 63);   // tile row
+    const int64_t f0 = (int64_t)blockIdx.x * kSideFrames, f = f0 + r;
+    if (f < B) {
+        const Emit E{sdof + r * kDofStride, local_rot ? local_rot + f * 124 : nullptr};
+        if (!side) emit_fixed_links(E);
+        const float *b = body + f * 63;
+        Q R10;
+        {
+            const V b10 = ld3(b + 30);
+            const V Mt[3] = {vsub(ld3(b + 51), b10), vsub(ld3(b + 39), b10), vsub(ld3(b + 33), b10)};
+            R10 = cal_joint_quat<3>(C.Zt, Mt);
+        }
+        float *brow = body_rot ? body_rot + f * 236 : nullptr;
+        if (side) solve_fbp_side<PRECISE, 1>(C, b, rh + f * 60, R10, E, brow);
+        else solve_fbp_side<PRECISE, 0>(C, b, lh + f * 60, R10, E, brow);
+    }
+    __syncthreads();
+    const int64_t nrows = (B - f0) < kSideFrames ? (B - f0) : kSideFrames;
+    const int nvals = (int)nrows * 30;
+    float *dst = dof + f0 * 30;
+    auto at = [&](int i) {
+        const int rr = i / 30;
+        return sdof[rr * kDofStride + (i - rr * 30)];
+    };
+    const int nvec = nvals >> 2;
+    for (int v = threadIdx.x; v < nvec; v += 256) {
+        const int i = v << 2;
+        *reinterpret_cast<float4 *>(dst + i) = make_float4(at(i), at(i + 1), at(i + 2), at(i + 3));
+    }
+    for (int i = (nvec << 2) + threadIdx.x; i < nvals; i += 256) dst[i] = at(i);
 }
 
 // ----------------------------------------------------------------------------
@@ -1201,6 +1289,15 @@ hipError_t launch_retarget(int kind, int precise, const SolverConsts &C, const f
     const dim3 grid(grid_for(B, kSolverBlock)), block(kSolverBlock);
     switch (kind) {
     case RTG_SOLVER_FULL_BODY_POS:
+#if RTG_FBP_SIDES
+        if (precise)
+            hipLaunchKernelGGL(k_fbp_sides<true>, dim3(grid_for(B, kSideFrames)), dim3(256), 0, s, C, in0, in1, in2,
+                               B, dof, local_rot, body_rot);
+        else
+            hipLaunchKernelGGL(k_fbp_sides<false>, dim3(grid_for(B, kSideFrames)), dim3(256), 0, s, C, in0, in1,
+                               in2, B, dof, local_rot, body_rot);
+        break;
+#endif
         if (precise)
             hipLaunchKernelGGL((k_retarget<RTG_SOLVER_FULL_BODY_POS, true>), grid, block, 0, s, C, in0, in1, in2,
                                in3, B, dof, local_rot, body_rot);
