@@ -86,14 +86,15 @@ def cpu_baseline(body, lh, rh, zl, zg, seconds):
 
 
 def pmc_traffic(B):
-    """HBM bytes per k_retarget launch from the committed rocprofv3 FETCH_SIZE + WRITE_SIZE passes
-    (profiles/pmc_traffic.json, written by tools/pmc_summary.py), when they were taken at this batch."""
+    """HBM bytes per k_solve_sides<FULL_BODY_POS> launch from the committed rocprofv3 FETCH_SIZE + WRITE_SIZE passes
+    (profiles/pmc_traffic.json, written by tools/pmc_summary.py), when they were taken at this batch.  rocprofv3's
+    grid counts threads: two per frame (one wave per side of each 64-frame tile)."""
     path = os.path.join(REPO, "profiles", "pmc_traffic.json")
     try:
-        rec = json.load(open(path)).get("rtg::k_retarget<0, true>")
+        rec = json.load(open(path)).get("rtg::k_solve_sides<0, true>")
     except (OSError, ValueError):
         return None
-    if not rec or rec.get("grid") != B:
+    if not rec or rec.get("grid") != 2 * B:
         return None
     return rec["traffic_bytes"]
 
@@ -244,7 +245,7 @@ def main():
                        "input_ring_sets": ring, "precise_gripper": True},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": pmc_traffic(B),
-                         "kernel": "k_retarget<FULL_BODY_POS>", "kernel_ms": kern_ms,
+                         "kernel": "k_solve_sides<FULL_BODY_POS>", "kernel_ms": kern_ms,
                          "bytes_per_frame": BYTES_PER_FRAME, "traffic_unit": "bytes/launch (rocprofv3 PMC)"},
         }
         if gather_ms is not None:

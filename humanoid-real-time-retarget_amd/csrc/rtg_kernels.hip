@@ -261,8 +261,8 @@ RTG_DEV void solve_body_rot(const SolverConsts &C, const float *__restrict__ g, 
 // solver kernel: per-frame body + coalesced DOF tile store
 // ----------------------------------------------------------------------------
 constexpr int kSolverBlock = 256;
-#ifndef RTG_FBP_SIDES
-#define RTG_FBP_SIDES 1
+#ifndef RTG_SOLVER_SIDES
+#define RTG_SOLVER_SIDES 1   // 0: always the fused one-lane-per-frame kernels (k_retarget), for comparison
 #endif
 constexpr int kDofStride = 31;   // LDS row pitch (dwords): odd -> conflict-free ds_write_b32
 
@@ -309,9 +309,10 @@ __global__ __launch_bounds__(kSolverBlock) void k_retarget(SolverConsts C, const
 }
 
 // ----------------------------------------------------------------------------
-// FULL_BODY_POS, two waves per frame tile.  After the torso fit the two sides are independent
-// (full_body_pos_retargeter.py:70-175), so waves 2k and 2k+1 of a block take the left and the right side of
-// the same 64 frames.  The side is wave-uniform: its constants stay scalar, the branch never diverges, and each
+// Every solver kind, two waves per frame tile.  After the torso fit (or, for the rotation solvers, from the
+// start) the two sides are independent (full_body_pos_retargeter.py:70-175, retarget_solver.py:72-99,
+// full_body_retargeter.py:60-177, body_retargeter.py:48-81), so waves 2k and 2k+1 of a block take the left
+// and the right side of the same 64 frames.  The side is wave-uniform: its constants stay scalar, the branch never diverges, and each
 // wave runs the torso fit plus half the frame program -- twice the waves in flight, about half the per-frame
 // latency, the same arithmetic per value (so the same bits as the fused body).
 // ----------------------------------------------------------------------------
@@ -353,11 +354,74 @@ RTG_DEV void solve_fbp_side(const SolverConsts &C, const float *__restrict__ b, 
     }
 }
 
-template <bool PRECISE>
-__global__ __launch_bounds__(256) void k_fbp_sides(SolverConsts C, const float *__restrict__ body,
-                                                   const float *__restrict__ lh, const float *__restrict__ rh,
-                                                   int64_t B, float *__restrict__ dof, float *__restrict__ local_rot,
-                                                   float *__restrict__ body_rot)
+// HuUpperBodyFromMocapRetarget (retarget_solver.py:40-99), one side: torso fit + one arm; wrists untouched
+template <int SIDE>
+RTG_DEV void solve_upper_side(const SolverConsts &C, const float *__restrict__ x, const Emit &E)
+{
+    auto pt = [&](int j) {   // coord_transform(dir=[-1,-1,1]) :41
+        const V v = ld3(x + 3 * j);
+        return V{v.x * -1.0f, v.y * -1.0f, v.z * 1.0f};
+    };
+    Q R10;
+    {
+        const V s10 = pt(10);
+        const V Mt[3] = {vsub(pt(17), s10), vsub(pt(13), s10), vsub(pt(11), s10)};
+        R10 = cal_joint_quat<3>(C.Zt, Mt);
+    }
+    constexpr int L0 = SIDE ? 21 : 12, E0 = SIDE ? 25 : 16, D0 = SIDE ? 27 : 18;
+    constexpr int SH = SIDE ? 14 : 18, EL = SIDE ? 15 : 19, WR = SIDE ? 16 : 20;
+    const V sel = pt(EL);
+    solve_arm<L0>(E, vsub(sel, pt(SH)), vsub(pt(WR), sel), SIDE ? C.rsh : C.lsh, SIDE ? C.rel : C.lel, R10);
+    E.identity<E0>(); E.identity<E0 + 1>(); E.identity<E0 + 2>();
+    E.row[D0] = 0.0f; E.row[D0 + 1] = 0.0f;
+}
+
+// VtrdynFullBodyRetargeter (full_body_retargeter.py:19-177), one side
+template <int SIDE>
+RTG_DEV void solve_full_body_rot_side(const SolverConsts &C, const float *__restrict__ q, const float *__restrict__ b,
+                                      const float *__restrict__ H, const Emit &E)
+{
+    constexpr int L0 = SIDE ? 21 : 12, E0 = SIDE ? 25 : 16, D0 = SIDE ? 27 : 18;
+    constexpr int SH = SIDE ? 14 : 18, EL = SIDE ? 15 : 19, WR = SIDE ? 16 : 20, PAR = SIDE ? 13 : 17;
+    const Q par = ld4(q + PAR * 4);
+    const V bel = ld3(b + 3 * EL);
+    const Q chain = solve_arm<L0>(E, vsub(bel, ld3(b + 3 * SH)), vsub(ld3(b + 3 * WR), bel), SIDE ? C.rsh : C.lsh,
+                                  SIDE ? C.rel : C.lel, par);
+    const Q w = ld4(q + WR * 4);
+    emit_euler_xyz<E0>(E, qmul_norm(qconj(qmul_norm(par, chain)), w));
+    constexpr int tips[5] = {3, 7, 11, 15, 19};   // :145-177 rotates by the wrist quaternion itself
+    const bool closed = hand_x_mean(w, H, tips) / C.orig < 0.7f;
+    E.row[D0] = closed ? 0.0f : 0.044f;
+    E.row[D0 + 1] = closed ? 0.0f : -0.044f;
+}
+
+// Mocap2HuBodyRetargeter (body_retargeter.py:34-81), one side
+template <int SIDE>
+RTG_DEV void solve_body_rot_side(const SolverConsts &C, const float *__restrict__ g, const Emit &E)
+{
+    auto local = [&](int j, int p) { return qmul_norm(qconj(ld4(g + 4 * p)), ld4(g + 4 * j)); };
+    constexpr int SH = SIDE ? 14 : 18, EL = SIDE ? 15 : 19, D0 = SIDE ? 27 : 18;
+    Q s3[3], e3[3];
+    quat_in_xyz_axis(local(SH, C.par[SIDE ? 1 : 0]), 1, 0, 2, false, s3);   // 'YXZ'
+    quat_in_xyz_axis(local(EL, C.par[SIDE ? 3 : 2]), 2, 1, 0, false, e3);   // 'ZYX'
+    if (SIDE) {
+        E.link<21>(s3[0]); E.link<22>(s3[1]); E.link<23>(qmul_norm(e3[0], s3[2]));
+        E.link<24>(e3[1]); E.link<25>(e3[2]);
+        E.identity<26>(); E.identity<27>();
+    } else {
+        E.link<12>(s3[0]); E.link<13>(s3[1]); E.link<14>(qmul_norm(e3[0], s3[2]));
+        E.link<15>(e3[1]); E.link<16>(e3[2]);
+        E.identity<17>(); E.identity<18>();
+    }
+    E.row[D0] = 0.0f; E.row[D0 + 1] = 0.0f;
+}
+
+template <int KIND, bool PRECISE>
+__global__ __launch_bounds__(256) void k_solve_sides(SolverConsts C, const float *__restrict__ in0,
+                                                     const float *__restrict__ in1, const float *__restrict__ in2,
+                                                     const float *__restrict__ in3, int64_t B,
+                                                     float *__restrict__ dof, float *__restrict__ local_rot,
+                                                     float *__restrict__ body_rot)
 {
     __shared__ float sdof[kSideFrames * kDofStride];
     const int w = threadIdx.x >> 6, side = w & 1;
@@ -366,16 +430,27 @@ __global__ __launch_bounds__(256) void k_fbp_sides(SolverConsts C, const float *
     if (f < B) {
         const Emit E{sdof + r * kDofStride, local_rot ? local_rot + f * 124 : nullptr};
         if (!side) emit_fixed_links(E);
-        const float *b = body + f * 63;
-        Q R10;
-        {
-            const V b10 = ld3(b + 30);
-            const V Mt[3] = {vsub(ld3(b + 51), b10), vsub(ld3(b + 39), b10), vsub(ld3(b + 33), b10)};
-            R10 = cal_joint_quat<3>(C.Zt, Mt);
+        if (KIND == RTG_SOLVER_FULL_BODY_POS) {
+            const float *b = in0 + f * 63;
+            Q R10;
+            {
+                const V b10 = ld3(b + 30);
+                const V Mt[3] = {vsub(ld3(b + 51), b10), vsub(ld3(b + 39), b10), vsub(ld3(b + 33), b10)};
+                R10 = cal_joint_quat<3>(C.Zt, Mt);
+            }
+            float *brow = body_rot ? body_rot + f * 236 : nullptr;
+            if (side) solve_fbp_side<PRECISE, 1>(C, b, in2 + f * 60, R10, E, brow);
+            else solve_fbp_side<PRECISE, 0>(C, b, in1 + f * 60, R10, E, brow);
+        } else if (KIND == RTG_SOLVER_UPPER_BODY) {
+            if (side) solve_upper_side<1>(C, in0 + f * 63, E);
+            else solve_upper_side<0>(C, in0 + f * 63, E);
+        } else if (KIND == RTG_SOLVER_FULL_BODY_ROT) {
+            if (side) solve_full_body_rot_side<1>(C, in0 + f * 84, in1 + f * 63, in3 + f * 60, E);
+            else solve_full_body_rot_side<0>(C, in0 + f * 84, in1 + f * 63, in2 + f * 60, E);
+        } else {
+            if (side) solve_body_rot_side<1>(C, in0 + f * 84, E);
+            else solve_body_rot_side<0>(C, in0 + f * 84, E);
         }
-        float *brow = body_rot ? body_rot + f * 236 : nullptr;
-        if (side) solve_fbp_side<PRECISE, 1>(C, b, rh + f * 60, R10, E, brow);
-        else solve_fbp_side<PRECISE, 0>(C, b, lh + f * 60, R10, E, brow);
     }
     __syncthreads();
     const int64_t nrows = (B - f0) < kSideFrames ? (B - f0) : kSideFrames;
@@ -1282,40 +1357,40 @@ hipError_t launch_solver_prep(SolverConsts *dev_consts, hipStream_t s)
     return hipGetLastError();
 }
 
+// Kernel choice.  The side-split kernel halves each wave's program and doubles the waves in flight.  Measured
+// against the fused body (same box, same session): 1.6-1.9x at 4096 frames for every kind; at
+// 262144 frames FULL_BODY_POS +4 %, FULL_BODY_ROT +15 %, UPPER_BODY and BODY_ROT within box-to-box noise
+// (-6..+2 % and -3..+10 % across two boxes).  So every kind runs split; RTG_SOLVER_SIDES=0 builds the fused
+// kernels for comparison.
+template <int KIND, bool PRECISE>
+static void launch_kind(const SolverConsts &C, const float *in0, const float *in1, const float *in2,
+                        const float *in3, int64_t B, float *dof, float *local_rot, float *body_rot, hipStream_t s)
+{
+    if (!RTG_SOLVER_SIDES)
+        hipLaunchKernelGGL((k_retarget<KIND, PRECISE>), dim3(grid_for(B, kSolverBlock)), dim3(kSolverBlock), 0, s,
+                           C, in0, in1, in2, in3, B, dof, local_rot, body_rot);
+    else
+        hipLaunchKernelGGL((k_solve_sides<KIND, PRECISE>), dim3(grid_for(B, kSideFrames)), dim3(256), 0, s, C,
+                           in0, in1, in2, in3, B, dof, local_rot, body_rot);
+}
+
 hipError_t launch_retarget(int kind, int precise, const SolverConsts &C, const float *in0, const float *in1,
                            const float *in2, const float *in3, int64_t B, float *dof, float *local_rot,
                            float *body_rot, hipStream_t s)
 {
-    const dim3 grid(grid_for(B, kSolverBlock)), block(kSolverBlock);
     switch (kind) {
     case RTG_SOLVER_FULL_BODY_POS:
-#if RTG_FBP_SIDES
-        if (precise)
-            hipLaunchKernelGGL(k_fbp_sides<true>, dim3(grid_for(B, kSideFrames)), dim3(256), 0, s, C, in0, in1, in2,
-                               B, dof, local_rot, body_rot);
-        else
-            hipLaunchKernelGGL(k_fbp_sides<false>, dim3(grid_for(B, kSideFrames)), dim3(256), 0, s, C, in0, in1,
-                               in2, B, dof, local_rot, body_rot);
-        break;
-#endif
-        if (precise)
-            hipLaunchKernelGGL((k_retarget<RTG_SOLVER_FULL_BODY_POS, true>), grid, block, 0, s, C, in0, in1, in2,
-                               in3, B, dof, local_rot, body_rot);
-        else
-            hipLaunchKernelGGL((k_retarget<RTG_SOLVER_FULL_BODY_POS, false>), grid, block, 0, s, C, in0, in1, in2,
-                               in3, B, dof, local_rot, body_rot);
+        if (precise) launch_kind<RTG_SOLVER_FULL_BODY_POS, true>(C, in0, in1, in2, in3, B, dof, local_rot, body_rot, s);
+        else launch_kind<RTG_SOLVER_FULL_BODY_POS, false>(C, in0, in1, in2, in3, B, dof, local_rot, body_rot, s);
         break;
     case RTG_SOLVER_UPPER_BODY:
-        hipLaunchKernelGGL((k_retarget<RTG_SOLVER_UPPER_BODY, false>), grid, block, 0, s, C, in0, in1, in2, in3, B,
-                           dof, local_rot, body_rot);
+        launch_kind<RTG_SOLVER_UPPER_BODY, false>(C, in0, in1, in2, in3, B, dof, local_rot, body_rot, s);
         break;
     case RTG_SOLVER_FULL_BODY_ROT:
-        hipLaunchKernelGGL((k_retarget<RTG_SOLVER_FULL_BODY_ROT, false>), grid, block, 0, s, C, in0, in1, in2, in3,
-                           B, dof, local_rot, body_rot);
+        launch_kind<RTG_SOLVER_FULL_BODY_ROT, false>(C, in0, in1, in2, in3, B, dof, local_rot, body_rot, s);
         break;
     default:
-        hipLaunchKernelGGL((k_retarget<RTG_SOLVER_BODY_ROT, false>), grid, block, 0, s, C, in0, in1, in2, in3, B,
-                           dof, local_rot, body_rot);
+        launch_kind<RTG_SOLVER_BODY_ROT, false>(C, in0, in1, in2, in3, B, dof, local_rot, body_rot, s);
         break;
     }
     return hipGetLastError();

@@ -361,6 +361,24 @@ def test_other_solvers(gpu, name, kind):
     _check_gold(name, _np(dof), d["dof"])
 
 
+@pytest.mark.parametrize("name,kind", [("full_body_pos_precise", 0), ("upper_body", 1), ("full_body_rot", 2),
+                                       ("body_rot", 3)])
+def test_solver_batch_invariance(gpu, name, kind):
+    """A frame's result does not depend on its batch or its position in the 128-frame tile: the golden frames
+    tiled to a ragged 131072+77-frame batch give the same bits, DOFs and local rotations, as the golden batch."""
+    d = golden(name)
+    ins = {0: ("body", "lh", "rh"), 1: ("x",), 2: ("body_rot", "body_pos", "lh", "rh"), 3: ("global_rot",)}[kind]
+    S = _solver(kind, True) if kind == 0 else _solver(kind)
+    small = _dev(*[d[k] for k in ins])
+    n = small[0].shape[0]
+    B = 131072 + 77
+    idx = torch.arange(B, device="cuda") % n
+    big = [t[idx].contiguous() for t in small]
+    dof_s, lr_s, _ = S.retarget(small, want_local_rot=True)
+    dof_b, lr_b, _ = S.retarget(big, want_local_rot=True)
+    assert torch.equal(dof_b, dof_s[idx]) and torch.equal(lr_b, lr_s[idx])
+
+
 def test_solver_full_size_properties(gpu):
     """BASELINE config 3 size (262144 frames, device-generated): finite, zero
     DOFs where the reference never writes, gripper range, and a 2048-frame
