@@ -166,9 +166,17 @@ def parity_vs_reference():
     dof, _, _ = S.retarget([torch.from_numpy(np.ascontiguousarray(g[k])).cuda() for k in ("body", "lh", "rh")])
     e = np.abs(dof.cpu().numpy().astype(np.float64) - g["dof"])
     fm = e.max(1)
-    return {"frames": int(len(fm)), "max_abs_err": float(e.max()), "p99_frame_err": float(np.quantile(fm, 0.99)),
-            "median_frame_err": float(np.median(fm)), "frac_frames_le_1e-5": float(np.mean(fm <= 1e-5)),
-            "unit": "rad (DOFs 18,19,27,28: m)"}
+    out = {"frames": int(len(fm)), "max_abs_err": float(e.max()), "p99_frame_err": float(np.quantile(fm, 0.99)),
+           "median_frame_err": float(np.median(fm)), "frac_frames_le_1e-5": float(np.mean(fm <= 1e-5)),
+           "unit": "rad (DOFs 18,19,27,28: m)"}
+    # the reference against itself: same inputs, MKL forced to another ISA (tools/ref_isa_spread.py)
+    sp = np.load(os.path.join(REPO, "tests", "golden", "ref_isa_spread.npz"))
+    for isa in sp["isas"]:
+        r = np.abs(sp[f"full_body_pos_precise_{isa}"].astype(np.float64) - g["dof"]).max(1)
+        out[f"reference_self_spread_mkl_{isa}"] = {"max_abs_err": float(r.max()),
+                                                   "p99_frame_err": float(np.quantile(r, 0.99)),
+                                                   "frac_frames_le_1e-5": float(np.mean(r <= 1e-5))}
+    return out
 
 
 def main():

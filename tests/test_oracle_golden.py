@@ -147,6 +147,23 @@ def test_solver_dofs_vs_reference(name):
     assert s["max"] <= mx and s["p99_frame"] <= p99 and s["frac_frames_gt_1e5"] <= frac, s
 
 
+@pytest.mark.parametrize("name", ["full_body_pos_precise", "full_body_pos_binary", "upper_body"])
+def test_solver_residual_within_reference_cross_isa_spread(name):
+    """The reference is not bit-reproducible across CPUs: MKL sgesdd picks its
+    kernels by instruction set.  tests/golden/ref_isa_spread.npz holds the
+    reference's own DOFs on the same inputs with MKL forced to AVX2 and to
+    SSE4_2 (tools/ref_isa_spread.py); the goldens are the AVX-512 run.  The
+    oracle's residual against the goldens must sit within 1.3x of the
+    reference-vs-reference spread (max, p99 per-frame max, frames > 1e-5)."""
+    dof, d = _run(name)
+    ours = frame_stats(dof, d["dof"])
+    spread = golden("ref_isa_spread")
+    floor = {k: max(frame_stats(spread[f"{name}_{isa}"], d["dof"])[k] for isa in spread["isas"])
+             for k in ("max", "p99_frame", "frac_frames_gt_1e5")}
+    for k, v in floor.items():
+        assert ours[k] <= 1.3 * v, (k, ours, floor)
+
+
 def test_full_body_pos_with_reference_kabsch_injected():
     """With the reference's own Kabsch quaternions injected, only the MKL VML
     ulps remain: >= 98% of frames within 1e-5 rad."""
