@@ -38,6 +38,7 @@ struct rtg_solver_s {
     int kind = 0;
     int precise = 0;
     SolverConsts consts{};
+    uint32_t *d_ang_tab = nullptr;   // exp-map angle table (consts.ang_tab), device of creation
 };
 
 namespace {
@@ -399,17 +400,32 @@ int rtg_solver_create(int kind, const float *zl, const float *zg, const int32_t 
     if (rc == RTG_OK) rc = hip_check(hipMemcpy(&C, d, sizeof C, hipMemcpyDeviceToHost), "hipMemcpy(consts)");
     (void)hipFree(d);
     if (rc != RTG_OK) return rc;
+    // exp-map angle table: built once per solver on the current device (4 MiB), read by every launch
+    uint32_t *tab = nullptr;
+    RTG_TRY(hipMalloc(&tab, kAngTabWords * sizeof(uint32_t)), "hipMalloc(exp-map angle table)");
+    rc = hip_check(launch_build_ang_tab(tab, nullptr), "k_build_ang_tab");
+    if (rc == RTG_OK) rc = hip_check(hipStreamSynchronize(nullptr), "k_build_ang_tab");
+    if (rc != RTG_OK) {
+        (void)hipFree(tab);
+        return rc;
+    }
+    C.ang_tab = tab;
     rtg_solver_s *s = new (std::nothrow) rtg_solver_s();
-    if (!s) return fail(RTG_ERR_OUT_OF_MEMORY, "rtg_solver_create: host allocation failed");
+    if (!s) {
+        (void)hipFree(tab);
+        return fail(RTG_ERR_OUT_OF_MEMORY, "rtg_solver_create: host allocation failed");
+    }
     s->kind = kind;
     s->precise = precise_gripper ? 1 : 0;
     s->consts = C;
+    s->d_ang_tab = tab;
     *out = s;
     return RTG_OK;
 }
 
 int rtg_solver_destroy(rtg_solver_t s)
 {
+    if (s) (void)hipFree(s->d_ang_tab);
     delete s;
     return RTG_OK;
 }

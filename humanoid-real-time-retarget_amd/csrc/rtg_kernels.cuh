@@ -36,6 +36,7 @@ struct SolverConsts {
     float grip_d[5];  // zero-pose x distances of the 5 finger tips to the wrist
     float orig;       // their mean (gripper denominator), filled by k_solver_prep
     int32_t par[4];   // BODY_ROT: parents of joints 18, 14, 19, 15
+    const uint32_t *ang_tab;   // exp-map angle table (kAngTabWords words, device), owned by the solver handle
 };
 
 // Joint-angle forward model (HuForwardModel): per-DOF axis and optional limits, device memory.
@@ -60,6 +61,7 @@ struct FkMultiArgs {
 };
 
 hipError_t launch_solver_prep(SolverConsts *dev_consts, hipStream_t s);
+hipError_t launch_build_ang_tab(uint32_t *tab, hipStream_t s);   // kAngTabWords words
 hipError_t launch_retarget(int kind, int precise, const SolverConsts &C, const float *in0, const float *in1,
                            const float *in2, const float *in3, int64_t B, float *dof, float *local_rot,
                            float *body_rot, hipStream_t s);

@@ -61,10 +61,11 @@ __global__ void k_solver_prep(SolverConsts *c)
 struct Emit {
     float *row;                  // LDS row of this frame (30 DOFs)
     float *__restrict__ lr;      // local_rot row (31 x 4) or nullptr
+    const uint32_t *__restrict__ ang;   // exp-map angle table (SolverConsts::ang_tab)
     template <int LINK>
     RTG_DEV void link(Q q) const
     {
-        row[LINK - 1] = qexp_component(q, hu_dof_axis(LINK - 1));
+        row[LINK - 1] = qexp_component_tab(q, hu_dof_axis(LINK - 1), ang);
         if (lr) st4(lr + 4 * LINK, q);
     }
     template <int LINK>
@@ -277,7 +278,7 @@ __global__ __launch_bounds__(kSolverBlock) void k_retarget(SolverConsts C, const
     __shared__ float sdof[kSolverBlock * kDofStride];
     const int64_t f = (int64_t)blockIdx.x * kSolverBlock + threadIdx.x;
     if (f < B) {
-        const Emit E{sdof + threadIdx.x * kDofStride, local_rot ? local_rot + f * 124 : nullptr};
+        const Emit E{sdof + threadIdx.x * kDofStride, local_rot ? local_rot + f * 124 : nullptr, C.ang_tab};
         emit_fixed_links(E);
         if (KIND == RTG_SOLVER_FULL_BODY_POS)
             solve_full_body_pos<PRECISE>(C, load_fbp(in0 + f * 63, in1 + f * 60, in2 + f * 60), E,
@@ -428,7 +429,7 @@ __global__ __launch_bounds__(256) void k_solve_sides(SolverConsts C, const float
     const int r = (w >> 1) * 64 + (threadIdx.x & 63);   // tile row
     const int64_t f0 = (int64_t)blockIdx.x * kSideFrames, f = f0 + r;
     if (f < B) {
-        const Emit E{sdof + r * kDofStride, local_rot ? local_rot + f * 124 : nullptr};
+        const Emit E{sdof + r * kDofStride, local_rot ? local_rot + f * 124 : nullptr, C.ang_tab};
         if (!side) emit_fixed_links(E);
         if (KIND == RTG_SOLVER_FULL_BODY_POS) {
             const float *b = in0 + f * 63;
@@ -1354,6 +1355,24 @@ static inline unsigned grid_for(int64_t n, int block) { return (unsigned)((n + b
 hipError_t launch_solver_prep(SolverConsts *dev_consts, hipStream_t s)
 {
     hipLaunchKernelGGL(k_solver_prep, dim3(1), dim3(64), 0, s, dev_consts);
+    return hipGetLastError();
+}
+
+// exp-map angle table (rtg_math.cuh, qexp_component_tab): one word of 16 two-bit codes per thread, each code
+// from the exact path it replaces.
+__global__ __launch_bounds__(256) void k_build_ang_tab(uint32_t *tab)
+{
+    const uint32_t wd = blockIdx.x * 256u + threadIdx.x;
+    if (wd >= kAngTabWords) return;
+    uint32_t word = 0;
+    for (uint32_t e = 0; e < 16u; ++e)
+        word |= ang_tab_code(__uint_as_float(kAngTabLo + wd * 16u + e)) << (2u * e);
+    tab[wd] = word;
+}
+
+hipError_t launch_build_ang_tab(uint32_t *tab, hipStream_t s)
+{
+    hipLaunchKernelGGL(k_build_ang_tab, dim3(kAngTabWords / 256u), dim3(256), 0, s, tab);
     return hipGetLastError();
 }
 

@@ -307,6 +307,42 @@ RTG_DEV float qexp_component(Q q, int k)
     return k == 0 ? e.x : (k == 1 ? e.y : e.z);
 }
 
+// ------------------------------------------------ exp-map angle table
+// The angle of quat_to_angle_axis (:595-597) is normalize_angle(2 acos w) = atan2f(RN sin A, RN cos A) with
+// A = 2 RN(acos w): A moved by at most 2 ulps (glibc atan2f is not correctly rounded, so the move has no closed
+// form).  For w in [0.25, 1) -- joint angles below 151 degrees -- the move is tabulated: 2 bits per f32 w
+// (0: A, 1: A + 1 ulp, 2: A - 1 ulp, 3: not tabulated), 2^24 entries in 4 MiB, built on the device from the exact
+// path itself (ang_tab_code, k_build_ang_tab).  qexp_component_tab then skips sincos + atan2f (200 of the 330
+// instructions of an exp-map); w outside the table or a code-3 entry (260 of the 2^24) takes the exact path.
+// tools/check_fastmath.hip checks qexp_component_tab == qexp_component for every f32 w.
+constexpr uint32_t kAngTabLo = 0x3e800000u;                     // bits of 0.25f
+constexpr uint32_t kAngTabEntries = 0x3f800000u - kAngTabLo;    // up to 1.0f (exclusive): 2^24
+constexpr uint32_t kAngTabWords = kAngTabEntries / 16u;         // 16 two-bit codes per word
+RTG_DEV uint32_t ang_tab_code(float w)
+{
+    const float A = 2.0f * cr_acos(w);
+    const float R = normalize_angle(A);
+    const int32_t d = (int32_t)__float_as_uint(R) - (int32_t)__float_as_uint(A);
+    if (!(R > 0.0f) || !(A > 0.0f)) return 3u;
+    return d == 0 ? 0u : (d == 1 ? 1u : (d == -1 ? 2u : 3u));
+}
+RTG_DEV float qexp_component_tab(Q q, int k, const uint32_t *__restrict__ tab)
+{
+    const uint32_t i = __float_as_uint(q.w) - kAngTabLo;
+    const bool in = i < kAngTabEntries;
+    const uint32_t word = tab[in ? (i >> 4) : 0u];   // issued first: the acos below hides its latency
+    const float sin_theta = cr_sqrt(1.0f - q.w * q.w);
+    const float A = 2.0f * cr_acos(q.w);
+    const bool mask = fabsf(sin_theta) > 1e-5f;
+    const uint32_t code = in ? (word >> ((i & 15u) * 2u)) & 3u : 3u;
+    float angle = __uint_as_float(__float_as_uint(A) + (code == 1u ? 1u : (code == 2u ? 0xffffffffu : 0u)));
+    if (__builtin_expect(mask && code == 3u, 0)) angle = normalize_angle(A);
+    const float a = mask ? angle : 0.0f;
+    const float qk = k == 0 ? q.x : (k == 1 ? q.y : q.z);
+    const float ak = mask ? qk / sin_theta : (k == 2 ? 1.0f : 0.0f);
+    return a * ak;
+}
+
 // ------------------------------------------------ vectors (transform3d.py)
 RTG_DEV float dot3(V a, V b) { return (a.x * b.x + a.y * b.y) + a.z * b.z; }          // torch.dot
 RTG_DEV float lnorm3(V a)                                                              // torch.linalg.norm

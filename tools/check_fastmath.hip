@@ -1,7 +1,8 @@
 // check_fastmath.hip -- exhaustive device proof for the two "fast exact" helpers of csrc/rtg_math.cuh:
 //  [1] cr_sqrt (v_sqrt_f64 + Newton) == IEEE f32 sqrt for EVERY f32 bit pattern (NaN == NaN);
 //  [2] (float)((double)a * rcp64(n)) == IEEE f32 a / n for 2^32 hashed (a, n) pairs (full bit patterns,
-//      clustered exponents, n near 1) plus every pair of 64 special values (0, denormals, inf, NaN, extremes).
+//      clustered exponents, n near 1) plus every pair of 64 special values (0, denormals, inf, NaN, extremes);
+//  [3] qexp_component_tab (exp-map angle table) == qexp_component for every f32 w bit pattern.
 // Built with the library's flags by __graft_entry__.build(); run by tests/test_gpu_parity.py.
 #include <hip/hip_runtime.h>
 #include <cstdio>
@@ -70,25 +71,53 @@ __global__ void k_div_special(unsigned long long *bad)
     if (!same(mulr(a, rcp64(n)), a / n)) atomicAdd(bad + 2, 1ull);
 }
 
+// [3] qexp_component_tab (exp-map angle table) == qexp_component for every f32 w (all 2^32 bit patterns; x, y, z
+// hashed, the component cycling through 0..2).  The table is built here exactly as rtg_solver_create builds it.
+__global__ void k_build_tab(uint32_t *tab)
+{
+    const uint32_t wd = blockIdx.x * 256u + threadIdx.x;
+    if (wd >= kAngTabWords) return;
+    uint32_t word = 0;
+    for (uint32_t e = 0; e < 16u; ++e) word |= ang_tab_code(__uint_as_float(kAngTabLo + wd * 16u + e)) << (2u * e);
+    tab[wd] = word;
+}
+
+__global__ void k_exptab(uint64_t base, const uint32_t *tab, unsigned long long *bad)
+{
+    const uint64_t i = base + (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const uint64_t h = mix(i);
+    const float x = (float)(int32_t)(h & 0xffff) * 0x1p-15f, y = (float)(int32_t)((h >> 16) & 0xffff) * 0x1p-15f,
+                z = (float)(int32_t)((h >> 32) & 0xffff) * 0x1p-15f;
+    const Q q{x - 1.0f, y - 1.0f, z - 1.0f, __uint_as_float((uint32_t)i)};
+    const int k = (int)(i % 3);
+    if (!same(qexp_component_tab(q, k, tab), qexp_component(q, k))) atomicAdd(bad + 3, 1ull);
+}
+
 int main()
 {
     unsigned long long *bad;
-    (void)hipMalloc(&bad, 3 * sizeof(unsigned long long));
-    (void)hipMemset(bad, 0, 3 * sizeof(unsigned long long));
+    (void)hipMalloc(&bad, 4 * sizeof(unsigned long long));
+    (void)hipMemset(bad, 0, 4 * sizeof(unsigned long long));
+    uint32_t *tab;
+    (void)hipMalloc(&tab, kAngTabWords * sizeof(uint32_t));
+    hipLaunchKernelGGL(k_build_tab, dim3(kAngTabWords / 256u), dim3(256), 0, 0, tab);
     const uint64_t chunk = 1ull << 30;
     for (uint64_t base = 0; base < (1ull << 32); base += chunk) {
         hipLaunchKernelGGL(k_sqrt, dim3((unsigned)(chunk / 256)), dim3(256), 0, 0, base, bad);
         hipLaunchKernelGGL(k_div, dim3((unsigned)(chunk / 256)), dim3(256), 0, 0, base, bad);
+        hipLaunchKernelGGL(k_exptab, dim3((unsigned)(chunk / 256)), dim3(256), 0, 0, base, tab, bad);
     }
     hipLaunchKernelGGL(k_div_special, dim3(64), dim3(64), 0, 0, bad);
-    unsigned long long h[3] = {0, 0, 0};
+    unsigned long long h[4] = {0, 0, 0, 0};
     (void)hipMemcpy(h, bad, sizeof h, hipMemcpyDeviceToHost);
     printf("[1] cr_sqrt: 4294967296 inputs, %llu mismatches\n", h[0]);
     printf("[2] rcp64 division: 4294967296 pairs, %llu mismatches\n", h[1]);
     printf("[2b] rcp64 division, special values: 4096 pairs, %llu mismatches\n", h[2]);
+    printf("[3] exp-map angle table: 4294967296 w bit patterns, %llu mismatches\n", h[3]);
     uint32_t f[16];
     (void)hipMemcpyFromSymbol(f, HIP_SYMBOL(g_first), sizeof f);
     for (unsigned k = 0; k < (h[1] < 4 ? h[1] : 4); ++k)
         printf("  a=%08x n=%08x fast=%08x ieee=%08x\n", f[4 * k], f[4 * k + 1], f[4 * k + 2], f[4 * k + 3]);
-    return (h[0] || h[1] || h[2]) ? 1 : 0;
+    (void)hipFree(tab);
+    return (h[0] || h[1] || h[2] || h[3]) ? 1 : 0;
 }
