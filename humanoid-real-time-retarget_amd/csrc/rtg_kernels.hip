@@ -319,22 +319,43 @@ __global__ __launch_bounds__(kSolverBlock) void k_retarget(SolverConsts C, const
 // ----------------------------------------------------------------------------
 constexpr int kSideFrames = 128;   // frames per 256-thread block
 
+// torso fit R10 (full_body_pos_retargeter.py:69-70 / retarget_solver.py:49-50)
+RTG_DEV Q fbp_torso(const SolverConsts &C, const float *__restrict__ b)
+{
+    const V b10 = ld3(b + 30);
+    const V Mt[3] = {vsub(ld3(b + 51), b10), vsub(ld3(b + 39), b10), vsub(ld3(b + 33), b10)};
+    return cal_joint_quat<3>(C.Zt, Mt);
+}
+RTG_DEV Q upper_pt_sign(V v) { return Q{v.x * -1.0f, v.y * -1.0f, v.z * 1.0f, 0.0f}; }   // coord_transform :41
+RTG_DEV Q upper_torso(const SolverConsts &C, const float *__restrict__ x)
+{
+    auto pt = [&](int j) {
+        const Q q = upper_pt_sign(ld3(x + 3 * j));
+        return V{q.x, q.y, q.z};
+    };
+    const V s10 = pt(10);
+    const V Mt[3] = {vsub(pt(17), s10), vsub(pt(13), s10), vsub(pt(11), s10)};
+    return cal_joint_quat<3>(C.Zt, Mt);
+}
+// wrist fit W (full_body_pos_retargeter.py:137-140 left, :160-163 right)
+template <int SIDE>
+RTG_DEV Q fbp_wrist_fit(const SolverConsts &C, const float *__restrict__ H)
+{
+    const V h0 = ld3(H);
+    const V M[5] = {vsub(ld3(H + 6), h0), vsub(ld3(H + 18), h0), vsub(ld3(H + 30), h0), vsub(ld3(H + 42), h0),
+                    vsub(ld3(H + 51), h0)};
+    return cal_joint_quat<5>(SIDE ? C.Zr : C.Zl, M);
+}
+
 template <bool PRECISE, int SIDE>
 RTG_DEV void solve_fbp_side(const SolverConsts &C, const float *__restrict__ b, const float *__restrict__ H,
-                            Q R10, const Emit &E, float *__restrict__ brow)
+                            Q R10, Q W, const Emit &E, float *__restrict__ brow)
 {
     constexpr int L0 = SIDE ? 21 : 12, E0 = SIDE ? 25 : 16, D0 = SIDE ? 27 : 18, WROW = SIDE ? 39 : 14;
     constexpr int SH = SIDE ? 14 : 18, EL = SIDE ? 15 : 19, WR = SIDE ? 16 : 20;
     const V bel = ld3(b + 3 * EL);
     const Q chain = solve_arm<L0>(E, vsub(bel, ld3(b + 3 * SH)), vsub(ld3(b + 3 * WR), bel), SIDE ? C.rsh : C.lsh,
                                   SIDE ? C.rel : C.lel, R10);
-    Q W;
-    {
-        const V h0 = ld3(H);
-        const V M[5] = {vsub(ld3(H + 6), h0), vsub(ld3(H + 18), h0), vsub(ld3(H + 30), h0), vsub(ld3(H + 42), h0),
-                        vsub(ld3(H + 51), h0)};
-        W = cal_joint_quat<5>(SIDE ? C.Zr : C.Zl, M);
-    }
     emit_euler_xyz<E0>(E, qmul_norm(qconj(qmul_norm(R10, chain)), W));
     constexpr int tips[5] = {4, 8, 12, 16, 19};
     const float a = hand_x_mean(qconj(W), H, tips);
@@ -355,20 +376,14 @@ RTG_DEV void solve_fbp_side(const SolverConsts &C, const float *__restrict__ b, 
     }
 }
 
-// HuUpperBodyFromMocapRetarget (retarget_solver.py:40-99), one side: torso fit + one arm; wrists untouched
+// HuUpperBodyFromMocapRetarget (retarget_solver.py:40-99), one side: one arm given the torso fit; wrists untouched
 template <int SIDE>
-RTG_DEV void solve_upper_side(const SolverConsts &C, const float *__restrict__ x, const Emit &E)
+RTG_DEV void solve_upper_side(const SolverConsts &C, const float *__restrict__ x, Q R10, const Emit &E)
 {
     auto pt = [&](int j) {   // coord_transform(dir=[-1,-1,1]) :41
-        const V v = ld3(x + 3 * j);
-        return V{v.x * -1.0f, v.y * -1.0f, v.z * 1.0f};
+        const Q q = upper_pt_sign(ld3(x + 3 * j));
+        return V{q.x, q.y, q.z};
     };
-    Q R10;
-    {
-        const V s10 = pt(10);
-        const V Mt[3] = {vsub(pt(17), s10), vsub(pt(13), s10), vsub(pt(11), s10)};
-        R10 = cal_joint_quat<3>(C.Zt, Mt);
-    }
     constexpr int L0 = SIDE ? 21 : 12, E0 = SIDE ? 25 : 16, D0 = SIDE ? 27 : 18;
     constexpr int SH = SIDE ? 14 : 18, EL = SIDE ? 15 : 19, WR = SIDE ? 16 : 20;
     const V sel = pt(EL);
@@ -425,27 +440,45 @@ __global__ __launch_bounds__(256) void k_solve_sides(SolverConsts C, const float
                                                      float *__restrict__ body_rot)
 {
     __shared__ float sdof[kSideFrames * kDofStride];
+    __shared__ float4 storso[kSideFrames];   // the tile's torso fit, handed from the left wave to the right one
     const int w = threadIdx.x >> 6, side = w & 1;
     const int r = (w >> 1) * 64 + (threadIdx.x & 63);   // tile row
     const int64_t f0 = (int64_t)blockIdx.x * kSideFrames, f = f0 + r;
-    if (f < B) {
-        const Emit E{sdof + r * kDofStride, local_rot ? local_rot + f * 124 : nullptr, C.ang_tab};
-        if (!side) emit_fixed_links(E);
-        if (KIND == RTG_SOLVER_FULL_BODY_POS) {
-            const float *b = in0 + f * 63;
-            Q R10;
-            {
-                const V b10 = ld3(b + 30);
-                const V Mt[3] = {vsub(ld3(b + 51), b10), vsub(ld3(b + 39), b10), vsub(ld3(b + 33), b10)};
-                R10 = cal_joint_quat<3>(C.Zt, Mt);
+    const bool live = f < B;
+    const Emit E{sdof + r * kDofStride, live && local_rot ? local_rot + f * 124 : nullptr, C.ang_tab};
+    if (KIND == RTG_SOLVER_FULL_BODY_POS || KIND == RTG_SOLVER_UPPER_BODY) {
+        // The torso fit is shared by both sides: the left wave fits it while the right wave fits its own hand
+        // (FULL_BODY_POS; nothing to overlap for UPPER_BODY), then one block barrier hands R10 over LDS.
+        const float *b = in0 + f * 63;   // body (FULL_BODY_POS) / mocap points (UPPER_BODY), both (B, 21, 3)
+        Q R10 = qident(), W = qident();
+        if (live) {
+            if (!side) {
+                R10 = KIND == RTG_SOLVER_FULL_BODY_POS ? fbp_torso(C, b) : upper_torso(C, b);
+                storso[r] = make_float4(R10.x, R10.y, R10.z, R10.w);
+            } else if (KIND == RTG_SOLVER_FULL_BODY_POS) {
+                W = fbp_wrist_fit<1>(C, in2 + f * 60);
             }
-            float *brow = body_rot ? body_rot + f * 236 : nullptr;
-            if (side) solve_fbp_side<PRECISE, 1>(C, b, in2 + f * 60, R10, E, brow);
-            else solve_fbp_side<PRECISE, 0>(C, b, in1 + f * 60, R10, E, brow);
-        } else if (KIND == RTG_SOLVER_UPPER_BODY) {
-            if (side) solve_upper_side<1>(C, in0 + f * 63, E);
-            else solve_upper_side<0>(C, in0 + f * 63, E);
-        } else if (KIND == RTG_SOLVER_FULL_BODY_ROT) {
+        }
+        __syncthreads();
+        if (live) {
+            if (side) {
+                const float4 t = storso[r];
+                R10 = Q{t.x, t.y, t.z, t.w};
+            } else {
+                emit_fixed_links(E);
+            }
+            if (KIND == RTG_SOLVER_FULL_BODY_POS) {
+                float *brow = body_rot ? body_rot + f * 236 : nullptr;
+                if (side) solve_fbp_side<PRECISE, 1>(C, b, in2 + f * 60, R10, W, E, brow);
+                else solve_fbp_side<PRECISE, 0>(C, b, in1 + f * 60, R10, fbp_wrist_fit<0>(C, in1 + f * 60), E, brow);
+            } else {
+                if (side) solve_upper_side<1>(C, b, R10, E);
+                else solve_upper_side<0>(C, b, R10, E);
+            }
+        }
+    } else if (live) {
+        if (!side) emit_fixed_links(E);
+        if (KIND == RTG_SOLVER_FULL_BODY_ROT) {
             if (side) solve_full_body_rot_side<1>(C, in0 + f * 84, in1 + f * 63, in3 + f * 60, E);
             else solve_full_body_rot_side<0>(C, in0 + f * 84, in1 + f * 63, in2 + f * 60, E);
         } else {

@@ -246,6 +246,14 @@ RTG_DEV Q qfrom_angle_axis(float angle, V axis)  // :122-143
     const float s = t.s, c = t.c;
     return qnormalize(Q{ax * s, ay * s, az * s, c});
 }
+// quat_from_angle_axis about an exact unit axis (ex / ey / ez): the axis normalisation is the identity
+// (sqrt(1) = 1, +0 and 1 times RN(1/1) stay +0 and 1), so it is skipped -- the same bits.
+RTG_DEV Q qfrom_angle_unit_axis(float angle, V axis)
+{
+    const float theta = angle / 2.0f;
+    const SC t = cr_sincos((double)theta);
+    return qnormalize(Q{axis.x * t.s, axis.y * t.s, axis.z * t.s, t.c});
+}
 
 RTG_DEV Q qfrom_rotmat(const float m[9])  // :146-193 (the four overlapping branches, in order)
 {
@@ -375,6 +383,14 @@ RTG_DEV float radians_between(V v1, V v2, V n)  // :77-100
     const V nrm = vdiv(n, lnorm3(n));
     const float c = clamp_lohi(dot3(v1, v2), -1.0f, 1.0f);
     return cr_acos(c) * tsign(dot3(nrm, cross3(v1, v2)));
+}
+// radians_between with v1 and n exact unit axes (the arm maps' ex / ey / ez): their normalisation is the
+// identity (lnorm3 = sqrt(1) = 1, x * RN(1/1) = x), so only v2 is normalised -- the same bits, 2/3 fewer divides.
+RTG_DEV float radians_between_axes(V v1, V v2, V n)
+{
+    v2 = vdiv(v2, lnorm3(v2));
+    const float c = clamp_lohi(dot3(v1, v2), -1.0f, 1.0f);
+    return cr_acos(c) * tsign(dot3(n, cross3(v1, v2)));
 }
 
 // ------------------------------------------------ Kabsch (float64)
@@ -534,7 +550,9 @@ RTG_DEV void kabsch_rot(const float A[9], float R[9])
     for (; it < 50; ++it) {
         const double P = ((lam * lam + c2) * lam + c1) * lam + c0;
         const double dP = (4.0 * lam * lam + 2.0 * c2) * lam + c1;
-        const double d = P / dP;
+        // the step only has to be near P/dP: v_rcp_f64's estimate keeps Newton's convergence (each step's error
+        // shrinks by the estimate's ~2^-26 on top of the quadratic term) at a tenth of the IEEE divide's cost
+        const double d = P * __builtin_amdgcn_rcp(dP);
         lam -= d;
         if (fabs(d) <= 1e-13 * fabs(lam)) break;
     }
@@ -547,7 +565,7 @@ RTG_DEV void kabsch_rot(const float A[9], float R[9])
     if (fabs(adj[5]) > best) { best = fabs(adj[5]); k = 1; }
     if (fabs(adj[10]) > best) { best = fabs(adj[10]); k = 2; }
     if (fabs(adj[15]) > best) { best = fabs(adj[15]); k = 3; }
-    if (it >= 16 || best <= 1e-6 * F2 * sqrt(F2)) {
+    if (it >= 16 || best * best <= 1e-12 * F2 * F2 * F2) {   // best <= 1e-6 |S|_F^3, without the sqrt
         kabsch_rot_jacobi(A, R);
         return;
     }
@@ -555,17 +573,18 @@ RTG_DEV void kabsch_rot(const float A[9], float R[9])
 #pragma unroll
     for (int r = 0; r < 4; ++r)
         q[r] = k == 0 ? adj[r * 4] : (k == 1 ? adj[r * 4 + 1] : (k == 2 ? adj[r * 4 + 2] : adj[r * 4 + 3]));
-    const double qn = sqrt(q[0] * q[0] + q[1] * q[1] + q[2] * q[2] + q[3] * q[3]);
-    const double w = q[0] / qn, x = q[1] / qn, y = q[2] / qn, z = q[3] / qn;
-    R[0] = (float)(1.0 - 2.0 * (y * y + z * z));
-    R[1] = (float)(2.0 * (x * y - w * z));
-    R[2] = (float)(2.0 * (x * z + w * y));
-    R[3] = (float)(2.0 * (x * y + w * z));
-    R[4] = (float)(1.0 - 2.0 * (x * x + z * z));
-    R[5] = (float)(2.0 * (y * z - w * x));
-    R[6] = (float)(2.0 * (x * z - w * y));
-    R[7] = (float)(2.0 * (y * z + w * x));
-    R[8] = (float)(1.0 - 2.0 * (x * x + y * y));
+    // R(q) of the unnormalised column: R = I + s [..] with s = 2 / |q|^2 (one divide instead of sqrt + 4 divides)
+    const double w = q[0], x = q[1], y = q[2], z = q[3];
+    const double s = 2.0 / (w * w + x * x + y * y + z * z);
+    R[0] = (float)(1.0 - s * (y * y + z * z));
+    R[1] = (float)(s * (x * y - w * z));
+    R[2] = (float)(s * (x * z + w * y));
+    R[3] = (float)(s * (x * y + w * z));
+    R[4] = (float)(1.0 - s * (x * x + z * z));
+    R[5] = (float)(s * (y * z - w * x));
+    R[6] = (float)(s * (x * z - w * y));
+    R[7] = (float)(s * (y * z + w * x));
+    R[8] = (float)(1.0 - s * (x * x + y * y));
 }
 
 // cal_joint_quat (transform3d.py:31-50): A = M^T Z by einsum (sequential in j, no FMA)
@@ -683,10 +702,10 @@ RTG_DEV void shoulder_pr(V v1, ArmZero z0, Q parent, Q &pitch, Q &roll)
     const V ex{1.f, 0.f, 0.f}, ey{0.f, 1.f, 0.f};
     const V v1r = qrotate(qconj(parent), v1);
     const V v1p = proj_in_plane(v1r, ey);
-    const float th1 = radians_between(ex, v1p, ey);
-    pitch = qfrom_angle_axis(th1 - z0.th0, ey);
+    const float th1 = radians_between_axes(ex, v1p, ey);
+    pitch = qfrom_angle_unit_axis(th1 - z0.th0, ey);
     const float ph1 = radians_between(v1p, v1r, cross3(v1p, ey));
-    roll = qfrom_angle_axis(ph1 - z0.ph0, ex);
+    roll = qfrom_angle_unit_axis(ph1 - z0.ph0, ex);
 }
 
 // cal_elbowP_and_shoulderY (full_body_pos_retargeter.py:220-243)
@@ -695,10 +714,10 @@ RTG_DEV void elbow_py(V v1, ArmZero z0, Q parent, Q &yaw, Q &elbow)
     const V ex{1.f, 0.f, 0.f}, ey{0.f, 1.f, 0.f}, ez{0.f, 0.f, 1.f};
     const V v1r = qrotate(qconj(parent), v1);
     const V v1p = proj_in_plane(v1r, ez);
-    const float th1 = radians_between(ex, v1p, ez);
-    yaw = qfrom_angle_axis(th1 - z0.th0, ez);
+    const float th1 = radians_between_axes(ex, v1p, ez);
+    yaw = qfrom_angle_unit_axis(th1 - z0.th0, ez);
     const float ph1 = radians_between(v1p, v1r, cross3(ez, v1p));
-    elbow = qfrom_angle_axis(ph1 - z0.ph0, ey);
+    elbow = qfrom_angle_unit_axis(ph1 - z0.ph0, ey);
 }
 
 // torch sum of 5 elements (cascade reduce order, measured) / 5
