@@ -1391,15 +1391,14 @@ hipError_t launch_solver_prep(SolverConsts *dev_consts, hipStream_t s)
     return hipGetLastError();
 }
 
-// exp-map angle table (rtg_math.cuh, qexp_component_tab): one word of 16 two-bit codes per thread, each code
+// exp-map angle table (rtg_math.cuh, qexp_component_tab): one word of 8 four-bit codes per thread, each code
 // from the exact path it replaces.
 __global__ __launch_bounds__(256) void k_build_ang_tab(uint32_t *tab)
 {
     const uint32_t wd = blockIdx.x * 256u + threadIdx.x;
     if (wd >= kAngTabWords) return;
     uint32_t word = 0;
-    for (uint32_t e = 0; e < 16u; ++e)
-        word |= ang_tab_code(__uint_as_float(kAngTabLo + wd * 16u + e)) << (2u * e);
+    for (uint32_t e = 0; e < 8u; ++e) word |= ang_tab_code(__uint_as_float(kAngTabLo + wd * 8u + e)) << (4u * e);
     tab[wd] = word;
 }
 

@@ -316,35 +316,48 @@ RTG_DEV float qexp_component(Q q, int k)
 }
 
 // ------------------------------------------------ exp-map angle table
-// The angle of quat_to_angle_axis (:595-597) is normalize_angle(2 acos w) = atan2f(RN sin A, RN cos A) with
-// A = 2 RN(acos w): A moved by at most 2 ulps (glibc atan2f is not correctly rounded, so the move has no closed
-// form).  For w in [0.25, 1) -- joint angles below 151 degrees -- the move is tabulated: 2 bits per f32 w
-// (0: A, 1: A + 1 ulp, 2: A - 1 ulp, 3: not tabulated), 2^24 entries in 4 MiB, built on the device from the exact
-// path itself (ang_tab_code, k_build_ang_tab).  qexp_component_tab then skips sincos + atan2f (200 of the 330
-// instructions of an exp-map); w outside the table or a code-3 entry (260 of the 2^24) takes the exact path.
-// tools/check_fastmath.hip checks qexp_component_tab == qexp_component for every f32 w.
+// The angle of quat_to_angle_axis (:595-597) is R(w) = normalize_angle(2 acos w) = atan2f(RN sin A, RN cos A)
+// with A = 2 RN(acos w): glibc atan2f is not correctly rounded, so R has no closed form.  For w in [0.25, 1) --
+// joint angles below 151 degrees -- R(w) is stored as a 4-bit move from a cheap f32 estimate P(w) =
+// 4 asin(sqrt((1 - w) / 2)) (v_sqrt_f32 and a degree-6 fma polynomial, within 3 ulps of R): code c in 1..15 means
+// R = P + (c - 8) ulps, 0 means "not tabulated".  2^24 entries in 8 MiB, built on the device by the exact path
+// itself (ang_tab_code, k_build_ang_tab) with the same P.  qexp_component_tab thus skips acos, sincos and
+// atan2f (290 of the 330 instructions of an exp-map); w outside the table or a code-0 entry takes the exact
+// path.  tools/check_fastmath.hip checks qexp_component_tab == qexp_component for every f32 w.
 constexpr uint32_t kAngTabLo = 0x3e800000u;                     // bits of 0.25f
 constexpr uint32_t kAngTabEntries = 0x3f800000u - kAngTabLo;    // up to 1.0f (exclusive): 2^24
-constexpr uint32_t kAngTabWords = kAngTabEntries / 16u;         // 16 two-bit codes per word
+constexpr uint32_t kAngTabWords = kAngTabEntries / 8u;          // 8 four-bit codes per word
+RTG_DEV float exp_angle_estimate(float w)
+{
+    const float t2 = (1.0f - w) * 0.5f;
+    const float t = __builtin_amdgcn_sqrtf(t2);
+    float p = __builtin_fmaf(0.04965998747593211f, t2, -0.005969297163659217f);
+    p = __builtin_fmaf(p, t2, 0.029188122223620813f);
+    p = __builtin_fmaf(p, t2, 0.02938421651028137f);
+    p = __builtin_fmaf(p, t2, 0.0447135443846629f);
+    p = __builtin_fmaf(p, t2, 0.07499796602478857f);
+    p = __builtin_fmaf(p, t2, 0.1666666806527845f);
+    return 4.0f * __builtin_fmaf(t, t2 * p, t);
+}
 RTG_DEV uint32_t ang_tab_code(float w)
 {
-    const float A = 2.0f * cr_acos(w);
-    const float R = normalize_angle(A);
-    const int32_t d = (int32_t)__float_as_uint(R) - (int32_t)__float_as_uint(A);
-    if (!(R > 0.0f) || !(A > 0.0f)) return 3u;
-    return d == 0 ? 0u : (d == 1 ? 1u : (d == -1 ? 2u : 3u));
+    const float R = normalize_angle(2.0f * cr_acos(w));
+    const float P = exp_angle_estimate(w);
+    if (!(R > 0.0f) || !(P > 0.0f) || !(R < 4.0f) || !(P < 4.0f)) return 0u;
+    const int32_t d = (int32_t)__float_as_uint(R) - (int32_t)__float_as_uint(P);
+    return (d >= -7 && d <= 7) ? (uint32_t)(d + 8) : 0u;
 }
 RTG_DEV float qexp_component_tab(Q q, int k, const uint32_t *__restrict__ tab)
 {
     const uint32_t i = __float_as_uint(q.w) - kAngTabLo;
     const bool in = i < kAngTabEntries;
-    const uint32_t word = tab[in ? (i >> 4) : 0u];   // issued first: the acos below hides its latency
+    const uint32_t word = tab[in ? (i >> 3) : 0u];
     const float sin_theta = cr_sqrt(1.0f - q.w * q.w);
-    const float A = 2.0f * cr_acos(q.w);
     const bool mask = fabsf(sin_theta) > 1e-5f;
-    const uint32_t code = in ? (word >> ((i & 15u) * 2u)) & 3u : 3u;
-    float angle = __uint_as_float(__float_as_uint(A) + (code == 1u ? 1u : (code == 2u ? 0xffffffffu : 0u)));
-    if (__builtin_expect(mask && code == 3u, 0)) angle = normalize_angle(A);
+    const float P = exp_angle_estimate(q.w);
+    const uint32_t code = in ? (word >> ((i & 7u) * 4u)) & 15u : 0u;
+    float angle = __uint_as_float(__float_as_uint(P) + code - 8u);
+    if (__builtin_expect(mask && code == 0u, 0)) angle = normalize_angle(2.0f * cr_acos(q.w));
     const float a = mask ? angle : 0.0f;
     const float qk = k == 0 ? q.x : (k == 1 ? q.y : q.z);
     const float ak = mask ? qk / sin_theta : (k == 2 ? 1.0f : 0.0f);

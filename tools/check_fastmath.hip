@@ -78,7 +78,7 @@ __global__ void k_build_tab(uint32_t *tab)
     const uint32_t wd = blockIdx.x * 256u + threadIdx.x;
     if (wd >= kAngTabWords) return;
     uint32_t word = 0;
-    for (uint32_t e = 0; e < 16u; ++e) word |= ang_tab_code(__uint_as_float(kAngTabLo + wd * 16u + e)) << (2u * e);
+    for (uint32_t e = 0; e < 8u; ++e) word |= ang_tab_code(__uint_as_float(kAngTabLo + wd * 8u + e)) << (4u * e);
     tab[wd] = word;
 }
 
