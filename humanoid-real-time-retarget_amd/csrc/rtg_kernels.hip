@@ -62,17 +62,34 @@ struct Emit {
     float *row;                  // LDS row of this frame (30 DOFs)
     float *__restrict__ lr;      // local_rot row (31 x 4) or nullptr
     const uint32_t *__restrict__ ang;   // exp-map angle table (SolverConsts::ang_tab)
+    float2 *st;                  // LDS stash of this lane: (w, Hu_DOF_AXIS component) per DOF link, stride sst
+    int sst;
+    // links 12..18 and 21..27 (DOFs 11..17, 20..26) -> stash slots 0..13
+    template <int LINK>
+    static constexpr int slot() { return LINK <= 18 ? LINK - 12 : LINK - 14; }
     template <int LINK>
     RTG_DEV void link(Q q) const
     {
-        row[LINK - 1] = qexp_component_tab(q, hu_dof_axis(LINK - 1), ang);
+        constexpr int k = hu_dof_axis(LINK - 1);
+        st[slot<LINK>() * sst] = make_float2(q.w, k == 0 ? q.x : (k == 1 ? q.y : q.z));
         if (lr) st4(lr + 4 * LINK, q);
     }
     template <int LINK>
     RTG_DEV void identity() const   // untouched link: exp-map of the identity is +0
     {
-        row[LINK - 1] = 0.0f;
+        st[slot<LINK>() * sst] = make_float2(1.0f, 0.0f);
         if (lr) st4(lr + 4 * LINK, qident());
+    }
+    // The DOF read-out of slots [s0, s0 + n) in one batch: the table loads of all links are in flight together
+    // and their arithmetic interleaves, instead of one exposed load latency per link.
+    RTG_DEV void finalize(int s0, int n) const
+    {
+#pragma unroll
+        for (int j = 0; j < 14; ++j)
+            if (j >= s0 && j < s0 + n) {
+                const float2 v = st[j * sst];
+                row[j < 7 ? 11 + j : 13 + j] = exp_dof_tab(v.x, v.y, ang);
+            }
     }
 };
 
@@ -276,9 +293,11 @@ __global__ __launch_bounds__(kSolverBlock) void k_retarget(SolverConsts C, const
                                                            float *__restrict__ body_rot)
 {
     __shared__ float sdof[kSolverBlock * kDofStride];
+    __shared__ float2 sst[14 * kSolverBlock];
     const int64_t f = (int64_t)blockIdx.x * kSolverBlock + threadIdx.x;
     if (f < B) {
-        const Emit E{sdof + threadIdx.x * kDofStride, local_rot ? local_rot + f * 124 : nullptr, C.ang_tab};
+        const Emit E{sdof + threadIdx.x * kDofStride, local_rot ? local_rot + f * 124 : nullptr, C.ang_tab,
+                     sst + threadIdx.x, kSolverBlock};
         emit_fixed_links(E);
         if (KIND == RTG_SOLVER_FULL_BODY_POS)
             solve_full_body_pos<PRECISE>(C, load_fbp(in0 + f * 63, in1 + f * 60, in2 + f * 60), E,
@@ -289,6 +308,7 @@ __global__ __launch_bounds__(kSolverBlock) void k_retarget(SolverConsts C, const
             solve_full_body_rot(C, in0 + f * 84, in1 + f * 63, in2 + f * 60, in3 + f * 60, E);
         else
             solve_body_rot(C, in0 + f * 84, E);
+        E.finalize(0, 14);
     }
     __syncthreads();
     // coalesced store of the block's contiguous DOF tile: rows [f0, min(B, f0+256)) x 30.
@@ -441,11 +461,13 @@ __global__ __launch_bounds__(256) void k_solve_sides(SolverConsts C, const float
 {
     __shared__ float sdof[kSideFrames * kDofStride];
     __shared__ float4 storso[kSideFrames];   // the tile's torso fit, handed from the left wave to the right one
+    __shared__ float2 sst[2 * 14 * 64];      // exp-map stash, [tile][slot][lane]
     const int w = threadIdx.x >> 6, side = w & 1;
     const int r = (w >> 1) * 64 + (threadIdx.x & 63);   // tile row
     const int64_t f0 = (int64_t)blockIdx.x * kSideFrames, f = f0 + r;
     const bool live = f < B;
-    const Emit E{sdof + r * kDofStride, live && local_rot ? local_rot + f * 124 : nullptr, C.ang_tab};
+    const Emit E{sdof + r * kDofStride, live && local_rot ? local_rot + f * 124 : nullptr, C.ang_tab,
+                 sst + (w >> 1) * 14 * 64 + (threadIdx.x & 63), 64};
     if (KIND == RTG_SOLVER_FULL_BODY_POS || KIND == RTG_SOLVER_UPPER_BODY) {
         // The torso fit is shared by both sides: the left wave fits it while the right wave fits its own hand
         // (FULL_BODY_POS; nothing to overlap for UPPER_BODY), then one block barrier hands R10 over LDS.
@@ -486,6 +508,7 @@ __global__ __launch_bounds__(256) void k_solve_sides(SolverConsts C, const float
             else solve_body_rot_side<0>(C, in0 + f * 84, E);
         }
     }
+    if (live) E.finalize(side * 7, 7);
     __syncthreads();
     const int64_t nrows = (B - f0) < kSideFrames ? (B - f0) : kSideFrames;
     const int nvals = (int)nrows * 30;

@@ -347,21 +347,24 @@ RTG_DEV uint32_t ang_tab_code(float w)
     const int32_t d = (int32_t)__float_as_uint(R) - (int32_t)__float_as_uint(P);
     return (d >= -7 && d <= 7) ? (uint32_t)(d + 8) : 0u;
 }
-RTG_DEV float qexp_component_tab(Q q, int k, const uint32_t *__restrict__ tab)
+// quat_to_exp_map(q)[k] given only w = q.w and qk = q[k]: for |sin_theta| <= 1e-5 the reference's product is
+// 0 * (0 or 1) = +0 whatever k is, so the component index itself is not needed.
+RTG_DEV float exp_dof_tab(float w, float qk, const uint32_t *__restrict__ tab)
 {
-    const uint32_t i = __float_as_uint(q.w) - kAngTabLo;
+    const uint32_t i = __float_as_uint(w) - kAngTabLo;
     const bool in = i < kAngTabEntries;
     const uint32_t word = tab[in ? (i >> 3) : 0u];
-    const float sin_theta = cr_sqrt(1.0f - q.w * q.w);
+    const float sin_theta = cr_sqrt(1.0f - w * w);
     const bool mask = fabsf(sin_theta) > 1e-5f;
-    const float P = exp_angle_estimate(q.w);
+    const float P = exp_angle_estimate(w);
     const uint32_t code = in ? (word >> ((i & 7u) * 4u)) & 15u : 0u;
     float angle = __uint_as_float(__float_as_uint(P) + code - 8u);
-    if (__builtin_expect(mask && code == 0u, 0)) angle = normalize_angle(2.0f * cr_acos(q.w));
-    const float a = mask ? angle : 0.0f;
-    const float qk = k == 0 ? q.x : (k == 1 ? q.y : q.z);
-    const float ak = mask ? qk / sin_theta : (k == 2 ? 1.0f : 0.0f);
-    return a * ak;
+    if (__builtin_expect(mask && code == 0u, 0)) angle = normalize_angle(2.0f * cr_acos(w));
+    return mask ? angle * (qk / sin_theta) : 0.0f;
+}
+RTG_DEV float qexp_component_tab(Q q, int k, const uint32_t *__restrict__ tab)
+{
+    return exp_dof_tab(q.w, k == 0 ? q.x : (k == 1 ? q.y : q.z), tab);
 }
 
 // ------------------------------------------------ vectors (transform3d.py)
@@ -742,7 +745,7 @@ RTG_DEV float mean5(float v0, float v1, float v2, float v3, float v4)
 // Hu_v5.Hu_DOF_AXIS (retarget/robot_config/Hu_v5.py:12-18), dof k <-> link k+1
 __constant__ static const int8_t kHuDofAxis[30] = {2, 0, 1, 1, 1, 2, 0, 1, 1, 1, 2, 1, 0, 2, 1,
                                                    0, 1, 2, 1, 1, 1, 0, 2, 1, 0, 1, 2, 1, 1, 2};
-RTG_DEV int hu_dof_axis(int k)
+__host__ __device__ constexpr int hu_dof_axis(int k)
 {
     // compile-time table for unrolled uses; avoids a constant-memory load
     constexpr int8_t t[30] = {2, 0, 1, 1, 1, 2, 0, 1, 1, 1, 2, 1, 0, 2, 1,
