@@ -279,6 +279,12 @@ RTG_DEV void solve_body_rot(const SolverConsts &C, const float *__restrict__ g, 
 // solver kernel: per-frame body + coalesced DOF tile store
 // ----------------------------------------------------------------------------
 constexpr int kSolverBlock = 256;
+#ifndef RTG_SIDES_WAVES
+#define RTG_SIDES_WAVES 1   // min waves per SIMD for the side kernel (1: the compiler picks; measured best)
+#endif
+#ifndef RTG_EXP_HOT_INPUTS
+#define RTG_EXP_HOT_INPUTS 0
+#endif
 #ifndef RTG_SOLVER_SIDES
 #define RTG_SOLVER_SIDES 1   // 0: always the fused one-lane-per-frame kernels (k_retarget), for comparison
 #endif
@@ -453,7 +459,7 @@ RTG_DEV void solve_body_rot_side(const SolverConsts &C, const float *__restrict_
 }
 
 template <int KIND, bool PRECISE>
-__global__ __launch_bounds__(256) void k_solve_sides(SolverConsts C, const float *__restrict__ in0,
+__global__ __launch_bounds__(256, RTG_SIDES_WAVES) void k_solve_sides(SolverConsts C, const float *__restrict__ in0,
                                                      const float *__restrict__ in1, const float *__restrict__ in2,
                                                      const float *__restrict__ in3, int64_t B,
                                                      float *__restrict__ dof, float *__restrict__ local_rot,
@@ -468,17 +474,22 @@ __global__ __launch_bounds__(256) void k_solve_sides(SolverConsts C, const float
     const bool live = f < B;
     const Emit E{sdof + r * kDofStride, live && local_rot ? local_rot + f * 124 : nullptr, C.ang_tab,
                  sst + (w >> 1) * 14 * 64 + (threadIdx.x & 63), 64};
+#if RTG_EXP_HOT_INPUTS   // measurement knob (tools/build_variants.sh): every tile reads the first block's rows
+    const int64_t fi = f & (kSideFrames - 1);
+#else
+    const int64_t fi = f;
+#endif
     if (KIND == RTG_SOLVER_FULL_BODY_POS || KIND == RTG_SOLVER_UPPER_BODY) {
         // The torso fit is shared by both sides: the left wave fits it while the right wave fits its own hand
         // (FULL_BODY_POS; nothing to overlap for UPPER_BODY), then one block barrier hands R10 over LDS.
-        const float *b = in0 + f * 63;   // body (FULL_BODY_POS) / mocap points (UPPER_BODY), both (B, 21, 3)
+        const float *b = in0 + fi * 63;   // body (FULL_BODY_POS) / mocap points (UPPER_BODY), both (B, 21, 3)
         Q R10 = qident(), W = qident();
         if (live) {
             if (!side) {
                 R10 = KIND == RTG_SOLVER_FULL_BODY_POS ? fbp_torso(C, b) : upper_torso(C, b);
                 storso[r] = make_float4(R10.x, R10.y, R10.z, R10.w);
             } else if (KIND == RTG_SOLVER_FULL_BODY_POS) {
-                W = fbp_wrist_fit<1>(C, in2 + f * 60);
+                W = fbp_wrist_fit<1>(C, in2 + fi * 60);
             }
         }
         __syncthreads();
@@ -491,8 +502,8 @@ __global__ __launch_bounds__(256) void k_solve_sides(SolverConsts C, const float
             }
             if (KIND == RTG_SOLVER_FULL_BODY_POS) {
                 float *brow = body_rot ? body_rot + f * 236 : nullptr;
-                if (side) solve_fbp_side<PRECISE, 1>(C, b, in2 + f * 60, R10, W, E, brow);
-                else solve_fbp_side<PRECISE, 0>(C, b, in1 + f * 60, R10, fbp_wrist_fit<0>(C, in1 + f * 60), E, brow);
+                if (side) solve_fbp_side<PRECISE, 1>(C, b, in2 + fi * 60, R10, W, E, brow);
+                else solve_fbp_side<PRECISE, 0>(C, b, in1 + fi * 60, R10, fbp_wrist_fit<0>(C, in1 + fi * 60), E, brow);
             } else {
                 if (side) solve_upper_side<1>(C, b, R10, E);
                 else solve_upper_side<0>(C, b, R10, E);
@@ -501,11 +512,11 @@ __global__ __launch_bounds__(256) void k_solve_sides(SolverConsts C, const float
     } else if (live) {
         if (!side) emit_fixed_links(E);
         if (KIND == RTG_SOLVER_FULL_BODY_ROT) {
-            if (side) solve_full_body_rot_side<1>(C, in0 + f * 84, in1 + f * 63, in3 + f * 60, E);
-            else solve_full_body_rot_side<0>(C, in0 + f * 84, in1 + f * 63, in2 + f * 60, E);
+            if (side) solve_full_body_rot_side<1>(C, in0 + fi * 84, in1 + fi * 63, in3 + fi * 60, E);
+            else solve_full_body_rot_side<0>(C, in0 + fi * 84, in1 + fi * 63, in2 + fi * 60, E);
         } else {
-            if (side) solve_body_rot_side<1>(C, in0 + f * 84, E);
-            else solve_body_rot_side<0>(C, in0 + f * 84, E);
+            if (side) solve_body_rot_side<1>(C, in0 + fi * 84, E);
+            else solve_body_rot_side<0>(C, in0 + fi * 84, E);
         }
     }
     if (live) E.finalize(side * 7, 7);

@@ -324,6 +324,9 @@ RTG_DEV float qexp_component(Q q, int k)
 // itself (ang_tab_code, k_build_ang_tab) with the same P.  qexp_component_tab thus skips acos, sincos and
 // atan2f (290 of the 330 instructions of an exp-map); w outside the table or a code-0 entry takes the exact
 // path.  tools/check_fastmath.hip checks qexp_component_tab == qexp_component for every f32 w.
+#ifndef RTG_EXP_NO_TABLE
+#define RTG_EXP_NO_TABLE 0
+#endif
 constexpr uint32_t kAngTabLo = 0x3e800000u;                     // bits of 0.25f
 constexpr uint32_t kAngTabEntries = 0x3f800000u - kAngTabLo;    // up to 1.0f (exclusive): 2^24
 constexpr uint32_t kAngTabWords = kAngTabEntries / 8u;          // 8 four-bit codes per word
@@ -353,7 +356,11 @@ RTG_DEV float exp_dof_tab(float w, float qk, const uint32_t *__restrict__ tab)
 {
     const uint32_t i = __float_as_uint(w) - kAngTabLo;
     const bool in = i < kAngTabEntries;
+#if RTG_EXP_NO_TABLE   // measurement knob (tools/build_variants.sh): no table traffic, wrong angles
+    const uint32_t word = 0x88888888u + 0u * tab[0];
+#else
     const uint32_t word = tab[in ? (i >> 3) : 0u];
+#endif
     const float sin_theta = cr_sqrt(1.0f - w * w);
     const bool mask = fabsf(sin_theta) > 1e-5f;
     const float P = exp_angle_estimate(w);
