@@ -216,17 +216,18 @@ def main():
         b, l, r_, d = sets[i % ring]
         solver.retarget([b, l, r_], out_dof=d)
     barrier(world)
-    starts = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps)]
-    ends = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps)]
+    # kernel time: one HIP event pair around the K launches on the launch stream (a pair per launch would add each
+    # event's own packet and cache release to every launch, ~10 us, which rocprofv3's kernel trace does not see)
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     t0 = time.perf_counter()
+    ev0.record(stream)
     for i in range(args.steps):
         b, l, r_, d = sets[i % ring]
-        starts[i].record(stream)
         solver.retarget([b, l, r_], out_dof=d)
-        ends[i].record(stream)
+    ev1.record(stream)
     barrier(world)
     wall = time.perf_counter() - t0
-    kern_ms = float(np.mean([s.elapsed_time(e) for s, e in zip(starts, ends)]))
+    kern_ms = ev0.elapsed_time(ev1) / args.steps
     if world > 1:
         wall = shard.max_over_ranks(wall, dev)
     frames = world * B * args.steps

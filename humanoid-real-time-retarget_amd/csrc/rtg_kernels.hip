@@ -1425,20 +1425,18 @@ hipError_t launch_solver_prep(SolverConsts *dev_consts, hipStream_t s)
     return hipGetLastError();
 }
 
-// exp-map angle table (rtg_math.cuh, qexp_component_tab): one word of 8 four-bit codes per thread, each code
+// exp-map angle table (rtg_math.cuh, qexp_component_tab): one word of codes per thread, each code
 // from the exact path it replaces.
 __global__ __launch_bounds__(256) void k_build_ang_tab(uint32_t *tab)
 {
     const uint32_t wd = blockIdx.x * 256u + threadIdx.x;
     if (wd >= kAngTabWords) return;
-    uint32_t word = 0;
-    for (uint32_t e = 0; e < 8u; ++e) word |= ang_tab_code(__uint_as_float(kAngTabLo + wd * 8u + e)) << (4u * e);
-    tab[wd] = word;
+    tab[wd] = ang_tab_build_word(wd);
 }
 
 hipError_t launch_build_ang_tab(uint32_t *tab, hipStream_t s)
 {
-    hipLaunchKernelGGL(k_build_ang_tab, dim3(kAngTabWords / 256u), dim3(256), 0, s, tab);
+    hipLaunchKernelGGL(k_build_ang_tab, dim3((kAngTabWords + 255u) / 256u), dim3(256), 0, s, tab);
     return hipGetLastError();
 }
 

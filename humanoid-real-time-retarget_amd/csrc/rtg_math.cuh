@@ -329,7 +329,14 @@ RTG_DEV float qexp_component(Q q, int k)
 #endif
 constexpr uint32_t kAngTabLo = 0x3e800000u;                     // bits of 0.25f
 constexpr uint32_t kAngTabEntries = 0x3f800000u - kAngTabLo;    // up to 1.0f (exclusive): 2^24
-constexpr uint32_t kAngTabWords = kAngTabEntries / 8u;          // 8 four-bit codes per word
+#ifndef RTG_ANG_TAB_BITS
+#define RTG_ANG_TAB_BITS 3
+#endif
+constexpr uint32_t kAngTabBits = RTG_ANG_TAB_BITS;              // 3: moves -3..3, 10 codes per word; 4: -7..7, 8
+constexpr uint32_t kAngTabPer = kAngTabBits == 3 ? 10u : 8u;
+constexpr uint32_t kAngTabWords = (kAngTabEntries + kAngTabPer - 1) / kAngTabPer;
+constexpr uint32_t kAngTabBias = 1u << (kAngTabBits - 1);      // code = move + bias; code 0 = not tabulated
+RTG_DEV uint32_t ang_tab_word(uint32_t i) { return kAngTabPer == 10u ? __umulhi(i, 0xCCCCCCCDu) >> 3 : i >> 3; }
 RTG_DEV float exp_angle_estimate(float w)
 {
     const float t2 = (1.0f - w) * 0.5f;
@@ -348,7 +355,18 @@ RTG_DEV uint32_t ang_tab_code(float w)
     const float P = exp_angle_estimate(w);
     if (!(R > 0.0f) || !(P > 0.0f) || !(R < 4.0f) || !(P < 4.0f)) return 0u;
     const int32_t d = (int32_t)__float_as_uint(R) - (int32_t)__float_as_uint(P);
-    return (d >= -7 && d <= 7) ? (uint32_t)(d + 8) : 0u;
+    const int32_t lim = (int32_t)kAngTabBias - 1;
+    return (d >= -lim && d <= lim) ? (uint32_t)(d + (int32_t)kAngTabBias) : 0u;
+}
+// word wd of the table: the codes of entries wd * kAngTabPer ... (k_build_ang_tab, tools/check_fastmath.hip)
+RTG_DEV uint32_t ang_tab_build_word(uint32_t wd)
+{
+    uint32_t word = 0;
+    for (uint32_t e = 0; e < kAngTabPer; ++e) {
+        const uint32_t i = wd * kAngTabPer + e;
+        if (i < kAngTabEntries) word |= ang_tab_code(__uint_as_float(kAngTabLo + i)) << (kAngTabBits * e);
+    }
+    return word;
 }
 // quat_to_exp_map(q)[k] given only w = q.w and qk = q[k]: for |sin_theta| <= 1e-5 the reference's product is
 // 0 * (0 or 1) = +0 whatever k is, so the component index itself is not needed.
@@ -357,15 +375,17 @@ RTG_DEV float exp_dof_tab(float w, float qk, const uint32_t *__restrict__ tab)
     const uint32_t i = __float_as_uint(w) - kAngTabLo;
     const bool in = i < kAngTabEntries;
 #if RTG_EXP_NO_TABLE   // measurement knob (tools/build_variants.sh): no table traffic, wrong angles
-    const uint32_t word = 0x88888888u + 0u * tab[0];
+    const uint32_t wd = ang_tab_word(i);
+    const uint32_t word = 0x24924924u + 0u * tab[0];
 #else
-    const uint32_t word = tab[in ? (i >> 3) : 0u];
+    const uint32_t wd = ang_tab_word(i);
+    const uint32_t word = tab[in ? wd : 0u];
 #endif
     const float sin_theta = cr_sqrt(1.0f - w * w);
     const bool mask = fabsf(sin_theta) > 1e-5f;
     const float P = exp_angle_estimate(w);
-    const uint32_t code = in ? (word >> ((i & 7u) * 4u)) & 15u : 0u;
-    float angle = __uint_as_float(__float_as_uint(P) + code - 8u);
+    const uint32_t code = in ? (word >> ((i - wd * kAngTabPer) * kAngTabBits)) & ((1u << kAngTabBits) - 1u) : 0u;
+    float angle = __uint_as_float(__float_as_uint(P) + code - kAngTabBias);
     if (__builtin_expect(mask && code == 0u, 0)) angle = normalize_angle(2.0f * cr_acos(w));
     return mask ? angle * (qk / sin_theta) : 0.0f;
 }

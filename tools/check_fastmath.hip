@@ -77,9 +77,7 @@ __global__ void k_build_tab(uint32_t *tab)
 {
     const uint32_t wd = blockIdx.x * 256u + threadIdx.x;
     if (wd >= kAngTabWords) return;
-    uint32_t word = 0;
-    for (uint32_t e = 0; e < 8u; ++e) word |= ang_tab_code(__uint_as_float(kAngTabLo + wd * 8u + e)) << (4u * e);
-    tab[wd] = word;
+    tab[wd] = ang_tab_build_word(wd);
 }
 
 __global__ void k_exptab(uint64_t base, const uint32_t *tab, unsigned long long *bad)
@@ -100,7 +98,7 @@ int main()
     (void)hipMemset(bad, 0, 4 * sizeof(unsigned long long));
     uint32_t *tab;
     (void)hipMalloc(&tab, kAngTabWords * sizeof(uint32_t));
-    hipLaunchKernelGGL(k_build_tab, dim3(kAngTabWords / 256u), dim3(256), 0, 0, tab);
+    hipLaunchKernelGGL(k_build_tab, dim3((kAngTabWords + 255u) / 256u), dim3(256), 0, 0, tab);
     const uint64_t chunk = 1ull << 30;
     for (uint64_t base = 0; base < (1ull << 32); base += chunk) {
         hipLaunchKernelGGL(k_sqrt, dim3((unsigned)(chunk / 256)), dim3(256), 0, 0, base, bad);
