@@ -400,7 +400,7 @@ int rtg_solver_create(int kind, const float *zl, const float *zg, const int32_t 
     if (rc == RTG_OK) rc = hip_check(hipMemcpy(&C, d, sizeof C, hipMemcpyDeviceToHost), "hipMemcpy(consts)");
     (void)hipFree(d);
     if (rc != RTG_OK) return rc;
-    // exp-map angle table: built once per solver on the current device (8 MiB), read by every launch
+    // exp-map angle table: built once per solver on the current device (6.7 MiB), read by every launch
     uint32_t *tab = nullptr;
     RTG_TRY(hipMalloc(&tab, kAngTabWords * sizeof(uint32_t)), "hipMalloc(exp-map angle table)");
     rc = hip_check(launch_build_ang_tab(tab, nullptr), "k_build_ang_tab");

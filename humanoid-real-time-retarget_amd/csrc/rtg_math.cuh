@@ -318,9 +318,10 @@ RTG_DEV float qexp_component(Q q, int k)
 // ------------------------------------------------ exp-map angle table
 // The angle of quat_to_angle_axis (:595-597) is R(w) = normalize_angle(2 acos w) = atan2f(RN sin A, RN cos A)
 // with A = 2 RN(acos w): glibc atan2f is not correctly rounded, so R has no closed form.  For w in [0.25, 1) --
-// joint angles below 151 degrees -- R(w) is stored as a 4-bit move from a cheap f32 estimate P(w) =
-// 4 asin(sqrt((1 - w) / 2)) (v_sqrt_f32 and a degree-6 fma polynomial, within 3 ulps of R): code c in 1..15 means
-// R = P + (c - 8) ulps, 0 means "not tabulated".  2^24 entries in 8 MiB, built on the device by the exact path
+// joint angles below 151 degrees -- R(w) is stored as a short move from a cheap f32 estimate P(w) =
+// 4 asin(sqrt((1 - w) / 2)) (v_sqrt_f32 and a degree-6 fma polynomial, within 3 ulps of R): the 3-bit code c in
+// 1..7 means R = P + (c - 4) ulps, 0 means "not tabulated" (exact path).  2^24 entries, 10 per 32-bit word, in
+// 6.7 MiB (RTG_ANG_TAB_BITS=4 packs 8 per word in 8 MiB; measured no faster), built on the device by the exact path
 // itself (ang_tab_code, k_build_ang_tab) with the same P.  qexp_component_tab thus skips acos, sincos and
 // atan2f (290 of the 330 instructions of an exp-map); w outside the table or a code-0 entry takes the exact
 // path.  tools/check_fastmath.hip checks qexp_component_tab == qexp_component for every f32 w.
