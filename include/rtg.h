@@ -159,7 +159,11 @@ typedef enum rtg_solver_kind {
  * RobotZeroPose local / global translations (Js,3), src_parents (Js) -- host
  * pointers.  The target is always Hu v5 (31 links, 30 DOFs; Hu_v5.py:12-18).
  * Zero-pose-only terms of the joint maps (theta0 / phi0, Kabsch zero vectors,
- * gripper denominator) are evaluated once here, on the device. */
+ * gripper denominator) are evaluated once here, on the device.  The solver
+ * also owns a 6.7 MiB exp-map angle table, built here on the current device
+ * (synchronously); use the solver on that device only.  Replaces the
+ * constructors at full_body_pos_retargeter.py:18, retarget_solver.py:28,
+ * full_body_retargeter.py:16, body_retargeter.py:31. */
 int rtg_solver_create(int kind, const float *src_zero_local_t, const float *src_zero_global_t,
                       const int32_t *src_parents, int32_t Js, int precise_gripper, rtg_solver_t *out);
 int rtg_solver_destroy(rtg_solver_t solver);
