@@ -288,6 +288,19 @@ constexpr int kSolverBlock = 256;
 #ifndef RTG_SOLVER_SIDES
 #define RTG_SOLVER_SIDES 1   // 0: always the fused one-lane-per-frame kernels (k_retarget), for comparison
 #endif
+#ifndef RTG_L2_PREFETCH
+#define RTG_L2_PREFETCH 0    // 1: each side wave pulls the input rows it reads late into L2 at kernel start
+#endif
+
+// Fire-and-forget touch of the 128-byte lines covering [p, p + nbytes): one line per lane per instruction, loaded
+// by LDS-DMA into a sink slot nobody reads, so no VGPR is held while the line travels.
+RTG_DEV void l2_touch(const float *p, int nbytes, float *sink)
+{
+    const int nlines = (nbytes + 127) >> 7;
+    for (int k = threadIdx.x & 63; k < nlines; k += 64)
+        __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void *)(p + 32 * k),
+                                         (__attribute__((address_space(3))) void *)sink, 4, 0, 0);
+}
 constexpr int kDofStride = 31;   // LDS row pitch (dwords): odd -> conflict-free ds_write_b32
 
 template <int KIND, bool PRECISE>
@@ -478,6 +491,16 @@ __global__ __launch_bounds__(256, RTG_SIDES_WAVES) void k_solve_sides(SolverCons
     const int64_t fi = f & (kSideFrames - 1);
 #else
     const int64_t fi = f;
+#endif
+#if RTG_L2_PREFETCH
+    if (KIND == RTG_SOLVER_FULL_BODY_POS) {
+        __shared__ float sink[64 * 4];
+        const int64_t ft = f0 + (w >> 1) * 64, nt = B - ft < 64 ? B - ft : 64;
+        if (nt > 0) {
+            if (side) l2_touch(in0 + ft * 63, (int)nt * 252, sink + 64 * (w & 3));   // the right arm's body rows
+            else l2_touch(in1 + ft * 60, (int)nt * 240, sink + 64 * (w & 3));       // the left hand
+        }
+    }
 #endif
     if (KIND == RTG_SOLVER_FULL_BODY_POS || KIND == RTG_SOLVER_UPPER_BODY) {
         // The torso fit is shared by both sides: the left wave fits it while the right wave fits its own hand
