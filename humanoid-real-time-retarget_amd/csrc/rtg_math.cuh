@@ -9,8 +9,8 @@
 //    here they are correctly rounded (evaluated in float64, rounded once).
 //  * atan2 on the 30-element DOF tensor runs glibc's scalar atan2f: restated
 //    exactly (fdlibm s_atanf/e_atan2f).
-//  * torch.linalg.svd (MKL sgesdd) in the Kabsch fit: the proper-rotation polar
-//    factor is computed in float64 (cyclic Jacobi on A^T A) and rounded.
+//  * torch.linalg.svd (MKL sgesdd) in the Kabsch fit: oneMKL 2024.2's 3x3 path
+//    (SGEBD2 / SBDSQR / SORMBR with MKL's measured FMA placement), restated.
 //  * scipy Rotation.as_euler / from_euler: float64 restatement.
 #pragma once
 #include <hip/hip_runtime.h>
@@ -437,198 +437,490 @@ RTG_DEV float radians_between_axes(V v1, V v2, V n)
     return cr_acos(c) * tsign(dot3(n, cross3(v1, v2)));
 }
 
-// ------------------------------------------------ Kabsch (float64)
-// Proper-rotation polar factor of A: R = u1 v1^T + u2 v2^T + (u1 x u2)(v1 x v2)^T
-// where (v_i) are eigenvectors of A^T A for the two largest eigenvalues and
-// u_i = A v_i / |A v_i| (u2 re-orthogonalised).  Equals U diag(1,1,det(UV^T)) V^T,
-// the reference's det-fixed SVD solution (transform3d.py:40-45).
-RTG_DEV void jacobi_eig3(double S[3][3], double Vm[3][3])
+// ------------------------------------------------ Kabsch: torch.linalg.svd as MKL sgesdd computes it
+// transform3d.py:40-45 runs torch.linalg.svd on one (1,3,3) float32 matrix, i.e. oneMKL 2024.2 SGESDD(JOBZ='A').
+// For 3x3 that is SGEBD2 -> SBDSDC('U','I') -> SLASDQ -> SBDSQR -> SORMBR('Q') on U / SORMBR('P') on VT.  Each
+// routine follows the published LAPACK algorithm; the FMA placement inside MKL's BLAS kernels was measured stage
+// by stage against MKL's own entry points (tools/mkl_sgesdd_probe.py) and matches bit for bit.  The
+// oracle (oracle/rtg_oracle.c, la_gesdd3) restates the same routines independently.  All divisions / square
+// roots are IEEE-exact (fdiv = one rcp64 + mulr, cr_sqrt).  Matrices are column-major: a[r + 3 c].
+RTG_DEV float fdiv(float a, float b) { return mulr(a, rcp64(b)); }
+RTG_DEV float la_sign(float a, float b) { return __builtin_copysignf(fabsf(a), b); }   // Fortran SIGN
+RTG_DEV float la_lapy2(float x, float y)                                                 // SLAPY2
 {
-#pragma unroll
-    for (int i = 0; i < 3; ++i)
-#pragma unroll
-        for (int j = 0; j < 3; ++j) Vm[i][j] = i == j ? 1.0 : 0.0;
-    for (int sweep = 0; sweep < 8; ++sweep) {
-#pragma unroll
-        for (int r = 0; r < 3; ++r) {
-            const int p = r == 2 ? 1 : 0;
-            const int qq = r == 0 ? 1 : 2;
-            const double apq = S[p][qq];
-            if (apq == 0.0) continue;
-            const double theta = (S[qq][qq] - S[p][p]) / (2.0 * apq);
-            double t = 1.0 / (fabs(theta) + sqrt(theta * theta + 1.0));
-            if (theta < 0.0) t = -t;
-            const double c = 1.0 / sqrt(t * t + 1.0);
-            const double s = t * c;
-#pragma unroll
-            for (int k = 0; k < 3; ++k) {
-                const double skp = S[k][p], skq = S[k][qq];
-                S[k][p] = c * skp - s * skq;
-                S[k][qq] = s * skp + c * skq;
+    const float xa = fabsf(x), ya = fabsf(y);
+    const float w = fmaxf(xa, ya), z = fminf(xa, ya);
+    const float r = fdiv(z, w);
+    return z == 0.0f ? w : w * cr_sqrt(1.0f + r * r);
+}
+// SLARFG(n, alpha, x): n = 3 (x = x0, x1) or n = 2 (x = x0); returns tau, updates alpha (= beta) and x
+template <int NX>
+RTG_DEV float la_larfg(float &alpha, float &x0, float &x1)
+{
+    const float safmin = 1.17549435e-38f / 5.96046448e-08f, rsafmn = 1.0f / safmin;
+    float xn = NX == 1 ? fabsf(x0) : la_lapy2(x0, x1);
+    if (xn == 0.0f) return 0.0f;
+    float beta = -__builtin_copysignf(la_lapy2(alpha, xn), alpha);
+    int knt = 0;
+    if (__builtin_expect(fabsf(beta) < safmin, 0)) {
+        do {
+            ++knt;
+            x0 *= rsafmn;
+            if (NX == 2) x1 *= rsafmn;
+            beta *= rsafmn;
+            alpha *= rsafmn;
+        } while (fabsf(beta) < safmin && knt < 20);
+        xn = NX == 1 ? fabsf(x0) : la_lapy2(x0, x1);
+        beta = -__builtin_copysignf(la_lapy2(alpha, xn), alpha);
+    }
+    const float tau = fdiv(beta - alpha, beta);
+    const float sc = fdiv(1.0f, alpha - beta);
+    x0 *= sc;
+    if (NX == 2) x1 *= sc;
+    for (int j = 0; j < knt; ++j) beta *= safmin;
+    alpha = beta;
+    return tau;
+}
+RTG_DEV void la_lartg(float f, float g, float &c, float &s, float &r)   // SLARTG (LAPACK >= 3.10)
+{
+    const float safmin = 1.17549435e-38f, safmax = 1.0f / safmin;
+    const float rtmin = 1.08420217e-19f, rtmax = 1.30438176e+19f;   // sqrt(safmin), sqrt(safmax / 2)
+    const float f1 = fabsf(f), g1 = fabsf(g);
+    if (g == 0.0f) { c = 1.0f; s = 0.0f; r = f; }
+    else if (f == 0.0f) { c = 0.0f; s = __builtin_copysignf(1.0f, g); r = g1; }
+    else if (f1 > rtmin && f1 < rtmax && g1 > rtmin && g1 < rtmax) {
+        const float d = cr_sqrt(f * f + g * g);
+        const Rcp rd = rcp64(d);
+        c = mulr(f1, rd);
+        r = __builtin_copysignf(d, f);
+        s = f < 0.0f ? -mulr(g, rd) : mulr(g, rd);   // g / r with r = +-d (RN is sign-symmetric)
+    } else {
+        const float u = fminf(safmax, fmaxf(safmin, fmaxf(f1, g1)));
+        const float fs = fdiv(f, u), gs = fdiv(g, u), d = cr_sqrt(fs * fs + gs * gs);
+        c = fdiv(fabsf(fs), d);
+        r = __builtin_copysignf(d, f);
+        s = fdiv(gs, r);
+        r *= u;
+    }
+}
+RTG_DEV float la_las2_min(float f, float g, float h)   // SLAS2, SSMIN only (the shift)
+{
+    const float fa = fabsf(f), ga = fabsf(g), ha = fabsf(h);
+    const float fhmn = fminf(fa, ha), fhmx = fmaxf(fa, ha);
+    if (fhmn == 0.0f) return 0.0f;
+    if (ga < fhmx) {
+        const float as = 1.0f + fdiv(fhmn, fhmx), at = fdiv(fhmx - fhmn, fhmx);
+        float au = fdiv(ga, fhmx);
+        au = au * au;
+        const float c = fdiv(2.0f, cr_sqrt(as * as + au) + cr_sqrt(at * at + au));
+        return fhmn * c;
+    }
+    const float au = fdiv(fhmx, ga);
+    if (au == 0.0f) return fdiv(fhmn * fhmx, ga);
+    const float as = 1.0f + fdiv(fhmn, fhmx), at = fdiv(fhmx - fhmn, fhmx), p = as * au, q = at * au;
+    const float c = fdiv(1.0f, cr_sqrt(1.0f + p * p) + cr_sqrt(1.0f + q * q));
+    const float mn = (fhmn * c) * au;
+    return mn + mn;
+}
+// SLASV2
+RTG_DEV void la_lasv2(float f, float g, float h, float &ssmin, float &ssmax, float &snr, float &csr, float &snl,
+                      float &csl)
+{
+    const float eps = 5.96046448e-08f;
+    float ft = f, fa = fabsf(ft), ht = h, ha = fabsf(h), gt = g;
+    float clt = 1.0f, crt = 1.0f, slt = 0.0f, srt = 0.0f;
+    int pmax = 1;
+    const bool swap = ha > fa;
+    if (swap) { pmax = 3; float t = ft; ft = ht; ht = t; t = fa; fa = ha; ha = t; }
+    const float ga = fabsf(gt);
+    if (ga == 0.0f) { ssmin = ha; ssmax = fa; }
+    else {
+        bool gasmal = true;
+        if (ga > fa) {
+            pmax = 2;
+            if (fdiv(fa, ga) < eps) {
+                gasmal = false;
+                ssmax = ga;
+                ssmin = ha > 1.0f ? fdiv(fa, fdiv(ga, ha)) : fdiv(fa, ga) * ha;
+                clt = 1.0f; slt = fdiv(ht, gt); srt = 1.0f; crt = fdiv(ft, gt);
             }
+        }
+        if (gasmal) {
+            const float d = fa - ha, l = d == fa ? 1.0f : fdiv(d, fa);
+            const float m = fdiv(gt, ft), mm = m * m;
+            float t = 2.0f - l;
+            const float tt = t * t;
+            const float s = cr_sqrt(tt + mm);
+            const float r = l == 0.0f ? fabsf(m) : cr_sqrt(l * l + mm);
+            const float a = 0.5f * (s + r);
+            ssmin = fdiv(ha, a);
+            ssmax = fa * a;
+            if (mm == 0.0f) t = l == 0.0f ? la_sign(2.0f, ft) * la_sign(1.0f, gt) : fdiv(gt, la_sign(d, ft)) + fdiv(m, t);
+            else t = (fdiv(m, s + t) + fdiv(m, r + l)) * (1.0f + a);
+            const float l2 = cr_sqrt(t * t + 4.0f);
+            const Rcp rl = rcp64(l2);
+            crt = mulr(2.0f, rl);
+            srt = mulr(t, rl);
+            const Rcp ra = rcp64(a);
+            clt = mulr(crt + srt * m, ra);
+            slt = mulr(fdiv(ht, ft) * srt, ra);
+        }
+    }
+    if (swap) { csl = srt; snl = crt; csr = slt; snr = clt; }
+    else { csl = clt; snl = slt; csr = crt; snr = srt; }
+    const float tsg = pmax == 1 ? la_sign(1.0f, csr) * la_sign(1.0f, csl) * la_sign(1.0f, f)
+                    : pmax == 2 ? la_sign(1.0f, snr) * la_sign(1.0f, csl) * la_sign(1.0f, g)
+                                : la_sign(1.0f, snr) * la_sign(1.0f, snl) * la_sign(1.0f, h);
+    ssmax = la_sign(ssmax, tsg);
+    ssmin = la_sign(ssmin, tsg * la_sign(1.0f, f) * la_sign(1.0f, h));
+}
+RTG_DEV void la_rot(float &x, float &y, float c, float s)   // MKL's SROT / SLASR pair update
+{
+    const float xv = x, yv = y;
+    x = __builtin_fmaf(s, yv, c * xv);
+    y = __builtin_fmaf(c, yv, -(s * xv));
+}
+struct Svd3 { float u[9], vt[9]; };
+// rotate VT rows (r, r+1) / U columns (r, r+1), r in {0, 1} (runtime)
+RTG_DEV void vt_rot(Svd3 &z, int r, float c, float s)
+{
+    if (r == 0) {
 #pragma unroll
-            for (int k = 0; k < 3; ++k) {
-                const double spk = S[p][k], sqk = S[qq][k];
-                S[p][k] = c * spk - s * sqk;
-                S[qq][k] = s * spk + c * sqk;
+        for (int k = 0; k < 3; ++k) la_rot(z.vt[0 + 3 * k], z.vt[1 + 3 * k], c, s);
+    } else {
+#pragma unroll
+        for (int k = 0; k < 3; ++k) la_rot(z.vt[1 + 3 * k], z.vt[2 + 3 * k], c, s);
+    }
+}
+RTG_DEV void u_rot(Svd3 &z, int r, float c, float s)
+{
+    if (r == 0) {
+#pragma unroll
+        for (int k = 0; k < 3; ++k) la_rot(z.u[k], z.u[k + 3], c, s);
+    } else {
+#pragma unroll
+        for (int k = 0; k < 3; ++k) la_rot(z.u[k + 3], z.u[k + 6], c, s);
+    }
+}
+// SBDSQR('U', 3, ncvt = 3, nru = 3, ncc = 0) from U = VT = I (SBDSDC / SLASDQ), n = 3 specialised: the only
+// multi-element block is (ll, m) = (1, 3), every other case is a 2x2 SLASV2 block.
+RTG_DEV void la_bdsqr3(float &d1, float &d2, float &d3, float e1, float e2, Svd3 &z)
+{
+    const float eps = 5.96046448e-08f, tol = 10.0f * eps, unfl = 1.17549435e-38f;
+    float sminoa = fabsf(d1);
+    if (sminoa != 0.0f) {
+        float mu = fabsf(d2) * fdiv(sminoa, sminoa + fabsf(e1));
+        sminoa = fminf(sminoa, mu);
+        if (sminoa != 0.0f) {
+            mu = fabsf(d3) * fdiv(mu, mu + fabsf(e2));
+            sminoa = fminf(sminoa, mu);
+        }
+    }
+    sminoa = fdiv(sminoa, 1.73205078f);   // / sqrt(real(3))
+    const float thresh = fmaxf(tol * sminoa, 6.0f * (3.0f * (3.0f * unfl)));
+    int m = 3, iter = -1, iterdivn = 0, idir = 0;
+    bool fresh = true;   // (ll, m) = (1, 3) differs from (oldll, oldm)
+    for (;;) {
+        if (m <= 1) break;
+        if (iter >= 3) { iter -= 3; if (++iterdivn >= 18) break; }   // no convergence: INFO > 0 (never seen)
+        if (m == 2) {                       // block (1, 2)
+            if (fabsf(e1) <= thresh) { e1 = 0.0f; break; }
+            float sigmn, sigmx, sinr, cosr, sinl, cosl;
+            la_lasv2(d1, e1, d2, sigmn, sigmx, sinr, cosr, sinl, cosl);
+            d1 = sigmx; e1 = 0.0f; d2 = sigmn;
+            vt_rot(z, 0, cosr, sinr);
+            u_rot(z, 0, cosl, sinl);
+            break;
+        }
+        // m == 3
+        if (fabsf(e2) <= thresh) { e2 = 0.0f; m = 2; continue; }
+        const float smax = fmaxf(fmaxf(fabsf(d3), fmaxf(fabsf(d2), fabsf(e2))), fmaxf(fabsf(d1), fabsf(e1)));
+        if (fabsf(e1) <= thresh) {          // split at E(1): block (2, 3)
+            e1 = 0.0f;
+            float sigmn, sigmx, sinr, cosr, sinl, cosl;
+            la_lasv2(d2, e2, d3, sigmn, sigmx, sinr, cosr, sinl, cosl);
+            d2 = sigmx; e2 = 0.0f; d3 = sigmn;
+            vt_rot(z, 1, cosr, sinr);
+            u_rot(z, 1, cosl, sinl);
+            break;
+        }
+        if (fresh) { idir = fabsf(d1) >= fabsf(d3) ? 1 : 2; fresh = false; }
+        float smin;
+        if (idir == 1) {
+            if (fabsf(e2) <= fabsf(tol) * fabsf(d3)) { e2 = 0.0f; continue; }
+            float mu = fabsf(d1);
+            smin = mu;
+            if (fabsf(e1) <= tol * mu) { e1 = 0.0f; continue; }
+            mu = fabsf(d2) * fdiv(mu, mu + fabsf(e1));
+            smin = fminf(smin, mu);
+            if (fabsf(e2) <= tol * mu) { e2 = 0.0f; continue; }
+            mu = fabsf(d3) * fdiv(mu, mu + fabsf(e2));
+            smin = fminf(smin, mu);
+        } else {
+            if (fabsf(e1) <= fabsf(tol) * fabsf(d1)) { e1 = 0.0f; continue; }
+            float mu = fabsf(d3);
+            smin = mu;
+            if (fabsf(e2) <= tol * mu) { e2 = 0.0f; continue; }
+            mu = fabsf(d2) * fdiv(mu, mu + fabsf(e2));
+            smin = fminf(smin, mu);
+            if (fabsf(e1) <= tol * mu) { e1 = 0.0f; continue; }
+            mu = fabsf(d1) * fdiv(mu, mu + fabsf(e1));
+            smin = fminf(smin, mu);
+        }
+        float shift;
+        if ((3.0f * tol) * fdiv(smin, smax) <= fmaxf(eps, 0.01f * tol)) shift = 0.0f;
+        else {
+            float sll;
+            if (idir == 1) { sll = fabsf(d1); shift = la_las2_min(d2, e2, d3); }
+            else { sll = fabsf(d3); shift = la_las2_min(d1, e1, d2); }
+            if (sll > 0.0f) { const float q = fdiv(shift, sll); if (q * q < eps) shift = 0.0f; }
+        }
+        iter += 2;
+        float c1, s1, c2, s2, oc1, os1, oc2, os2;   // rotations of the sweep (VT pair, U pair) at i = 1, 2
+        if (shift == 0.0f) {
+            float cs, sn, oldcs, oldsn, r, h;
+            if (idir == 1) {
+                la_lartg(d1, e1, cs, sn, r);                      // i = 1 (cs = 1)
+                la_lartg(r, d2 * sn, oldcs, oldsn, d1);           // oldcs = 1
+                c1 = cs; s1 = sn; oc1 = oldcs; os1 = oldsn;
+                la_lartg(d2 * cs, e2, cs, sn, r);                 // i = 2
+                e1 = oldsn * r;
+                la_lartg(oldcs * r, d3 * sn, oldcs, oldsn, d2);
+                c2 = cs; s2 = sn; oc2 = oldcs; os2 = oldsn;
+                h = d3 * cs; d3 = h * oldcs; e2 = h * oldsn;
+                vt_rot(z, 0, c1, s1); vt_rot(z, 1, c2, s2);
+                u_rot(z, 0, oc1, os1); u_rot(z, 1, oc2, os2);
+                if (fabsf(e2) <= thresh) e2 = 0.0f;
+            } else {
+                la_lartg(d3, e2, cs, sn, r);                      // i = 3
+                la_lartg(r, d2 * sn, oldcs, oldsn, d3);
+                c2 = cs; s2 = -sn; oc2 = oldcs; os2 = -oldsn;     // work(i - ll) = work(2)
+                la_lartg(d2 * cs, e1, cs, sn, r);                 // i = 2
+                e2 = oldsn * r;
+                la_lartg(oldcs * r, d1 * sn, oldcs, oldsn, d2);
+                c1 = cs; s1 = -sn; oc1 = oldcs; os1 = -oldsn;
+                h = d1 * cs; d1 = h * oldcs; e1 = h * oldsn;
+                vt_rot(z, 1, oc2, os2); vt_rot(z, 0, oc1, os1);   // SLASR('L','V','B') with work(nm12+1..)
+                u_rot(z, 1, c2, s2); u_rot(z, 0, c1, s1);         // SLASR('R','V','B') with work(1..)
+                if (fabsf(e1) <= thresh) e1 = 0.0f;
             }
-            S[p][qq] = 0.0;
-            S[qq][p] = 0.0;
-#pragma unroll
-            for (int k = 0; k < 3; ++k) {
-                const double vkp = Vm[k][p], vkq = Vm[k][qq];
-                Vm[k][p] = c * vkp - s * vkq;
-                Vm[k][qq] = s * vkp + c * vkq;
+        } else {
+            float f, g, r, cosr, sinr, cosl, sinl;
+            if (idir == 1) {
+                f = (fabsf(d1) - shift) * (__builtin_copysignf(1.0f, d1) + fdiv(shift, d1));
+                g = e1;
+                // i = 1
+                la_lartg(f, g, cosr, sinr, r);
+                f = cosr * d1 + sinr * e1;
+                e1 = cosr * e1 - sinr * d1;
+                g = sinr * d2;
+                d2 = cosr * d2;
+                la_lartg(f, g, cosl, sinl, r);
+                d1 = r;
+                f = cosl * e1 + sinl * d2;
+                d2 = cosl * d2 - sinl * e1;
+                g = sinl * e2;
+                e2 = cosl * e2;
+                c1 = cosr; s1 = sinr; oc1 = cosl; os1 = sinl;
+                // i = 2
+                la_lartg(f, g, cosr, sinr, r);
+                e1 = r;
+                f = cosr * d2 + sinr * e2;
+                e2 = cosr * e2 - sinr * d2;
+                g = sinr * d3;
+                d3 = cosr * d3;
+                la_lartg(f, g, cosl, sinl, r);
+                d2 = r;
+                f = cosl * e2 + sinl * d3;
+                d3 = cosl * d3 - sinl * e2;
+                c2 = cosr; s2 = sinr; oc2 = cosl; os2 = sinl;
+                e2 = f;
+                vt_rot(z, 0, c1, s1); vt_rot(z, 1, c2, s2);
+                u_rot(z, 0, oc1, os1); u_rot(z, 1, oc2, os2);
+                if (fabsf(e2) <= thresh) e2 = 0.0f;
+            } else {
+                f = (fabsf(d3) - shift) * (__builtin_copysignf(1.0f, d3) + fdiv(shift, d3));
+                g = e2;
+                // i = 3
+                la_lartg(f, g, cosr, sinr, r);
+                f = cosr * d3 + sinr * e2;
+                e2 = cosr * e2 - sinr * d3;
+                g = sinr * d2;
+                d2 = cosr * d2;
+                la_lartg(f, g, cosl, sinl, r);
+                d3 = r;
+                f = cosl * e2 + sinl * d2;
+                d2 = cosl * d2 - sinl * e2;
+                g = sinl * e1;
+                e1 = cosl * e1;
+                c2 = cosr; s2 = -sinr; oc2 = cosl; os2 = -sinl;
+                // i = 2
+                la_lartg(f, g, cosr, sinr, r);
+                e2 = r;
+                f = cosr * d2 + sinr * e1;
+                e1 = cosr * e1 - sinr * d2;
+                g = sinr * d1;
+                d1 = cosr * d1;
+                la_lartg(f, g, cosl, sinl, r);
+                d2 = r;
+                f = cosl * e1 + sinl * d1;
+                d1 = cosl * d1 - sinl * e1;
+                c1 = cosr; s1 = -sinr; oc1 = cosl; os1 = -sinl;
+                e1 = f;
+                if (fabsf(e1) <= thresh) e1 = 0.0f;
+                vt_rot(z, 1, oc2, os2); vt_rot(z, 0, oc1, os1);
+                u_rot(z, 1, c2, s2); u_rot(z, 0, c1, s1);
             }
         }
     }
+    // singular values made positive (VT rows negated), then sorted decreasing (SBDSQR :160-190)
+    if (d1 < 0.0f) { d1 = -d1; z.vt[0] = -z.vt[0]; z.vt[3] = -z.vt[3]; z.vt[6] = -z.vt[6]; }
+    if (d2 < 0.0f) { d2 = -d2; z.vt[1] = -z.vt[1]; z.vt[4] = -z.vt[4]; z.vt[7] = -z.vt[7]; }
+    if (d3 < 0.0f) { d3 = -d3; z.vt[2] = -z.vt[2]; z.vt[5] = -z.vt[5]; z.vt[8] = -z.vt[8]; }
+    // pass 1: smallest of (d1, d2, d3), ties to the later index, moves to position 3
+    {
+        int isub = 1;
+        float mn = d1;
+        if (d2 <= mn) { isub = 2; mn = d2; }
+        if (d3 <= mn) { isub = 3; mn = d3; }
+        if (isub == 1) {
+            d1 = d3; d3 = mn;
+#pragma unroll
+            for (int k = 0; k < 3; ++k) {
+                float t = z.vt[0 + 3 * k]; z.vt[0 + 3 * k] = z.vt[2 + 3 * k]; z.vt[2 + 3 * k] = t;
+                t = z.u[k]; z.u[k] = z.u[k + 6]; z.u[k + 6] = t;
+            }
+        } else if (isub == 2) {
+            d2 = d3; d3 = mn;
+#pragma unroll
+            for (int k = 0; k < 3; ++k) {
+                float t = z.vt[1 + 3 * k]; z.vt[1 + 3 * k] = z.vt[2 + 3 * k]; z.vt[2 + 3 * k] = t;
+                t = z.u[k + 3]; z.u[k + 3] = z.u[k + 6]; z.u[k + 6] = t;
+            }
+        }
+    }
+    // pass 2: smaller of (d1, d2), ties to d2, moves to position 2
+    if (!(d2 <= d1)) {
+        const float t0 = d1; d1 = d2; d2 = t0;
+#pragma unroll
+        for (int k = 0; k < 3; ++k) {
+            float t = z.vt[0 + 3 * k]; z.vt[0 + 3 * k] = z.vt[1 + 3 * k]; z.vt[1 + 3 * k] = t;
+            t = z.u[k]; z.u[k] = z.u[k + 3]; z.u[k + 3] = t;
+        }
+    }
 }
-
-RTG_DEV void kabsch_rot_jacobi(const float A[9], float R[9])
+// SGESDD(JOBZ='A') of a 3x3 (column-major a, overwritten): U and VT (column-major) in z
+RTG_DEV void la_gesdd3(float a[9], Svd3 &z)
 {
-    double a[3][3], S[3][3], Vm[3][3];
+    const float smlnum = 9.09494702e-13f, bignum = 1.0f / smlnum;   // sqrt(slamch('S')) / slamch('P') = 2^-40
+    float anrm = 0.0f;
 #pragma unroll
-    for (int i = 0; i < 3; ++i)
+    for (int i = 0; i < 9; ++i) anrm = fmaxf(anrm, fabsf(a[i]));
+    if (__builtin_expect((anrm > 0.0f && anrm < smlnum) || anrm > bignum, 0)) {
+        const float mul = anrm < smlnum ? fdiv(smlnum, anrm) : fdiv(bignum, anrm);
 #pragma unroll
-        for (int j = 0; j < 3; ++j) a[i][j] = (double)A[i * 3 + j];
-#pragma unroll
-    for (int i = 0; i < 3; ++i)
-#pragma unroll
-        for (int j = 0; j < 3; ++j) S[i][j] = a[0][i] * a[0][j] + a[1][i] * a[1][j] + a[2][i] * a[2][j];
-    jacobi_eig3(S, Vm);
-    // descending order of the eigenvalues (same selection as the oracle's sort),
-    // done on values so no array is indexed at run time
-    int o0 = 0, o1 = 1, o2 = 2, ti;
-    double a0 = S[0][0], a1 = S[1][1], a2 = S[2][2], td;
-    if (a1 > a0) { ti = o0; o0 = o1; o1 = ti; td = a0; a0 = a1; a1 = td; }
-    if (a2 > a0) { ti = o0; o0 = o2; o2 = ti; td = a0; a0 = a2; a2 = td; }
-    if (a2 > a1) { ti = o1; o1 = o2; o2 = ti; td = a1; a1 = a2; a2 = td; }
-    double v1[3], v2[3], u1[3], u2[3];
-#pragma unroll
-    for (int i = 0; i < 3; ++i) {
-        v1[i] = o0 == 0 ? Vm[i][0] : (o0 == 1 ? Vm[i][1] : Vm[i][2]);
-        v2[i] = o1 == 0 ? Vm[i][0] : (o1 == 1 ? Vm[i][1] : Vm[i][2]);
+        for (int i = 0; i < 9; ++i) a[i] *= mul;
     }
+    // SGEBD2, i = 0: H_0 from the left (v = (1, a1, a2)), G_0 from the right (v = (1, a6))
+    const float tq0 = la_larfg<2>(a[0], a[1], a[2]);
+    const float d1 = a[0];
+    if (tq0 != 0.0f) {
 #pragma unroll
-    for (int i = 0; i < 3; ++i) {
-        u1[i] = a[i][0] * v1[0] + a[i][1] * v1[1] + a[i][2] * v1[2];
-        u2[i] = a[i][0] * v2[0] + a[i][1] * v2[1] + a[i][2] * v2[2];
+        for (int j = 1; j < 3; ++j) {
+            const float w = a[3 * j] + (a[1 + 3 * j] * a[1] + a[2 + 3 * j] * a[2]);
+            const float tw = -(tq0 * w);
+            a[3 * j] = __builtin_fmaf(1.0f, tw, a[3 * j]);
+            a[1 + 3 * j] = __builtin_fmaf(a[1], tw, a[1 + 3 * j]);
+            a[2 + 3 * j] = __builtin_fmaf(a[2], tw, a[2 + 3 * j]);
+        }
     }
-    const double n1 = sqrt(u1[0] * u1[0] + u1[1] * u1[1] + u1[2] * u1[2]);
+    float dum = 0.0f;
+    const float tp0 = la_larfg<1>(a[3], a[6], dum);
+    const float e1 = a[3];
+    if (tp0 != 0.0f) {
+        const float tv1 = -(tp0 * 1.0f), tv2 = -(tp0 * a[6]);
 #pragma unroll
-    for (int i = 0; i < 3; ++i) u1[i] /= n1;
-    const double d = u1[0] * u2[0] + u1[1] * u2[1] + u1[2] * u2[2];
+        for (int r = 1; r < 3; ++r) {
+            const float w = __builtin_fmaf(a[r + 6], a[6], a[r + 3]);
+            a[r + 3] = __builtin_fmaf(w, tv1, a[r + 3]);
+            a[r + 6] = __builtin_fmaf(w, tv2, a[r + 6]);
+        }
+    }
+    // i = 1: H_1 from the left (v = (1, a5)) on column 2; G_1 = I (one-element reflector)
+    const float tq1 = la_larfg<1>(a[4], a[5], dum);
+    const float d2 = a[4];
+    if (tq1 != 0.0f) {
+        const float w = a[7] + a[8] * a[5];
+        const float tw = -(tq1 * w);
+        a[7] = __builtin_fmaf(1.0f, tw, a[7]);
+        a[8] = __builtin_fmaf(a[5], tw, a[8]);
+    }
+    const float e2 = a[7];
+    const float d3 = a[8];   // i = 2: H_2 = I
+    // SBDSDC('U','I') -> SLASDQ -> SBDSQR with U = VT = I
 #pragma unroll
-    for (int i = 0; i < 3; ++i) u2[i] -= d * u1[i];
-    const double n2 = sqrt(u2[0] * u2[0] + u2[1] * u2[1] + u2[2] * u2[2]);
+    for (int i = 0; i < 9; ++i) { z.u[i] = (i % 4 == 0) ? 1.0f : 0.0f; z.vt[i] = z.u[i]; }
+    float s1 = d1, s2 = d2, s3 = d3;
+    la_bdsqr3(s1, s2, s3, e1, e2, z);
+    // SORMBR('Q','L','N'): U := H_0 H_1 U (H_1 first), the unit row fused as fma(-tau, w, c)
+    if (tq1 != 0.0f) {
 #pragma unroll
-    for (int i = 0; i < 3; ++i) u2[i] /= n2;
-    const double u3[3] = {u1[1] * u2[2] - u1[2] * u2[1], u1[2] * u2[0] - u1[0] * u2[2],
-                          u1[0] * u2[1] - u1[1] * u2[0]};
-    const double v3[3] = {v1[1] * v2[2] - v1[2] * v2[1], v1[2] * v2[0] - v1[0] * v2[2],
-                          v1[0] * v2[1] - v1[1] * v2[0]};
+        for (int j = 0; j < 3; ++j) {
+            const float w = z.u[1 + 3 * j] + z.u[2 + 3 * j] * a[5];
+            const float tw = -(tq1 * w);
+            z.u[1 + 3 * j] = __builtin_fmaf(-tq1, w, z.u[1 + 3 * j]);
+            z.u[2 + 3 * j] = __builtin_fmaf(a[5], tw, z.u[2 + 3 * j]);
+        }
+    }
+    if (tq0 != 0.0f) {
 #pragma unroll
-    for (int i = 0; i < 3; ++i)
+        for (int j = 0; j < 3; ++j) {
+            const float w = z.u[3 * j] + (z.u[1 + 3 * j] * a[1] + z.u[2 + 3 * j] * a[2]);
+            const float tw = -(tq0 * w);
+            z.u[3 * j] = __builtin_fmaf(-tq0, w, z.u[3 * j]);
+            z.u[1 + 3 * j] = __builtin_fmaf(a[1], tw, z.u[1 + 3 * j]);
+            z.u[2 + 3 * j] = __builtin_fmaf(a[2], tw, z.u[2 + 3 * j]);
+        }
+    }
+    // SORMBR('P','R','T'): VT := VT G_0^T on columns 1..2
+    if (tp0 != 0.0f) {
+        const float tv1 = -(tp0 * 1.0f), tv2 = -(tp0 * a[6]);
 #pragma unroll
-        for (int j = 0; j < 3; ++j) R[i * 3 + j] = (float)(u1[i] * v1[j] + u2[i] * v2[j] + u3[i] * v3[j]);
+        for (int r = 0; r < 3; ++r) {
+            const float w = __builtin_fmaf(z.vt[r + 6], a[6], z.vt[r + 3]);
+            z.vt[r + 3] = __builtin_fmaf(w, tv1, z.vt[r + 3]);
+            z.vt[r + 6] = __builtin_fmaf(w, tv2, z.vt[r + 6]);
+        }
+    }
 }
-
-// 4x4 adjugate (and determinant) by 2x2 sub-determinants; m row-major
-RTG_DEV double adj4(const double m[16], double inv[16], bool want_adj)
-{
-    const double s0 = m[0] * m[5] - m[4] * m[1], s1 = m[0] * m[6] - m[4] * m[2];
-    const double s2 = m[0] * m[7] - m[4] * m[3], s3 = m[1] * m[6] - m[5] * m[2];
-    const double s4 = m[1] * m[7] - m[5] * m[3], s5 = m[2] * m[7] - m[6] * m[3];
-    const double c5 = m[10] * m[15] - m[14] * m[11], c4 = m[9] * m[15] - m[13] * m[11];
-    const double c3 = m[9] * m[14] - m[13] * m[10], c2 = m[8] * m[15] - m[12] * m[11];
-    const double c1 = m[8] * m[14] - m[12] * m[10], c0 = m[8] * m[13] - m[12] * m[9];
-    if (want_adj) {
-        inv[0] = m[5] * c5 - m[6] * c4 + m[7] * c3;
-        inv[1] = -m[1] * c5 + m[2] * c4 - m[3] * c3;
-        inv[2] = m[13] * s5 - m[14] * s4 + m[15] * s3;
-        inv[3] = -m[9] * s5 + m[10] * s4 - m[11] * s3;
-        inv[4] = -m[4] * c5 + m[6] * c2 - m[7] * c1;
-        inv[5] = m[0] * c5 - m[2] * c2 + m[3] * c1;
-        inv[6] = -m[12] * s5 + m[14] * s2 - m[15] * s1;
-        inv[7] = m[8] * s5 - m[10] * s2 + m[11] * s1;
-        inv[8] = m[4] * c4 - m[5] * c2 + m[7] * c0;
-        inv[9] = -m[0] * c4 + m[1] * c2 - m[3] * c0;
-        inv[10] = m[12] * s4 - m[13] * s2 + m[15] * s0;
-        inv[11] = -m[8] * s4 + m[9] * s2 - m[11] * s0;
-        inv[12] = -m[4] * c3 + m[5] * c1 - m[6] * c0;
-        inv[13] = m[0] * c3 - m[1] * c1 + m[2] * c0;
-        inv[14] = -m[12] * s3 + m[13] * s1 - m[14] * s0;
-        inv[15] = m[8] * s3 - m[9] * s1 + m[10] * s0;
-    }
-    return s0 * c5 - s1 * c4 + s2 * c3 + s3 * c2 - s4 * c1 + s5 * c0;
-}
-
-// Kabsch rotation, fast path: Horn's quaternion form of the same problem
-// (max tr(R^T A) over proper rotations == the det-fixed SVD solution).  The
-// largest eigenvalue of the 4x4 key matrix N of S = A^T comes from Newton on
-// its characteristic quartic started above the root at sqrt(3)|S|_F (QCP);
-// the quaternion is the largest-diagonal column of adj(N - lambda I).  A
-// (nearly) degenerate top eigenvalue -- a reflection fit with sigma2 ~ sigma3,
-// ill-posed for any method -- falls back to the Jacobi polar factor.
+// transform3d.py:40-45: R = U Vt ((p0 + p1) + p2, torch's bmm order); det(R) < 0 -> Vt[-1,:] *= -1; R = U Vt.
+// A and R row-major.  det only decides a sign (|det| = 1 up to rounding), taken in float64.
 RTG_DEV void kabsch_rot(const float A[9], float R[9])
 {
-    const double Sxx = A[0], Sxy = A[3], Sxz = A[6], Syx = A[1], Syy = A[4], Syz = A[7], Szx = A[2], Szy = A[5],
-                 Szz = A[8];
-    const double F2 = Sxx * Sxx + Sxy * Sxy + Sxz * Sxz + Syx * Syx + Syy * Syy + Syz * Syz + Szx * Szx +
-                      Szy * Szy + Szz * Szz;
-    if (F2 == 0.0) {   // all-zero fit: the reference's SVD gives U = V = I
+    float a[9];
 #pragma unroll
-        for (int i = 0; i < 9; ++i) R[i] = (i % 4 == 0) ? 1.0f : 0.0f;
-        return;
-    }
-    double N[16] = {Sxx + Syy + Szz, Syz - Szy, Szx - Sxz, Sxy - Syx,
-                    Syz - Szy, Sxx - Syy - Szz, Sxy + Syx, Szx + Sxz,
-                    Szx - Sxz, Sxy + Syx, -Sxx + Syy - Szz, Syz + Szy,
-                    Sxy - Syx, Szx + Sxz, Syz + Szy, -Sxx - Syy + Szz};
-    const double detS = Sxx * (Syy * Szz - Syz * Szy) - Sxy * (Syx * Szz - Syz * Szx) + Sxz * (Syx * Szy - Syy * Szx);
-    double scratch[16];
-    const double c0 = adj4(N, scratch, false);
-    const double c2 = -2.0 * F2, c1 = -8.0 * detS;
-    double lam = sqrt(3.0 * F2);
-    int it = 0;
-    for (; it < 50; ++it) {
-        const double P = ((lam * lam + c2) * lam + c1) * lam + c0;
-        const double dP = (4.0 * lam * lam + 2.0 * c2) * lam + c1;
-        // the step only has to be near P/dP: v_rcp_f64's estimate keeps Newton's convergence (each step's error
-        // shrinks by the estimate's ~2^-26 on top of the quadratic term) at a tenth of the IEEE divide's cost
-        const double d = P * __builtin_amdgcn_rcp(dP);
-        lam -= d;
-        if (fabs(d) <= 1e-13 * fabs(lam)) break;
-    }
+    for (int i = 0; i < 3; ++i)
 #pragma unroll
-    for (int i = 0; i < 4; ++i) N[i * 5] -= lam;
-    double adj[16];
-    adj4(N, adj, true);
-    int k = 0;
-    double best = fabs(adj[0]);
-    if (fabs(adj[5]) > best) { best = fabs(adj[5]); k = 1; }
-    if (fabs(adj[10]) > best) { best = fabs(adj[10]); k = 2; }
-    if (fabs(adj[15]) > best) { best = fabs(adj[15]); k = 3; }
-    if (it >= 16 || best * best <= 1e-12 * F2 * F2 * F2) {   // best <= 1e-6 |S|_F^3, without the sqrt
-        kabsch_rot_jacobi(A, R);
-        return;
-    }
-    double q[4];
+        for (int k = 0; k < 3; ++k) a[i + 3 * k] = A[i * 3 + k];
+    Svd3 z;
+    la_gesdd3(a, z);
 #pragma unroll
-    for (int r = 0; r < 4; ++r)
-        q[r] = k == 0 ? adj[r * 4] : (k == 1 ? adj[r * 4 + 1] : (k == 2 ? adj[r * 4 + 2] : adj[r * 4 + 3]));
-    // R(q) of the unnormalised column: R = I + s [..] with s = 2 / |q|^2 (one divide instead of sqrt + 4 divides)
-    const double w = q[0], x = q[1], y = q[2], z = q[3];
-    const double s = 2.0 / (w * w + x * x + y * y + z * z);
-    R[0] = (float)(1.0 - s * (y * y + z * z));
-    R[1] = (float)(s * (x * y - w * z));
-    R[2] = (float)(s * (x * z + w * y));
-    R[3] = (float)(s * (x * y + w * z));
-    R[4] = (float)(1.0 - s * (x * x + z * z));
-    R[5] = (float)(s * (y * z - w * x));
-    R[6] = (float)(s * (x * z - w * y));
-    R[7] = (float)(s * (y * z + w * x));
-    R[8] = (float)(1.0 - s * (x * x + y * y));
+    for (int i = 0; i < 3; ++i)
+#pragma unroll
+        for (int k = 0; k < 3; ++k)
+            R[i * 3 + k] = (z.u[i] * z.vt[3 * k] + z.u[i + 3] * z.vt[1 + 3 * k]) + z.u[i + 6] * z.vt[2 + 3 * k];
+    const double det = (double)R[0] * ((double)R[4] * R[8] - (double)R[5] * R[7]) -
+                       (double)R[1] * ((double)R[3] * R[8] - (double)R[5] * R[6]) +
+                       (double)R[2] * ((double)R[3] * R[7] - (double)R[4] * R[6]);
+    if (det < 0.0) {
+#pragma unroll
+        for (int k = 0; k < 3; ++k) z.vt[2 + 3 * k] = -z.vt[2 + 3 * k];
+#pragma unroll
+        for (int i = 0; i < 3; ++i)
+#pragma unroll
+            for (int k = 0; k < 3; ++k)
+                R[i * 3 + k] = (z.u[i] * z.vt[3 * k] + z.u[i + 3] * z.vt[1 + 3 * k]) + z.u[i + 6] * z.vt[2 + 3 * k];
+    }
 }
 
 // cal_joint_quat (transform3d.py:31-50): A = M^T Z by einsum (sequential in j, no FMA)

@@ -235,10 +235,29 @@ def cal_joint_quat(Z, M):
 
 
 def kabsch_rotmat(A):
+    """transform3d.py:40-45 as the reference computes it: MKL sgesdd restated (the oracle's Kabsch)."""
+    A = _c32(np.reshape(A, (-1, 9)))
+    out = np.empty_like(A)
+    lib().oracle_kabsch_rotmat_sgesdd(_fp(A), _i64(len(A)), _fp(out))
+    return out.reshape(-1, 3, 3)
+
+
+def kabsch_rotmat_polar(A):
+    """Cross-check: the exact proper-rotation polar factor in float64 (round-1 oracle), rounded to f32."""
     A = _c32(np.reshape(A, (-1, 9)))
     out = np.empty_like(A)
     lib().oracle_kabsch_rotmat(_fp(A), _i64(len(A)), _fp(out))
     return out.reshape(-1, 3, 3)
+
+
+def sgesdd3(A):
+    """torch.linalg.svd of (n,3,3) float32 as MKL 2024.2 sgesdd computes it -> (U, S, Vt), row-major."""
+    A = _c32(np.reshape(A, (-1, 9)))
+    n = len(A)
+    U, S, Vt = np.empty((n, 3, 3), np.float32), np.empty((n, 3), np.float32), np.empty((n, 3, 3), np.float32)
+    info = lib().oracle_sgesdd3(_fp(A), _i64(n), _fp(U), _fp(S), _fp(Vt))
+    assert info == 0, "sbdsqr did not converge"
+    return U, S, Vt
 
 
 def kabsch_rotmat_horn(A):

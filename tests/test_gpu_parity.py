@@ -303,13 +303,14 @@ def _dev(*arrs):
     return [torch.from_numpy(np.ascontiguousarray(a)).cuda() for a in arrs]
 
 
-# reference-vs-port bounds (same numbers the oracle meets in test_oracle_golden.py)
+# reference-vs-port bounds: the measured residual + 10 % (the numbers the oracle meets in test_oracle_golden.py;
+# what is left is MKL VML's acos/sin/cos/sqrt rounding, test_oracle_golden.py::test_vml_attribution)
 GOLD_BOUNDS = {
-    "full_body_pos_precise": dict(max=2e-3, p99=2e-4, frac=0.25),
-    "full_body_pos_binary": dict(max=2e-3, p99=2e-4, frac=0.25),
-    "upper_body": dict(max=2e-3, p99=2e-4, frac=0.25),
-    "full_body_rot": dict(max=2e-4, p99=2e-5, frac=0.03),
-    "body_rot": dict(max=1e-6, p99=1e-6, frac=0.0),
+    "full_body_pos_precise": dict(max=2.4e-5, p99=6.1e-6, frac=0.0086),
+    "full_body_pos_binary": dict(max=4.0e-5, p99=4.5e-6, frac=0.0086),
+    "upper_body": dict(max=9.5e-5, p99=1.3e-5, frac=0.0151),
+    "full_body_rot": dict(max=3.6e-5, p99=8.4e-6, frac=0.0086),
+    "body_rot": dict(max=1.4e-7, p99=1.4e-7, frac=0.0),
 }
 
 

@@ -4,7 +4,9 @@ Golden vectors were produced by running the reference in the build container
 (tools/make_golden.py).  Where the reference path is reproducible op for op
 (FK, inverse FK, quaternion algebra, glibc atan2f, scipy Euler) the oracle is
 bit-exact.  The reference's MKL VML transcendentals and MKL sgesdd are closed
-source; there the bounds below are the measured residual."""
+source.  MKL's sgesdd (the Kabsch SVD) is restated routine by routine and is bit-exact with
+torch.linalg.svd (test_sgesdd_restatement_bit_exact); the VML transcendentals are not, and the bounds below
+are the measured residual, with test_vml_attribution showing VML is all that is left."""
 import os
 
 import numpy as np
@@ -108,20 +110,73 @@ def test_transcendental_primitives_within_mkl_ulps():
 
 
 def test_kabsch_within_reference_noise():
-    """MKL sgesdd vs float64 polar factor: R agrees to ~1e-7, the reference's own
-    quat_from_rotation_matrix amplifies that for small quaternion components."""
+    """cal_joint_quat with the restated sgesdd: R bit-exact, quat_from_rotation_matrix then differs from the
+    reference only by VML's sqrt (torch.sqrt / pow(0.5) is vmsSqrt, -1 ulp on ~0.5 % of inputs): <= 1 ulp."""
     p = golden("primitives")
     for n in (3, 5):
         s = frame_stats(orc.cal_joint_quat(p[f"cjq{n}_Z"], p[f"cjq{n}_M"]), p[f"cal_joint_quat{n}"])
-        assert s["max"] <= 2e-4 and s["p99_frame"] <= 5e-5, s
+        assert s["max"] <= 6e-8 and s["exact_elems"] >= 0.98, s
 
 
-BOUNDS = {  # measured residual, see DESIGN.md §3 (max, p99 of per-frame max, frac frames > 1e-5)
-    "full_body_pos_precise": (2e-3, 2e-4, 0.25),
-    "full_body_pos_binary": (2e-3, 2e-4, 0.25),
-    "upper_body": (2e-3, 2e-4, 0.25),
-    "full_body_rot": (2e-4, 2e-5, 0.03),
-    "body_rot": (1e-6, 1e-6, 0.0),
+def test_sgesdd_restatement_bit_exact():
+    """torch.linalg.svd of a (1,3,3) float32 matrix is MKL 2024.2 sgesdd(JOBZ='A'); the oracle's restatement
+    (rtg_oracle.c la_gesdd3: SGEBD2 -> SBDSQR -> SORMBR with MKL's measured FMA placement) reproduces U, S
+    and Vt bit for bit on the 1024 seeded matrices tools/mkl_svd_probe.py recorded in this container."""
+    g = golden("mkl_svd_probe")
+    U, S, Vt = orc.sgesdd3(g["A"])
+    ours = np.concatenate([U.reshape(-1, 9), S, Vt.reshape(-1, 9)], 1)
+    np.testing.assert_array_equal(ours, g["usv"])
+
+
+def test_kabsch_sgesdd_vs_polar_factor():
+    """The reference's Kabsch (sgesdd in f32) against the exact proper-rotation polar factor (f64): the two
+    agree to a few f32 ulps on well-conditioned fits -- the size of what the round-1 oracle left on the table."""
+    rng = np.random.default_rng(3)
+    A = np.einsum("bji,bjk->bik", rng.standard_normal((4096, 5, 3)), rng.standard_normal((4096, 5, 3))).astype(np.float32)
+    d = np.abs(orc.kabsch_rotmat(A) - orc.kabsch_rotmat_polar(A)).reshape(len(A), -1).max(1)
+    assert np.median(d) <= 3e-7 and np.mean(d <= 1e-5) >= 0.99, (np.median(d), d.max())
+
+
+def _torch_vml():
+    """MKL VML entry points torch itself calls for acos / sin / cos (VML_HA), or None."""
+    import ctypes
+    try:
+        import torch
+        L = ctypes.CDLL(os.path.join(os.path.dirname(torch.__file__), "lib", "libtorch_cpu.so"))
+        return [ctypes.cast(getattr(L, f), ctypes.c_void_p) for f in ("vmsAcos", "vmsSin", "vmsCos")]
+    except (OSError, AttributeError, ImportError):
+        return None
+
+
+def test_vml_attribution():
+    """Attribution of the remaining residual: with torch's own VML acos/sin/cos routed into the oracle (a
+    test-only hook), every solver moves to (near) bit-equality with the reference -- what is left after the
+    sgesdd restatement is MKL VML's rounding, which no restatement of the published algorithm can reproduce.
+    VML's bits depend on the host CPU's dispatch; the numbers were measured on the build container's AVX-512
+    Xeon, where the goldens were made."""
+    import ctypes
+    fns = _torch_vml()
+    if fns is None or "avx512f" not in open("/proc/cpuinfo").read():
+        pytest.skip("torch's VML or an AVX-512 host (the goldens' ISA) is not available")
+    lib = orc.lib()
+    lib.oracle_set_vml(*fns, ctypes.c_longlong(0x140102))   # VML_HA | VML_FTZDAZ_OFF | VML_ERRMODE_IGNORE
+    try:
+        stats = {}
+        for name in BOUNDS:
+            dof, d = _run(name)
+            stats[name] = frame_stats(dof, d["dof"])
+    finally:
+        lib.oracle_set_vml(None, None, None, ctypes.c_longlong(0))
+    for name, s in stats.items():
+        assert s["exact_elems"] >= 0.98 and s["frac_frames_gt_1e5"] <= 0.008 and s["p99_frame"] <= 2e-6, (name, s)
+
+
+BOUNDS = {  # measured residual + 10 % (DESIGN.md §2): max, p99 of per-frame max, frac frames > 1e-5
+    "full_body_pos_precise": (2.4e-5, 6.1e-6, 0.0086),
+    "full_body_pos_binary": (4.0e-5, 4.5e-6, 0.0086),
+    "upper_body": (9.5e-5, 1.3e-5, 0.0151),
+    "full_body_rot": (3.6e-5, 8.4e-6, 0.0086),
+    "body_rot": (1.4e-7, 1.4e-7, 0.0),
 }
 
 
@@ -154,14 +209,15 @@ def test_solver_residual_within_reference_cross_isa_spread(name):
     reference's own DOFs on the same inputs with MKL forced to AVX2 and to
     SSE4_2 (tools/ref_isa_spread.py); the goldens are the AVX-512 run.  The
     oracle's residual against the goldens must sit within 1.3x of the
-    reference-vs-reference spread (max, p99 per-frame max, frames > 1e-5)."""
+    reference-vs-reference spread (max, p99 per-frame max, frames > 1e-5) -- with the sgesdd restatement
+    it sits at or below it."""
     dof, d = _run(name)
     ours = frame_stats(dof, d["dof"])
     spread = golden("ref_isa_spread")
     floor = {k: max(frame_stats(spread[f"{name}_{isa}"], d["dof"])[k] for isa in spread["isas"])
              for k in ("max", "p99_frame", "frac_frames_gt_1e5")}
     for k, v in floor.items():
-        assert ours[k] <= 1.3 * v, (k, ours, floor)
+        assert ours[k] <= v, (k, ours, floor)
 
 
 def test_full_body_pos_with_reference_kabsch_injected():
@@ -266,7 +322,7 @@ def test_motion_prep_vs_reference():
     """retarget/main.py prep, pinned to the reference's own functions:
     coord_transform + rescale_motion_to_standard_size bit-exact; quat_between_two_vecs bit-exact (incl. the
     batch-level identity branch); _rebuild_with_vtrdyn_zero_pose's rotations bit-exact except the two Kabsch
-    rows (0, 10: MKL sgesdd, the residual bound of the solvers)."""
+    rows (0, 10), which are within VML sqrt's ulp (sgesdd itself is restated exactly)."""
     from rtg import assets
     d = golden("motion_prep")
     par, zl = assets.parents("vtrdyn"), golden("zero_pose")["vtrdyn_local_t"]
@@ -279,4 +335,4 @@ def test_motion_prep_vs_reference():
     other = [j for j in range(21) if j not in (0, 10)]
     np.testing.assert_array_equal(gr[:, other], d["g_rot"][:, other])
     e = np.abs(gr[:, [0, 10]] - d["g_rot"][:, [0, 10]]).reshape(len(gr), -1).max(1)   # per-frame max
-    assert e.max() <= 5e-4 and np.median(e) <= 5e-6 and (e > 1e-5).mean() <= 0.2, (e.max(), np.median(e))
+    assert e.max() <= 6e-8 and (gr[:, [0, 10]] == d["g_rot"][:, [0, 10]]).mean() >= 0.99, e.max()
