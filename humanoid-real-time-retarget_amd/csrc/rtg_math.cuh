@@ -444,14 +444,35 @@ RTG_DEV float radians_between_axes(V v1, V v2, V n)
 // by stage against MKL's own entry points (tools/mkl_sgesdd_probe.py) and matches bit for bit.  The
 // oracle (oracle/rtg_oracle.c, la_gesdd3) restates the same routines independently.  All divisions / square
 // roots are IEEE-exact (fdiv = one rcp64 + mulr, cr_sqrt).  Matrices are column-major: a[r + 3 c].
-RTG_DEV float fdiv(float a, float b) { return mulr(a, rcp64(b)); }
+#ifndef RTG_SVD_DIV
+#define RTG_SVD_DIV 1   // 1: the compiler's IEEE f32 division sequence (measured +6 %); 0: rcp64 + mulr
+#endif
+#ifndef RTG_SVD_SQRT
+#define RTG_SVD_SQRT 0  // 0: cr_sqrt (v_sqrt_f64 + Newton); 1: the compiler's IEEE f32 sqrt sequence
+#endif
+RTG_DEV float fdiv(float a, float b)
+{
+#if RTG_SVD_DIV
+    return a / b;
+#else
+    return mulr(a, rcp64(b));
+#endif
+}
+RTG_DEV float la_sqrt(float x)
+{
+#if RTG_SVD_SQRT
+    return __builtin_sqrtf(x);
+#else
+    return cr_sqrt(x);
+#endif
+}
 RTG_DEV float la_sign(float a, float b) { return __builtin_copysignf(fabsf(a), b); }   // Fortran SIGN
 RTG_DEV float la_lapy2(float x, float y)                                                 // SLAPY2
 {
     const float xa = fabsf(x), ya = fabsf(y);
     const float w = fmaxf(xa, ya), z = fminf(xa, ya);
     const float r = fdiv(z, w);
-    return z == 0.0f ? w : w * cr_sqrt(1.0f + r * r);
+    return z == 0.0f ? w : w * la_sqrt(1.0f + r * r);
 }
 // SLARFG(n, alpha, x): n = 3 (x = x0, x1) or n = 2 (x = x0); returns tau, updates alpha (= beta) and x
 template <int NX>
@@ -489,14 +510,14 @@ RTG_DEV void la_lartg(float f, float g, float &c, float &s, float &r)   // SLART
     if (g == 0.0f) { c = 1.0f; s = 0.0f; r = f; }
     else if (f == 0.0f) { c = 0.0f; s = __builtin_copysignf(1.0f, g); r = g1; }
     else if (f1 > rtmin && f1 < rtmax && g1 > rtmin && g1 < rtmax) {
-        const float d = cr_sqrt(f * f + g * g);
+        const float d = la_sqrt(f * f + g * g);
         const Rcp rd = rcp64(d);
         c = mulr(f1, rd);
         r = __builtin_copysignf(d, f);
         s = f < 0.0f ? -mulr(g, rd) : mulr(g, rd);   // g / r with r = +-d (RN is sign-symmetric)
     } else {
         const float u = fminf(safmax, fmaxf(safmin, fmaxf(f1, g1)));
-        const float fs = fdiv(f, u), gs = fdiv(g, u), d = cr_sqrt(fs * fs + gs * gs);
+        const float fs = fdiv(f, u), gs = fdiv(g, u), d = la_sqrt(fs * fs + gs * gs);
         c = fdiv(fabsf(fs), d);
         r = __builtin_copysignf(d, f);
         s = fdiv(gs, r);
@@ -512,13 +533,13 @@ RTG_DEV float la_las2_min(float f, float g, float h)   // SLAS2, SSMIN only (the
         const float as = 1.0f + fdiv(fhmn, fhmx), at = fdiv(fhmx - fhmn, fhmx);
         float au = fdiv(ga, fhmx);
         au = au * au;
-        const float c = fdiv(2.0f, cr_sqrt(as * as + au) + cr_sqrt(at * at + au));
+        const float c = fdiv(2.0f, la_sqrt(as * as + au) + la_sqrt(at * at + au));
         return fhmn * c;
     }
     const float au = fdiv(fhmx, ga);
     if (au == 0.0f) return fdiv(fhmn * fhmx, ga);
     const float as = 1.0f + fdiv(fhmn, fhmx), at = fdiv(fhmx - fhmn, fhmx), p = as * au, q = at * au;
-    const float c = fdiv(1.0f, cr_sqrt(1.0f + p * p) + cr_sqrt(1.0f + q * q));
+    const float c = fdiv(1.0f, la_sqrt(1.0f + p * p) + la_sqrt(1.0f + q * q));
     const float mn = (fhmn * c) * au;
     return mn + mn;
 }
@@ -550,14 +571,14 @@ RTG_DEV void la_lasv2(float f, float g, float h, float &ssmin, float &ssmax, flo
             const float m = fdiv(gt, ft), mm = m * m;
             float t = 2.0f - l;
             const float tt = t * t;
-            const float s = cr_sqrt(tt + mm);
-            const float r = l == 0.0f ? fabsf(m) : cr_sqrt(l * l + mm);
+            const float s = la_sqrt(tt + mm);
+            const float r = l == 0.0f ? fabsf(m) : la_sqrt(l * l + mm);
             const float a = 0.5f * (s + r);
             ssmin = fdiv(ha, a);
             ssmax = fa * a;
             if (mm == 0.0f) t = l == 0.0f ? la_sign(2.0f, ft) * la_sign(1.0f, gt) : fdiv(gt, la_sign(d, ft)) + fdiv(m, t);
             else t = (fdiv(m, s + t) + fdiv(m, r + l)) * (1.0f + a);
-            const float l2 = cr_sqrt(t * t + 4.0f);
+            const float l2 = la_sqrt(t * t + 4.0f);
             const Rcp rl = rcp64(l2);
             crt = mulr(2.0f, rl);
             srt = mulr(t, rl);
@@ -581,29 +602,34 @@ RTG_DEV void la_rot(float &x, float &y, float c, float s)   // MKL's SROT / SLAS
     y = __builtin_fmaf(c, yv, -(s * xv));
 }
 struct Svd3 { float u[9], vt[9]; };
-// rotate VT rows (r, r+1) / U columns (r, r+1), r in {0, 1} (runtime)
-RTG_DEV void vt_rot(Svd3 &z, int r, float c, float s)
+// rotate VT rows (p, p+1) / U columns (p, p+1), p = p1 ? 1 : 0 chosen per lane by selects (no divergence)
+RTG_DEV void vt_rot(Svd3 &z, bool p1, float c, float s)
 {
-    if (r == 0) {
 #pragma unroll
-        for (int k = 0; k < 3; ++k) la_rot(z.vt[0 + 3 * k], z.vt[1 + 3 * k], c, s);
-    } else {
-#pragma unroll
-        for (int k = 0; k < 3; ++k) la_rot(z.vt[1 + 3 * k], z.vt[2 + 3 * k], c, s);
+    for (int k = 0; k < 3; ++k) {
+        float x = p1 ? z.vt[1 + 3 * k] : z.vt[3 * k], y = p1 ? z.vt[2 + 3 * k] : z.vt[1 + 3 * k];
+        la_rot(x, y, c, s);
+        z.vt[3 * k] = p1 ? z.vt[3 * k] : x;
+        z.vt[1 + 3 * k] = p1 ? x : y;
+        z.vt[2 + 3 * k] = p1 ? y : z.vt[2 + 3 * k];
     }
 }
-RTG_DEV void u_rot(Svd3 &z, int r, float c, float s)
+RTG_DEV void u_rot(Svd3 &z, bool p1, float c, float s)
 {
-    if (r == 0) {
 #pragma unroll
-        for (int k = 0; k < 3; ++k) la_rot(z.u[k], z.u[k + 3], c, s);
-    } else {
-#pragma unroll
-        for (int k = 0; k < 3; ++k) la_rot(z.u[k + 3], z.u[k + 6], c, s);
+    for (int k = 0; k < 3; ++k) {
+        float x = p1 ? z.u[k + 3] : z.u[k], y = p1 ? z.u[k + 6] : z.u[k + 3];
+        la_rot(x, y, c, s);
+        z.u[k] = p1 ? z.u[k] : x;
+        z.u[k + 3] = p1 ? x : y;
+        z.u[k + 6] = p1 ? y : z.u[k + 6];
     }
 }
 // SBDSQR('U', 3, ncvt = 3, nru = 3, ncc = 0) from U = VT = I (SBDSDC / SLASDQ), n = 3 specialised: the only
-// multi-element block is (ll, m) = (1, 3), every other case is a 2x2 SLASV2 block.
+// multi-element block is (ll, m) = (1, 3); every other case ends in one 2x2 SLASV2 block.  A bottom-to-top
+// chase (IDIR = 2) is the top-to-bottom chase (IDIR = 1) of the reversed bidiagonal (d3, d2, d1; e2, e1) -- the
+// same scalar recurrences, with the rotations applied to the mirrored row / column pairs and negated sines
+// (SBDSQR :130/:150 store -SN) -- so both directions run one code path and a wave never executes both.
 RTG_DEV void la_bdsqr3(float &d1, float &d2, float &d3, float e1, float e2, Svd3 &z)
 {
     const float eps = 5.96046448e-08f, tol = 10.0f * eps, unfl = 1.17549435e-38f;
@@ -618,160 +644,108 @@ RTG_DEV void la_bdsqr3(float &d1, float &d2, float &d3, float e1, float e2, Svd3
     }
     sminoa = fdiv(sminoa, 1.73205078f);   // / sqrt(real(3))
     const float thresh = fmaxf(tol * sminoa, 6.0f * (3.0f * (3.0f * unfl)));
-    int m = 3, iter = -1, iterdivn = 0, idir = 0;
-    bool fresh = true;   // (ll, m) = (1, 3) differs from (oldll, oldm)
+    int m = 3, iter = -1, iterdivn = 0;
+    bool mir = false, fresh = true;   // mir: IDIR = 2; fresh: (ll, m) = (1, 3) differs from (oldll, oldm)
     for (;;) {
         if (m <= 1) break;
         if (iter >= 3) { iter -= 3; if (++iterdivn >= 18) break; }   // no convergence: INFO > 0 (never seen)
+        bool blk = false, p1 = false;
         if (m == 2) {                       // block (1, 2)
-            if (fabsf(e1) <= thresh) { e1 = 0.0f; break; }
-            float sigmn, sigmx, sinr, cosr, sinl, cosl;
-            la_lasv2(d1, e1, d2, sigmn, sigmx, sinr, cosr, sinl, cosl);
-            d1 = sigmx; e1 = 0.0f; d2 = sigmn;
-            vt_rot(z, 0, cosr, sinr);
-            u_rot(z, 0, cosl, sinl);
-            break;
-        }
-        // m == 3
-        if (fabsf(e2) <= thresh) { e2 = 0.0f; m = 2; continue; }
-        const float smax = fmaxf(fmaxf(fabsf(d3), fmaxf(fabsf(d2), fabsf(e2))), fmaxf(fabsf(d1), fabsf(e1)));
-        if (fabsf(e1) <= thresh) {          // split at E(1): block (2, 3)
-            e1 = 0.0f;
-            float sigmn, sigmx, sinr, cosr, sinl, cosl;
-            la_lasv2(d2, e2, d3, sigmn, sigmx, sinr, cosr, sinl, cosl);
-            d2 = sigmx; e2 = 0.0f; d3 = sigmn;
-            vt_rot(z, 1, cosr, sinr);
-            u_rot(z, 1, cosl, sinl);
-            break;
-        }
-        if (fresh) { idir = fabsf(d1) >= fabsf(d3) ? 1 : 2; fresh = false; }
-        float smin;
-        if (idir == 1) {
-            if (fabsf(e2) <= fabsf(tol) * fabsf(d3)) { e2 = 0.0f; continue; }
-            float mu = fabsf(d1);
-            smin = mu;
-            if (fabsf(e1) <= tol * mu) { e1 = 0.0f; continue; }
-            mu = fabsf(d2) * fdiv(mu, mu + fabsf(e1));
-            smin = fminf(smin, mu);
-            if (fabsf(e2) <= tol * mu) { e2 = 0.0f; continue; }
-            mu = fabsf(d3) * fdiv(mu, mu + fabsf(e2));
-            smin = fminf(smin, mu);
+            if (fabsf(e1) <= thresh) break;
+            blk = true;
         } else {
-            if (fabsf(e1) <= fabsf(tol) * fabsf(d1)) { e1 = 0.0f; continue; }
-            float mu = fabsf(d3);
-            smin = mu;
-            if (fabsf(e2) <= tol * mu) { e2 = 0.0f; continue; }
-            mu = fabsf(d2) * fdiv(mu, mu + fabsf(e2));
-            smin = fminf(smin, mu);
-            if (fabsf(e1) <= tol * mu) { e1 = 0.0f; continue; }
-            mu = fabsf(d1) * fdiv(mu, mu + fabsf(e1));
-            smin = fminf(smin, mu);
+            if (fabsf(e2) <= thresh) { e2 = 0.0f; m = 2; continue; }
+            if (fabsf(e1) <= thresh) { e1 = 0.0f; blk = true; p1 = true; }   // split at E(1): block (2, 3)
         }
-        float shift;
-        if ((3.0f * tol) * fdiv(smin, smax) <= fmaxf(eps, 0.01f * tol)) shift = 0.0f;
+        if (blk) {   // 2x2 block (p1 ? 2 : 1, +1)
+            float sigmn, sigmx, sinr, cosr, sinl, cosl;
+            la_lasv2(p1 ? d2 : d1, p1 ? e2 : e1, p1 ? d3 : d2, sigmn, sigmx, sinr, cosr, sinl, cosl);
+            d1 = p1 ? d1 : sigmx;
+            d2 = p1 ? sigmx : sigmn;
+            d3 = p1 ? sigmn : d3;
+            vt_rot(z, p1, cosr, sinr);
+            u_rot(z, p1, cosl, sinl);
+            break;
+        }
+        const float smax = fmaxf(fmaxf(fabsf(d3), fmaxf(fabsf(d2), fabsf(e2))), fmaxf(fabsf(d1), fabsf(e1)));
+        if (fresh) { mir = !(fabsf(d1) >= fabsf(d3)); fresh = false; }
+        // the IDIR = 1 form on (D1, D2, D3; E1, E2) = mir ? (d3, d2, d1; e2, e1) : (d1, d2, d3; e1, e2)
+        float D1 = mir ? d3 : d1, D2 = d2, D3 = mir ? d1 : d3, E1 = mir ? e2 : e1, E2 = mir ? e1 : e2;
+        bool zeroed = false;
+        float smin;
+        if (fabsf(E2) <= fabsf(tol) * fabsf(D3)) { E2 = 0.0f; zeroed = true; }
         else {
-            float sll;
-            if (idir == 1) { sll = fabsf(d1); shift = la_las2_min(d2, e2, d3); }
-            else { sll = fabsf(d3); shift = la_las2_min(d1, e1, d2); }
+            float mu = fabsf(D1);
+            smin = mu;
+            if (fabsf(E1) <= tol * mu) { E1 = 0.0f; zeroed = true; }
+            else {
+                mu = fabsf(D2) * fdiv(mu, mu + fabsf(E1));
+                smin = fminf(smin, mu);
+                if (fabsf(E2) <= tol * mu) { E2 = 0.0f; zeroed = true; }
+                else {
+                    mu = fabsf(D3) * fdiv(mu, mu + fabsf(E2));
+                    smin = fminf(smin, mu);
+                }
+            }
+        }
+        if (zeroed) {
+            e1 = mir ? E2 : E1;
+            e2 = mir ? E1 : E2;
+            continue;
+        }
+        float shift = 0.0f;
+        if (!((3.0f * tol) * fdiv(smin, smax) <= fmaxf(eps, 0.01f * tol))) {
+            const float sll = fabsf(D1);
+            shift = la_las2_min(D2, E2, D3);
             if (sll > 0.0f) { const float q = fdiv(shift, sll); if (q * q < eps) shift = 0.0f; }
         }
         iter += 2;
-        float c1, s1, c2, s2, oc1, os1, oc2, os2;   // rotations of the sweep (VT pair, U pair) at i = 1, 2
+        // rotations of the two steps: (ac, as) / (bc, bs) at the first, (cc, cs) / (dc, ds) at the second
+        float ac, as, bc, bs, cc, cs, dc, ds;
         if (shift == 0.0f) {
-            float cs, sn, oldcs, oldsn, r, h;
-            if (idir == 1) {
-                la_lartg(d1, e1, cs, sn, r);                      // i = 1 (cs = 1)
-                la_lartg(r, d2 * sn, oldcs, oldsn, d1);           // oldcs = 1
-                c1 = cs; s1 = sn; oc1 = oldcs; os1 = oldsn;
-                la_lartg(d2 * cs, e2, cs, sn, r);                 // i = 2
-                e1 = oldsn * r;
-                la_lartg(oldcs * r, d3 * sn, oldcs, oldsn, d2);
-                c2 = cs; s2 = sn; oc2 = oldcs; os2 = oldsn;
-                h = d3 * cs; d3 = h * oldcs; e2 = h * oldsn;
-                vt_rot(z, 0, c1, s1); vt_rot(z, 1, c2, s2);
-                u_rot(z, 0, oc1, os1); u_rot(z, 1, oc2, os2);
-                if (fabsf(e2) <= thresh) e2 = 0.0f;
-            } else {
-                la_lartg(d3, e2, cs, sn, r);                      // i = 3
-                la_lartg(r, d2 * sn, oldcs, oldsn, d3);
-                c2 = cs; s2 = -sn; oc2 = oldcs; os2 = -oldsn;     // work(i - ll) = work(2)
-                la_lartg(d2 * cs, e1, cs, sn, r);                 // i = 2
-                e2 = oldsn * r;
-                la_lartg(oldcs * r, d1 * sn, oldcs, oldsn, d2);
-                c1 = cs; s1 = -sn; oc1 = oldcs; os1 = -oldsn;
-                h = d1 * cs; d1 = h * oldcs; e1 = h * oldsn;
-                vt_rot(z, 1, oc2, os2); vt_rot(z, 0, oc1, os1);   // SLASR('L','V','B') with work(nm12+1..)
-                u_rot(z, 1, c2, s2); u_rot(z, 0, c1, s1);         // SLASR('R','V','B') with work(1..)
-                if (fabsf(e1) <= thresh) e1 = 0.0f;
-            }
+            float r, h;
+            la_lartg(D1, E1, ac, as, r);                 // cs = 1
+            la_lartg(r, D2 * as, bc, bs, D1);            // oldcs = 1
+            la_lartg(D2 * ac, E2, cc, cs, r);
+            E1 = bs * r;
+            la_lartg(bc * r, D3 * cs, dc, ds, D2);
+            h = D3 * cc;
+            D3 = h * dc;
+            E2 = h * ds;
         } else {
-            float f, g, r, cosr, sinr, cosl, sinl;
-            if (idir == 1) {
-                f = (fabsf(d1) - shift) * (__builtin_copysignf(1.0f, d1) + fdiv(shift, d1));
-                g = e1;
-                // i = 1
-                la_lartg(f, g, cosr, sinr, r);
-                f = cosr * d1 + sinr * e1;
-                e1 = cosr * e1 - sinr * d1;
-                g = sinr * d2;
-                d2 = cosr * d2;
-                la_lartg(f, g, cosl, sinl, r);
-                d1 = r;
-                f = cosl * e1 + sinl * d2;
-                d2 = cosl * d2 - sinl * e1;
-                g = sinl * e2;
-                e2 = cosl * e2;
-                c1 = cosr; s1 = sinr; oc1 = cosl; os1 = sinl;
-                // i = 2
-                la_lartg(f, g, cosr, sinr, r);
-                e1 = r;
-                f = cosr * d2 + sinr * e2;
-                e2 = cosr * e2 - sinr * d2;
-                g = sinr * d3;
-                d3 = cosr * d3;
-                la_lartg(f, g, cosl, sinl, r);
-                d2 = r;
-                f = cosl * e2 + sinl * d3;
-                d3 = cosl * d3 - sinl * e2;
-                c2 = cosr; s2 = sinr; oc2 = cosl; os2 = sinl;
-                e2 = f;
-                vt_rot(z, 0, c1, s1); vt_rot(z, 1, c2, s2);
-                u_rot(z, 0, oc1, os1); u_rot(z, 1, oc2, os2);
-                if (fabsf(e2) <= thresh) e2 = 0.0f;
-            } else {
-                f = (fabsf(d3) - shift) * (__builtin_copysignf(1.0f, d3) + fdiv(shift, d3));
-                g = e2;
-                // i = 3
-                la_lartg(f, g, cosr, sinr, r);
-                f = cosr * d3 + sinr * e2;
-                e2 = cosr * e2 - sinr * d3;
-                g = sinr * d2;
-                d2 = cosr * d2;
-                la_lartg(f, g, cosl, sinl, r);
-                d3 = r;
-                f = cosl * e2 + sinl * d2;
-                d2 = cosl * d2 - sinl * e2;
-                g = sinl * e1;
-                e1 = cosl * e1;
-                c2 = cosr; s2 = -sinr; oc2 = cosl; os2 = -sinl;
-                // i = 2
-                la_lartg(f, g, cosr, sinr, r);
-                e2 = r;
-                f = cosr * d2 + sinr * e1;
-                e1 = cosr * e1 - sinr * d2;
-                g = sinr * d1;
-                d1 = cosr * d1;
-                la_lartg(f, g, cosl, sinl, r);
-                d2 = r;
-                f = cosl * e1 + sinl * d1;
-                d1 = cosl * d1 - sinl * e1;
-                c1 = cosr; s1 = -sinr; oc1 = cosl; os1 = -sinl;
-                e1 = f;
-                if (fabsf(e1) <= thresh) e1 = 0.0f;
-                vt_rot(z, 1, oc2, os2); vt_rot(z, 0, oc1, os1);
-                u_rot(z, 1, c2, s2); u_rot(z, 0, c1, s1);
-            }
+            float f = (fabsf(D1) - shift) * (__builtin_copysignf(1.0f, D1) + fdiv(shift, D1)), g = E1, r;
+            la_lartg(f, g, ac, as, r);
+            f = ac * D1 + as * E1;
+            E1 = ac * E1 - as * D1;
+            g = as * D2;
+            D2 = ac * D2;
+            la_lartg(f, g, bc, bs, r);
+            D1 = r;
+            f = bc * E1 + bs * D2;
+            D2 = bc * D2 - bs * E1;
+            g = bs * E2;
+            E2 = bc * E2;
+            la_lartg(f, g, cc, cs, r);
+            E1 = r;
+            f = cc * D2 + cs * E2;
+            E2 = cc * E2 - cs * D2;
+            g = cs * D3;
+            D3 = cc * D3;
+            la_lartg(f, g, dc, ds, r);
+            D2 = r;
+            f = dc * E2 + ds * D3;
+            D3 = dc * D3 - ds * E2;
+            E2 = f;
         }
+        if (fabsf(E2) <= thresh) E2 = 0.0f;
+        d1 = mir ? D3 : D1; d2 = D2; d3 = mir ? D1 : D3;
+        e1 = mir ? E2 : E1; e2 = mir ? E1 : E2;
+        // IDIR = 1: VT pairs (1,2) then (2,3) by (a, c), U by (b, d).  IDIR = 2: VT (2,3) then (1,2) by (b, d),
+        // U by (a, c), sines negated.
+        vt_rot(z, mir, mir ? bc : ac, mir ? -bs : as);
+        vt_rot(z, !mir, mir ? dc : cc, mir ? -ds : cs);
+        u_rot(z, mir, mir ? ac : bc, mir ? -as : bs);
+        u_rot(z, !mir, mir ? cc : dc, mir ? -cs : ds);
     }
     // singular values made positive (VT rows negated), then sorted decreasing (SBDSQR :160-190)
     if (d1 < 0.0f) { d1 = -d1; z.vt[0] = -z.vt[0]; z.vt[3] = -z.vt[3]; z.vt[6] = -z.vt[6]; }
@@ -783,29 +757,36 @@ RTG_DEV void la_bdsqr3(float &d1, float &d2, float &d3, float e1, float e2, Svd3
         float mn = d1;
         if (d2 <= mn) { isub = 2; mn = d2; }
         if (d3 <= mn) { isub = 3; mn = d3; }
-        if (isub == 1) {
-            d1 = d3; d3 = mn;
+        const bool s1 = isub == 1, s2 = isub == 2;
+        d1 = s1 ? d3 : d1;
+        d2 = s2 ? d3 : d2;
+        d3 = mn;
 #pragma unroll
-            for (int k = 0; k < 3; ++k) {
-                float t = z.vt[0 + 3 * k]; z.vt[0 + 3 * k] = z.vt[2 + 3 * k]; z.vt[2 + 3 * k] = t;
-                t = z.u[k]; z.u[k] = z.u[k + 6]; z.u[k + 6] = t;
-            }
-        } else if (isub == 2) {
-            d2 = d3; d3 = mn;
-#pragma unroll
-            for (int k = 0; k < 3; ++k) {
-                float t = z.vt[1 + 3 * k]; z.vt[1 + 3 * k] = z.vt[2 + 3 * k]; z.vt[2 + 3 * k] = t;
-                t = z.u[k + 3]; z.u[k + 3] = z.u[k + 6]; z.u[k + 6] = t;
-            }
+        for (int k = 0; k < 3; ++k) {
+            const float v0 = z.vt[3 * k], v1 = z.vt[1 + 3 * k], v2 = z.vt[2 + 3 * k];
+            z.vt[3 * k] = s1 ? v2 : v0;
+            z.vt[1 + 3 * k] = s2 ? v2 : v1;
+            z.vt[2 + 3 * k] = s1 ? v0 : (s2 ? v1 : v2);
+            const float u0 = z.u[k], u1 = z.u[k + 3], u2 = z.u[k + 6];
+            z.u[k] = s1 ? u2 : u0;
+            z.u[k + 3] = s2 ? u2 : u1;
+            z.u[k + 6] = s1 ? u0 : (s2 ? u1 : u2);
         }
     }
     // pass 2: smaller of (d1, d2), ties to d2, moves to position 2
-    if (!(d2 <= d1)) {
-        const float t0 = d1; d1 = d2; d2 = t0;
+    {
+        const bool sw = !(d2 <= d1);
+        const float t0 = d1;
+        d1 = sw ? d2 : d1;
+        d2 = sw ? t0 : d2;
 #pragma unroll
         for (int k = 0; k < 3; ++k) {
-            float t = z.vt[0 + 3 * k]; z.vt[0 + 3 * k] = z.vt[1 + 3 * k]; z.vt[1 + 3 * k] = t;
-            t = z.u[k]; z.u[k] = z.u[k + 3]; z.u[k + 3] = t;
+            const float v0 = z.vt[3 * k], v1 = z.vt[1 + 3 * k];
+            z.vt[3 * k] = sw ? v1 : v0;
+            z.vt[1 + 3 * k] = sw ? v0 : v1;
+            const float u0 = z.u[k], u1 = z.u[k + 3];
+            z.u[k] = sw ? u1 : u0;
+            z.u[k + 3] = sw ? u0 : u1;
         }
     }
 }

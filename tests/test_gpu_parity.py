@@ -278,6 +278,36 @@ def test_transcendental_primitives_vs_oracle(gpu):
         assert s["exact_elems"] >= 0.999 and s["max"] <= 2.5e-7, (i, s)
 
 
+def test_kabsch_sgesdd_random_and_degenerate_vs_oracle(gpu):
+    """The device sgesdd restatement (rtg_math.cuh la_gesdd3) against the oracle's (rtg_oracle.c la_gesdd3),
+    bit for bit, on 3- and 5-point fits: well-conditioned rotations with noise, coplanar / collinear point sets
+    (rank 2 and 1), reflections, tiny (sgesdd's 2^-40 rescale) and huge scales, exact zeros and duplicates."""
+    import oracle as orc
+    from rtg import ops
+    rng = np.random.default_rng(11)
+    for npts in (3, 5):
+        n = 16384
+        Z = rng.standard_normal((n, npts, 3)).astype(np.float32) * 0.1
+        ang = rng.uniform(0, np.pi, n)
+        ax = rng.standard_normal((n, 3))
+        ax /= np.linalg.norm(ax, axis=1, keepdims=True)
+        q = np.concatenate([ax * np.sin(ang / 2)[:, None], np.cos(ang / 2)[:, None]], 1).astype(np.float32)
+        M = orc.quat_rotate(np.repeat(q, npts, 0), Z.reshape(-1, 3)).reshape(n, npts, 3)
+        M = (M + rng.standard_normal(M.shape) * 2e-3).astype(np.float32)
+        k = n // 8
+        M[0:k, :, 2] = 0.0                                    # coplanar motion points
+        M[k:2 * k] = M[k:2 * k, :1] * rng.uniform(0.5, 2, (k, npts, 1)).astype(np.float32)   # collinear
+        M[2 * k:3 * k, :, 0] *= -1.0                          # mirrored: det(U Vt) < 0 branch
+        M[3 * k:4 * k] *= np.float32(1e-12)                   # below sgesdd's smlnum: rescaled
+        M[4 * k:4 * k + 64] = 0.0                             # all-zero fit
+        M[4 * k + 64:4 * k + 128, 1] = M[4 * k + 64:4 * k + 128, 0]   # duplicated point
+        M[5 * k:6 * k] *= np.float32(1e3)
+        g = _np(ops.cal_joint_quat(Z, M))
+        o = orc.cal_joint_quat(Z, M)
+        bad = ~np.all((g == o) | (np.isnan(g) & np.isnan(o)), axis=1)
+        assert not bad.any(), (npts, int(bad.sum()), np.nonzero(bad)[0][:8])
+
+
 def test_proj_in_plane_and_reference(gpu):
     from rtg import ops
     p = golden("primitives")
