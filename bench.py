@@ -65,10 +65,48 @@ def barrier(world):
     torch.cuda.synchronize()
 
 
+def cpu_share() -> int:
+    """CPUs this process may use: the affinity mask, capped by a cgroup v2 CPU quota (the GPU box exposes the
+    whole machine in os.cpu_count() but grants one GPU's share of it)."""
+    n = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if q != "max":
+            n = min(n, max(1, int(int(q) // int(per))))
+    except (OSError, ValueError):
+        pass
+    return max(1, n)
+
+
+_PER_FRAME_CHILD = r"""
+import os, sys, time, numpy as np
+sys.path.insert(0, sys.argv[1])
+import oracle as orc
+orc.lib().oracle_set_threads(1)
+d = np.load(sys.argv[2])
+lo, hi, secs = int(sys.argv[3]), int(sys.argv[4]), float(sys.argv[5])
+b, l, r, zl, zg = d["body"][lo:hi], d["lh"][lo:hi], d["rh"][lo:hi], d["zl"], d["zg"]
+done, t0 = 0, time.perf_counter()
+while time.perf_counter() - t0 < secs:
+    for i in range(0, hi - lo, 64):   # 64-frame calls of the per-frame C solver, one core
+        orc.full_body_pos(zl, zg, b[i:i + 64], l[i:i + 64], r[i:i + 64], True, want_rot=False)
+        done += min(64, hi - lo - i)
+print(done, time.perf_counter() - t0)
+"""
+
+
 def cpu_baseline(body, lh, rh, zl, zg, seconds):
-    """Oracle (the C port of the reference path) on the host cores, bounded sample."""
+    """The oracle (the C port of the reference path, kind "port") on the host's CPU share, bounded sample:
+    (1) the batched path, OpenMP over every CPU of the share (thread count pinned through the oracle);
+    (2) SURVEY §8d's per-frame leg: one single-thread process per CPU of the share on disjoint frame slices.
+    The GPU box's os.cpu_count() is the whole machine; this job is granted a share of it (cpu_share())."""
+    import tempfile
+
     import oracle as orc
-    threads = int(os.environ.get("OMP_NUM_THREADS", str(min(16, os.cpu_count() or 1))))
+    share = cpu_share()
+    lib = orc.lib()
+    lib.oracle_set_threads(share)
+    threads = int(lib.oracle_max_threads())
     n = body.shape[0]
     orc.full_body_pos(zl, zg, body[:256], lh[:256], rh[:256], True, want_rot=False)   # warm
     done, t0 = 0, time.perf_counter()
@@ -80,9 +118,30 @@ def cpu_baseline(body, lh, rh, zl, zg, seconds):
         model = [l.split(":", 1)[1].strip() for l in open("/proc/cpuinfo") if l.startswith("model name")][0]
     except Exception:  # noqa: BLE001
         model = "unknown"
-    return {"value": done / dt, "unit": "frames/s", "cores": threads, "kind": "port",
-            "sample": f"{done} synthetic frames ({n}-frame slices of the bench workload), oracle/rtg_oracle.c "
-                      f"OpenMP x{threads}, {dt:.1f} s", "cpu": model}
+    out = {"value": done / dt, "unit": "frames/s", "cores": threads, "kind": "port",
+           "sample": f"{done} synthetic frames ({n}-frame slices of the bench workload), oracle/rtg_oracle.c "
+                     f"OpenMP x{threads}, {dt:.1f} s", "cpu": model, "host_cpus": os.cpu_count(), "cpu_share": share,
+           "per_core_frames_per_s": done / dt / threads}
+    # per-frame leg: `share` independent single-thread processes (children never touch the GPU)
+    try:
+        with tempfile.TemporaryDirectory() as td:
+            path = os.path.join(td, "frames.npz")
+            np.savez(path, body=body, lh=lh, rh=rh, zl=zl, zg=zg)
+            per = n // share
+            secs = max(2.0, seconds / 2)
+            procs = [subprocess.Popen([sys.executable, "-c", _PER_FRAME_CHILD, os.path.join(REPO, "oracle"), path,
+                                       str(k * per), str((k + 1) * per), str(secs)], stdout=subprocess.PIPE,
+                                      stderr=subprocess.DEVNULL, env=dict(os.environ, OMP_NUM_THREADS="1"), text=True)
+                     for k in range(share)]
+            res = [p.communicate(timeout=secs * 4 + 60)[0].split() for p in procs]
+            frames = sum(int(r[0]) for r in res)
+            rate = sum(int(r[0]) / float(r[1]) for r in res)
+            out["per_frame_processes"] = {"processes": share, "frames_per_s": rate, "frames": frames,
+                                          "us_per_frame_per_process": share / rate * 1e6,
+                                          "sample": f"{per}-frame slice per process, {secs:.0f} s each"}
+    except Exception as e:  # noqa: BLE001
+        out["per_frame_processes"] = {"error": repr(e)}
+    return out
 
 
 def pmc_traffic(B):
@@ -152,6 +211,33 @@ def secondary_configs(solver, sets, stream):
                                        "GBs_algorithmic": nbytes / (ms * 1e-3) / 1e9,
                                        "hbm_frac": nbytes / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS}
     return out
+
+
+def soa_line(solver, topo_full, B, rank, ring, steps, stream):
+    """The same workload with RTG_LAYOUT_SOA inputs ((P,C,B) component planes, emitted directly by the device
+    producer): every wave load of one component is 256 contiguous bytes instead of 64 row-strided 12-byte
+    reads.  Reported beside the AoS headline (the reference's own layout), not as `value`."""
+    import torch
+    from rtg import ops
+    sets = []
+    for r in range(ring):
+        b, l, r_ = ops.synth_full_body(topo_full, B, seed=1234 + rank, frame_offset=r * B, layout="soa")
+        sets.append((b, l, r_, torch.empty((B, 30), device=b.device)))
+    for i in range(5):
+        b, l, r_, d = sets[i % ring]
+        solver.retarget([b, l, r_], out_dof=d, layout="soa")
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record(stream)
+    for i in range(steps):
+        b, l, r_, d = sets[i % ring]
+        solver.retarget([b, l, r_], out_dof=d, layout="soa")
+    e1.record(stream)
+    e1.synchronize()
+    ms = e0.elapsed_time(e1) / steps
+    gbs = BYTES_PER_FRAME * B / (ms * 1e-3) / 1e9
+    return {"layout": "soa", "kernel_ms": ms, "frames_per_s": B / (ms * 1e-3), "achieved_GBs": gbs,
+            "hbm_frac": gbs / HBM_PEAK_GBS, "input_ring_sets": ring}
 
 
 def parity_vs_reference():
@@ -264,6 +350,12 @@ def main():
                 line["secondary"] = secondary_configs(solver, sets, stream)
             except Exception as e:  # noqa: BLE001
                 line["secondary"] = {"error": repr(e)}
+            try:
+                del sets[1:]
+                line["secondary"]["config3_soa_layout"] = soa_line(solver, topo_full, B, rank, ring, args.steps,
+                                                                   stream)
+            except Exception as e:  # noqa: BLE001
+                line["secondary"]["config3_soa_layout"] = {"error": repr(e)}
         try:
             line["parity_vs_reference"] = parity_vs_reference()
         except Exception as e:  # noqa: BLE001

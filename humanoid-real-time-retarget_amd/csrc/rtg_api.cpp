@@ -300,14 +300,16 @@ int rtg_dof_fk_f32(rtg_dof_model_t m, const float *dof, const float *root_rot, c
 }
 
 // ---------------------------------------------------------------- VTRDyn ingest
-int rtg_ingest_vtrdyn_f32(const float *bp, const float *lhp, const float *rhp, int64_t B, float *body, float *lh,
-                          float *rh, uint8_t *valid, rtg_stream_t stream)
+int rtg_ingest_vtrdyn_f32(const float *bp, const float *lhp, const float *rhp, int64_t B, int layout, float *body,
+                          float *lh, float *rh, uint8_t *valid, rtg_stream_t stream)
 {
     if (B < 0) return fail(RTG_ERR_INVALID_ARGUMENT, "rtg_ingest_vtrdyn_f32: B < 0");
+    if (layout != RTG_LAYOUT_AOS && layout != RTG_LAYOUT_SOA)
+        return fail(RTG_ERR_INVALID_ARGUMENT, "rtg_ingest_vtrdyn_f32: bad layout %d", layout);
     if (B == 0) return RTG_OK;
     if (!bp || !lhp || !rhp || !body || !lh || !rh || !valid)
         return fail(RTG_ERR_INVALID_ARGUMENT, "rtg_ingest_vtrdyn_f32: NULL buffer");
-    RTG_TRY(launch_ingest_vtrdyn(bp, lhp, rhp, B, body, lh, rh, valid, as_stream(stream)), "k_ingest_vtrdyn");
+    RTG_TRY(launch_ingest_vtrdyn(bp, lhp, rhp, B, layout, body, lh, rh, valid, as_stream(stream)), "k_ingest_vtrdyn");
     return RTG_OK;
 }
 
@@ -431,10 +433,12 @@ int rtg_solver_destroy(rtg_solver_t s)
 }
 
 int rtg_retarget_f32(rtg_solver_t s, const float *in0, const float *in1, const float *in2, const float *in3,
-                     int64_t B, float *dof, float *local_rot, float *body_rot, rtg_stream_t stream)
+                     int64_t B, int layout, float *dof, float *local_rot, float *body_rot, rtg_stream_t stream)
 {
     if (!s) return fail(RTG_ERR_INVALID_ARGUMENT, "rtg_retarget_f32: NULL solver");
     if (B < 0) return fail(RTG_ERR_INVALID_ARGUMENT, "rtg_retarget_f32: negative batch");
+    if (layout != RTG_LAYOUT_AOS && layout != RTG_LAYOUT_SOA)
+        return fail(RTG_ERR_INVALID_ARGUMENT, "rtg_retarget_f32: bad layout %d", layout);
     if (B == 0) return RTG_OK;
     if (B > (int64_t)0x7fffffff * 256) return fail(RTG_ERR_INVALID_ARGUMENT, "rtg_retarget_f32: batch too large");
     if (!dof) return fail(RTG_ERR_INVALID_ARGUMENT, "rtg_retarget_f32: NULL dof");
@@ -446,7 +450,7 @@ int rtg_retarget_f32(rtg_solver_t s, const float *in0, const float *in1, const f
     }
     if (body_rot && s->kind != RTG_SOLVER_FULL_BODY_POS)
         return fail(RTG_ERR_INVALID_ARGUMENT, "rtg_retarget_f32: body_rot is only produced by FULL_BODY_POS");
-    RTG_TRY(launch_retarget(s->kind, s->precise, s->consts, in0, in1, in2, in3, B, dof, local_rot, body_rot,
+    RTG_TRY(launch_retarget(s->kind, s->precise, s->consts, in0, in1, in2, in3, B, layout, dof, local_rot, body_rot,
                             as_stream(stream)),
             "k_retarget");
     return RTG_OK;
@@ -537,14 +541,17 @@ int rtg_angular_velocity_f32(const float *r, int64_t nseq, int64_t L, int64_t J,
 }
 
 // ---------------------------------------------------------------- synthetic input
-int rtg_synth_full_body_f32(rtg_topology_t t, uint64_t seed, int64_t off, int64_t B, float *body, float *lh,
-                            float *rh, float *body_rot, rtg_stream_t stream)
+int rtg_synth_full_body_f32(rtg_topology_t t, uint64_t seed, int64_t off, int64_t B, int layout, float *body,
+                            float *lh, float *rh, float *body_rot, rtg_stream_t stream)
 {
+    if (layout != RTG_LAYOUT_AOS && layout != RTG_LAYOUT_SOA)
+        return fail(RTG_ERR_INVALID_ARGUMENT, "rtg_synth_full_body_f32: bad layout %d", layout);
     if (!t || t->J != 59) return fail(RTG_ERR_INVALID_ARGUMENT, "rtg_synth_full_body_f32: needs the 59-joint VTRDYN_FULL topology");
     if (B < 0 || off < 0) return fail(RTG_ERR_INVALID_ARGUMENT, "rtg_synth_full_body_f32: negative batch/offset");
     if (B == 0) return RTG_OK;
     if (!body || !lh || !rh) return fail(RTG_ERR_INVALID_ARGUMENT, "rtg_synth_full_body_f32: NULL buffer");
-    RTG_TRY(launch_synth_full_body(t->view(), seed, off, B, body, lh, rh, body_rot, as_stream(stream)), "k_synth_full_body");
+    RTG_TRY(launch_synth_full_body(t->view(), seed, off, B, body, lh, rh, body_rot, layout, as_stream(stream)),
+            "k_synth_full_body");
     return RTG_OK;
 }
 

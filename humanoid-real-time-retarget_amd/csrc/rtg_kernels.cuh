@@ -63,7 +63,7 @@ struct FkMultiArgs {
 hipError_t launch_solver_prep(SolverConsts *dev_consts, hipStream_t s);
 hipError_t launch_build_ang_tab(uint32_t *tab, hipStream_t s);   // kAngTabWords words
 hipError_t launch_retarget(int kind, int precise, const SolverConsts &C, const float *in0, const float *in1,
-                           const float *in2, const float *in3, int64_t B, float *dof, float *local_rot,
+                           const float *in2, const float *in3, int64_t B, int layout, float *dof, float *local_rot,
                            float *body_rot, hipStream_t s);
 hipError_t launch_fk(const TopoView &T, bool state, const float *lr, const float *rt, int64_t B, float *gr, float *gp,
                      hipStream_t s);
@@ -76,8 +76,8 @@ hipError_t launch_rescale_motion(const TopoView &T, const float *motion, int64_t
 hipError_t launch_quat_between(const float *v1, const float *v2, int64_t n, float *out, float *ws, hipStream_t s);
 hipError_t launch_rebuild_vtrdyn(const TopoView &T, const float *motion, int64_t B, float *g_rot, float *root_t,
                                  float *ws, hipStream_t s);
-hipError_t launch_ingest_vtrdyn(const float *bp, const float *lhp, const float *rhp, int64_t B, float *body,
-                                float *lh, float *rh, uint8_t *valid, hipStream_t s);
+hipError_t launch_ingest_vtrdyn(const float *bp, const float *lhp, const float *rhp, int64_t B, int layout,
+                                float *body, float *lh, float *rh, uint8_t *valid, hipStream_t s);
 hipError_t launch_quat_op(int op, const float *a, const float *b, const float *c, int64_t n, float *out,
                           hipStream_t s);
 hipError_t launch_cal_joint_quat(const float *Z, const float *M, int npts, int64_t n, float *out, hipStream_t s);
@@ -92,6 +92,6 @@ hipError_t launch_linear_velocity(const float *p, int64_t nseq, int64_t L, int64
 hipError_t launch_angular_velocity(const float *r, int64_t nseq, int64_t L, int64_t J, float dt,
                                    const GaussTaps *taps, float *tmp, float *out, hipStream_t s);
 hipError_t launch_synth_full_body(const TopoView &T, uint64_t seed, int64_t off, int64_t B, float *body, float *lh,
-                                  float *rh, float *body_rot, hipStream_t s);
+                                  float *rh, float *body_rot, int layout, hipStream_t s);
 
 }  // namespace rtg

@@ -140,11 +140,46 @@ RTG_DEV float hand_x_mean(Q rot, V h0, const V (&tip)[5])   // gripper x-spread
     return mean5(qrotate(rot, tip[0]).x - x0, qrotate(rot, tip[1]).x - x0, qrotate(rot, tip[2]).x - x0,
                  qrotate(rot, tip[3]).x - x0, qrotate(rot, tip[4]).x - x0);
 }
+// One frame's input rows.  AoS (the reference's layout): the frame's (P, C) row at p.  SoA (RTG_LAYOUT_SOA):
+// component planes of the whole batch, element (j, c) of frame f at p[(j C + c) B + f] with p pointing at frame f
+// -- a wave's load of one component is 256 contiguous bytes.
+template <bool SOA>
+struct FV;
+template <>
+struct FV<false> {
+    const float *__restrict__ p;
+    RTG_DEV V p3(int j) const { return ld3(p + 3 * j); }
+    RTG_DEV Q q4(int j) const { return ld4(p + 4 * j); }
+};
+template <>
+struct FV<true> {
+    const float *__restrict__ p;
+    int64_t s;
+    RTG_DEV V p3(int j) const { return V{p[(3 * j) * s], p[(3 * j + 1) * s], p[(3 * j + 2) * s]}; }
+    RTG_DEV Q q4(int j) const { return Q{p[(4 * j) * s], p[(4 * j + 1) * s], p[(4 * j + 2) * s], p[(4 * j + 3) * s]}; }
+};
+template <bool SOA>
+RTG_DEV FV<SOA> frame_view(const float *__restrict__ base, int64_t f, int row_floats, int64_t B);
+template <>
+RTG_DEV FV<false> frame_view<false>(const float *__restrict__ base, int64_t f, int row_floats, int64_t)
+{
+    return FV<false>{base + f * row_floats};
+}
+template <>
+RTG_DEV FV<true> frame_view<true>(const float *__restrict__ base, int64_t f, int, int64_t B)
+{
+    return FV<true>{base + f, B};
+}
+
+template <typename View>
+RTG_DEV float hand_x_mean(Q rot, const View &H, const int (&idx)[5])
+{
+    const V tip[5] = {H.p3(idx[0]), H.p3(idx[1]), H.p3(idx[2]), H.p3(idx[3]), H.p3(idx[4])};
+    return hand_x_mean(rot, H.p3(0), tip);
+}
 RTG_DEV float hand_x_mean(Q rot, const float *__restrict__ H, const int (&idx)[5])
 {
-    const V tip[5] = {ld3(H + 3 * idx[0]), ld3(H + 3 * idx[1]), ld3(H + 3 * idx[2]), ld3(H + 3 * idx[3]),
-                      ld3(H + 3 * idx[4])};
-    return hand_x_mean(rot, ld3(H), tip);
+    return hand_x_mean(rot, FV<false>{H}, idx);
 }
 
 // The 32 input points VtrdynFullBodyPosRetargeter reads (body 10,11,13..20; per
@@ -359,17 +394,19 @@ __global__ __launch_bounds__(kSolverBlock) void k_retarget(SolverConsts C, const
 constexpr int kSideFrames = 128;   // frames per 256-thread block
 
 // torso fit R10 (full_body_pos_retargeter.py:69-70 / retarget_solver.py:49-50)
-RTG_DEV Q fbp_torso(const SolverConsts &C, const float *__restrict__ b)
+template <typename View>
+RTG_DEV Q fbp_torso(const SolverConsts &C, const View &b)
 {
-    const V b10 = ld3(b + 30);
-    const V Mt[3] = {vsub(ld3(b + 51), b10), vsub(ld3(b + 39), b10), vsub(ld3(b + 33), b10)};
+    const V b10 = b.p3(10);
+    const V Mt[3] = {vsub(b.p3(17), b10), vsub(b.p3(13), b10), vsub(b.p3(11), b10)};
     return cal_joint_quat<3>(C.Zt, Mt);
 }
 RTG_DEV Q upper_pt_sign(V v) { return Q{v.x * -1.0f, v.y * -1.0f, v.z * 1.0f, 0.0f}; }   // coord_transform :41
-RTG_DEV Q upper_torso(const SolverConsts &C, const float *__restrict__ x)
+template <typename View>
+RTG_DEV Q upper_torso(const SolverConsts &C, const View &x)
 {
     auto pt = [&](int j) {
-        const Q q = upper_pt_sign(ld3(x + 3 * j));
+        const Q q = upper_pt_sign(x.p3(j));
         return V{q.x, q.y, q.z};
     };
     const V s10 = pt(10);
@@ -377,23 +414,22 @@ RTG_DEV Q upper_torso(const SolverConsts &C, const float *__restrict__ x)
     return cal_joint_quat<3>(C.Zt, Mt);
 }
 // wrist fit W (full_body_pos_retargeter.py:137-140 left, :160-163 right)
-template <int SIDE>
-RTG_DEV Q fbp_wrist_fit(const SolverConsts &C, const float *__restrict__ H)
+template <int SIDE, typename View>
+RTG_DEV Q fbp_wrist_fit(const SolverConsts &C, const View &H)
 {
-    const V h0 = ld3(H);
-    const V M[5] = {vsub(ld3(H + 6), h0), vsub(ld3(H + 18), h0), vsub(ld3(H + 30), h0), vsub(ld3(H + 42), h0),
-                    vsub(ld3(H + 51), h0)};
+    const V h0 = H.p3(0);
+    const V M[5] = {vsub(H.p3(2), h0), vsub(H.p3(6), h0), vsub(H.p3(10), h0), vsub(H.p3(14), h0), vsub(H.p3(17), h0)};
     return cal_joint_quat<5>(SIDE ? C.Zr : C.Zl, M);
 }
 
-template <bool PRECISE, int SIDE>
-RTG_DEV void solve_fbp_side(const SolverConsts &C, const float *__restrict__ b, const float *__restrict__ H,
-                            Q R10, Q W, const Emit &E, float *__restrict__ brow)
+template <bool PRECISE, int SIDE, typename View>
+RTG_DEV void solve_fbp_side(const SolverConsts &C, const View &b, const View &H, Q R10, Q W, const Emit &E,
+                            float *__restrict__ brow)
 {
     constexpr int L0 = SIDE ? 21 : 12, E0 = SIDE ? 25 : 16, D0 = SIDE ? 27 : 18, WROW = SIDE ? 39 : 14;
     constexpr int SH = SIDE ? 14 : 18, EL = SIDE ? 15 : 19, WR = SIDE ? 16 : 20;
-    const V bel = ld3(b + 3 * EL);
-    const Q chain = solve_arm<L0>(E, vsub(bel, ld3(b + 3 * SH)), vsub(ld3(b + 3 * WR), bel), SIDE ? C.rsh : C.lsh,
+    const V bel = b.p3(EL);
+    const Q chain = solve_arm<L0>(E, vsub(bel, b.p3(SH)), vsub(b.p3(WR), bel), SIDE ? C.rsh : C.lsh,
                                   SIDE ? C.rel : C.lel, R10);
     emit_euler_xyz<E0>(E, qmul_norm(qconj(qmul_norm(R10, chain)), W));
     constexpr int tips[5] = {4, 8, 12, 16, 19};
@@ -416,11 +452,11 @@ RTG_DEV void solve_fbp_side(const SolverConsts &C, const float *__restrict__ b, 
 }
 
 // HuUpperBodyFromMocapRetarget (retarget_solver.py:40-99), one side: one arm given the torso fit; wrists untouched
-template <int SIDE>
-RTG_DEV void solve_upper_side(const SolverConsts &C, const float *__restrict__ x, Q R10, const Emit &E)
+template <int SIDE, typename View>
+RTG_DEV void solve_upper_side(const SolverConsts &C, const View &x, Q R10, const Emit &E)
 {
     auto pt = [&](int j) {   // coord_transform(dir=[-1,-1,1]) :41
-        const Q q = upper_pt_sign(ld3(x + 3 * j));
+        const Q q = upper_pt_sign(x.p3(j));
         return V{q.x, q.y, q.z};
     };
     constexpr int L0 = SIDE ? 21 : 12, E0 = SIDE ? 25 : 16, D0 = SIDE ? 27 : 18;
@@ -432,17 +468,17 @@ RTG_DEV void solve_upper_side(const SolverConsts &C, const float *__restrict__ x
 }
 
 // VtrdynFullBodyRetargeter (full_body_retargeter.py:19-177), one side
-template <int SIDE>
-RTG_DEV void solve_full_body_rot_side(const SolverConsts &C, const float *__restrict__ q, const float *__restrict__ b,
-                                      const float *__restrict__ H, const Emit &E)
+template <int SIDE, typename View>
+RTG_DEV void solve_full_body_rot_side(const SolverConsts &C, const View &q, const View &b, const View &H,
+                                      const Emit &E)
 {
     constexpr int L0 = SIDE ? 21 : 12, E0 = SIDE ? 25 : 16, D0 = SIDE ? 27 : 18;
     constexpr int SH = SIDE ? 14 : 18, EL = SIDE ? 15 : 19, WR = SIDE ? 16 : 20, PAR = SIDE ? 13 : 17;
-    const Q par = ld4(q + PAR * 4);
-    const V bel = ld3(b + 3 * EL);
-    const Q chain = solve_arm<L0>(E, vsub(bel, ld3(b + 3 * SH)), vsub(ld3(b + 3 * WR), bel), SIDE ? C.rsh : C.lsh,
+    const Q par = q.q4(PAR);
+    const V bel = b.p3(EL);
+    const Q chain = solve_arm<L0>(E, vsub(bel, b.p3(SH)), vsub(b.p3(WR), bel), SIDE ? C.rsh : C.lsh,
                                   SIDE ? C.rel : C.lel, par);
-    const Q w = ld4(q + WR * 4);
+    const Q w = q.q4(WR);
     emit_euler_xyz<E0>(E, qmul_norm(qconj(qmul_norm(par, chain)), w));
     constexpr int tips[5] = {3, 7, 11, 15, 19};   // :145-177 rotates by the wrist quaternion itself
     const bool closed = hand_x_mean(w, H, tips) / C.orig < 0.7f;
@@ -451,10 +487,10 @@ RTG_DEV void solve_full_body_rot_side(const SolverConsts &C, const float *__rest
 }
 
 // Mocap2HuBodyRetargeter (body_retargeter.py:34-81), one side
-template <int SIDE>
-RTG_DEV void solve_body_rot_side(const SolverConsts &C, const float *__restrict__ g, const Emit &E)
+template <int SIDE, typename View>
+RTG_DEV void solve_body_rot_side(const SolverConsts &C, const View &g, const Emit &E)
 {
-    auto local = [&](int j, int p) { return qmul_norm(qconj(ld4(g + 4 * p)), ld4(g + 4 * j)); };
+    auto local = [&](int j, int p) { return qmul_norm(qconj(g.q4(p)), g.q4(j)); };
     constexpr int SH = SIDE ? 14 : 18, EL = SIDE ? 15 : 19, D0 = SIDE ? 27 : 18;
     Q s3[3], e3[3];
     quat_in_xyz_axis(local(SH, C.par[SIDE ? 1 : 0]), 1, 0, 2, false, s3);   // 'YXZ'
@@ -471,7 +507,7 @@ RTG_DEV void solve_body_rot_side(const SolverConsts &C, const float *__restrict_
     E.row[D0] = 0.0f; E.row[D0 + 1] = 0.0f;
 }
 
-template <int KIND, bool PRECISE>
+template <int KIND, bool PRECISE, bool SOA>
 __global__ __launch_bounds__(256, RTG_SIDES_WAVES) void k_solve_sides(SolverConsts C, const float *__restrict__ in0,
                                                      const float *__restrict__ in1, const float *__restrict__ in2,
                                                      const float *__restrict__ in3, int64_t B,
@@ -492,8 +528,9 @@ __global__ __launch_bounds__(256, RTG_SIDES_WAVES) void k_solve_sides(SolverCons
 #else
     const int64_t fi = f;
 #endif
+    auto view = [&](const float *base, int row_floats) { return frame_view<SOA>(base, fi, row_floats, B); };
 #if RTG_L2_PREFETCH
-    if (KIND == RTG_SOLVER_FULL_BODY_POS) {
+    if (KIND == RTG_SOLVER_FULL_BODY_POS && !SOA) {
         __shared__ float sink[64 * 4];
         const int64_t ft = f0 + (w >> 1) * 64, nt = B - ft < 64 ? B - ft : 64;
         if (nt > 0) {
@@ -505,14 +542,14 @@ __global__ __launch_bounds__(256, RTG_SIDES_WAVES) void k_solve_sides(SolverCons
     if (KIND == RTG_SOLVER_FULL_BODY_POS || KIND == RTG_SOLVER_UPPER_BODY) {
         // The torso fit is shared by both sides: the left wave fits it while the right wave fits its own hand
         // (FULL_BODY_POS; nothing to overlap for UPPER_BODY), then one block barrier hands R10 over LDS.
-        const float *b = in0 + fi * 63;   // body (FULL_BODY_POS) / mocap points (UPPER_BODY), both (B, 21, 3)
+        const auto b = view(in0, 63);   // body (FULL_BODY_POS) / mocap points (UPPER_BODY), both (B, 21, 3)
         Q R10 = qident(), W = qident();
         if (live) {
             if (!side) {
                 R10 = KIND == RTG_SOLVER_FULL_BODY_POS ? fbp_torso(C, b) : upper_torso(C, b);
                 storso[r] = make_float4(R10.x, R10.y, R10.z, R10.w);
             } else if (KIND == RTG_SOLVER_FULL_BODY_POS) {
-                W = fbp_wrist_fit<1>(C, in2 + fi * 60);
+                W = fbp_wrist_fit<1>(C, view(in2, 60));
             }
         }
         __syncthreads();
@@ -525,8 +562,8 @@ __global__ __launch_bounds__(256, RTG_SIDES_WAVES) void k_solve_sides(SolverCons
             }
             if (KIND == RTG_SOLVER_FULL_BODY_POS) {
                 float *brow = body_rot ? body_rot + f * 236 : nullptr;
-                if (side) solve_fbp_side<PRECISE, 1>(C, b, in2 + fi * 60, R10, W, E, brow);
-                else solve_fbp_side<PRECISE, 0>(C, b, in1 + fi * 60, R10, fbp_wrist_fit<0>(C, in1 + fi * 60), E, brow);
+                if (side) solve_fbp_side<PRECISE, 1>(C, b, view(in2, 60), R10, W, E, brow);
+                else solve_fbp_side<PRECISE, 0>(C, b, view(in1, 60), R10, fbp_wrist_fit<0>(C, view(in1, 60)), E, brow);
             } else {
                 if (side) solve_upper_side<1>(C, b, R10, E);
                 else solve_upper_side<0>(C, b, R10, E);
@@ -535,11 +572,11 @@ __global__ __launch_bounds__(256, RTG_SIDES_WAVES) void k_solve_sides(SolverCons
     } else if (live) {
         if (!side) emit_fixed_links(E);
         if (KIND == RTG_SOLVER_FULL_BODY_ROT) {
-            if (side) solve_full_body_rot_side<1>(C, in0 + fi * 84, in1 + fi * 63, in3 + fi * 60, E);
-            else solve_full_body_rot_side<0>(C, in0 + fi * 84, in1 + fi * 63, in2 + fi * 60, E);
+            if (side) solve_full_body_rot_side<1>(C, view(in0, 84), view(in1, 63), view(in3, 60), E);
+            else solve_full_body_rot_side<0>(C, view(in0, 84), view(in1, 63), view(in2, 60), E);
         } else {
-            if (side) solve_body_rot_side<1>(C, in0 + fi * 84, E);
-            else solve_body_rot_side<0>(C, in0 + fi * 84, E);
+            if (side) solve_body_rot_side<1>(C, view(in0, 84), E);
+            else solve_body_rot_side<0>(C, view(in0, 84), E);
         }
     }
     if (live) E.finalize(side * 7, 7);
@@ -1109,10 +1146,16 @@ __global__ __launch_bounds__(256) void k_rebuild_vtrdyn(TopoView T, const float 
 __constant__ int8_t c_body23_to_21[21] = {0, 1, 2, 3, 5, 6, 7, 9, 10, 11, 12, 13, 14, 15, 16, 17, 18, 19, 20, 21, 22};
 __constant__ int8_t c_hand_order[20] = {0, 4, 5, 6, 7, 8, 9, 10, 11, 16, 17, 18, 19, 12, 13, 14, 15, 1, 2, 3};
 
+// element (frame f, point j, component c) of a (B, P, C) batch in the given layout (rtg.h rtg_layout)
+RTG_DEV int64_t lay_idx(bool soa, int64_t f, int j, int c, int P, int C, int64_t B)
+{
+    return soa ? ((int64_t)(j * C + c)) * B + f : f * (P * C) + C * j + c;
+}
+
 __global__ __launch_bounds__(256) void k_ingest_vtrdyn(const float *__restrict__ bp, const float *__restrict__ lhp,
                                                        const float *__restrict__ rhp, int64_t B,
                                                        float *__restrict__ body, float *__restrict__ lh,
-                                                       float *__restrict__ rh, uint8_t *__restrict__ valid)
+                                                       float *__restrict__ rh, uint8_t *__restrict__ valid, bool soa)
 {
     const int64_t f = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (f >= B) return;
@@ -1120,11 +1163,21 @@ __global__ __launch_bounds__(256) void k_ingest_vtrdyn(const float *__restrict__
     bool close = true;   // np.allclose(body_pos, 0): |x| <= 1e-8 everywhere (a NaN is never close)
     for (int i = 0; i < 69; ++i) close = close && (fabsf(b[i]) <= 1e-8f);
     valid[f] = close ? 0 : 1;
-    for (int j = 0; j < 21; ++j) st3(body + f * 63 + 3 * j, ld3(b + 3 * c_body23_to_21[j]));
-    for (int j = 0; j < 20; ++j) {
-        st3(lh + f * 60 + 3 * j, ld3(lhp + f * 60 + 3 * c_hand_order[j]));
-        st3(rh + f * 60 + 3 * j, ld3(rhp + f * 60 + 3 * c_hand_order[j]));
+    if (!soa) {
+        for (int j = 0; j < 21; ++j) st3(body + f * 63 + 3 * j, ld3(b + 3 * c_body23_to_21[j]));
+        for (int j = 0; j < 20; ++j) {
+            st3(lh + f * 60 + 3 * j, ld3(lhp + f * 60 + 3 * c_hand_order[j]));
+            st3(rh + f * 60 + 3 * j, ld3(rhp + f * 60 + 3 * c_hand_order[j]));
+        }
+        return;
     }
+    for (int j = 0; j < 21; ++j)   // SoA planes: each store instruction writes 256 contiguous bytes per wave
+        for (int c = 0; c < 3; ++c) body[lay_idx(true, f, j, c, 21, 3, B)] = b[3 * c_body23_to_21[j] + c];
+    for (int j = 0; j < 20; ++j)
+        for (int c = 0; c < 3; ++c) {
+            lh[lay_idx(true, f, j, c, 20, 3, B)] = lhp[f * 60 + 3 * c_hand_order[j] + c];
+            rh[lay_idx(true, f, j, c, 20, 3, B)] = rhp[f * 60 + 3 * c_hand_order[j] + c];
+        }
 }
 
 int32_t fk_schedule(const int32_t *parents, int32_t J, int32_t *sched)
@@ -1378,7 +1431,7 @@ __constant__ int kFullToBody[21] = {0, 4, 5, 6, 1, 2, 3, 7, 8, 9, 10, 34, 35, 36
 
 __global__ __launch_bounds__(64) void k_synth_full_body(TopoView T, uint64_t seed, int64_t off, int64_t B,
                                                         float *__restrict__ body, float *__restrict__ lh,
-                                                        float *__restrict__ rh, float *__restrict__ body_rot)
+                                                        float *__restrict__ rh, float *__restrict__ body_rot, bool soa)
 {
     __shared__ float sp[64][59 * 3 + 1];
     __shared__ float sq[64][59 * 4];
@@ -1419,20 +1472,20 @@ __global__ __launch_bounds__(64) void k_synth_full_body(TopoView T, uint64_t see
     for (int i = 0; i < 21; ++i) {
         const int j = kFullToBody[i];
 #pragma unroll
-        for (int c = 0; c < 3; ++c) body[f * 63 + 3 * i + c] = jit(j, c);
+        for (int c = 0; c < 3; ++c) body[lay_idx(soa, f, i, c, 21, 3, B)] = jit(j, c);
         if (body_rot) {
             float n = sqrtf(G[4 * j] * G[4 * j] + G[4 * j + 1] * G[4 * j + 1] + G[4 * j + 2] * G[4 * j + 2] +
                             G[4 * j + 3] * G[4 * j + 3]);
             if (G[4 * j + 3] < 0.0f) n = -n;
 #pragma unroll
-            for (int c = 0; c < 4; ++c) body_rot[f * 84 + 4 * i + c] = G[4 * j + c] / n;
+            for (int c = 0; c < 4; ++c) body_rot[lay_idx(soa, f, i, c, 21, 4, B)] = G[4 * j + c] / n;
         }
     }
     for (int i = 0; i < 20; ++i) {
 #pragma unroll
         for (int c = 0; c < 3; ++c) {
-            lh[f * 60 + 3 * i + c] = jit(14 + i, c);
-            rh[f * 60 + 3 * i + c] = jit(39 + i, c);
+            lh[lay_idx(soa, f, i, c, 20, 3, B)] = jit(14 + i, c);
+            rh[lay_idx(soa, f, i, c, 20, 3, B)] = jit(39 + i, c);
         }
     }
 }
@@ -1470,33 +1523,37 @@ hipError_t launch_build_ang_tab(uint32_t *tab, hipStream_t s)
 // kernels for comparison.
 template <int KIND, bool PRECISE>
 static void launch_kind(const SolverConsts &C, const float *in0, const float *in1, const float *in2,
-                        const float *in3, int64_t B, float *dof, float *local_rot, float *body_rot, hipStream_t s)
+                        const float *in3, int64_t B, int layout, float *dof, float *local_rot, float *body_rot,
+                        hipStream_t s)
 {
-    if (!RTG_SOLVER_SIDES)
+    if (layout == RTG_LAYOUT_SOA)
+        hipLaunchKernelGGL((k_solve_sides<KIND, PRECISE, true>), dim3(grid_for(B, kSideFrames)), dim3(256), 0, s, C,
+                           in0, in1, in2, in3, B, dof, local_rot, body_rot);
+    else if (!RTG_SOLVER_SIDES)
         hipLaunchKernelGGL((k_retarget<KIND, PRECISE>), dim3(grid_for(B, kSolverBlock)), dim3(kSolverBlock), 0, s,
                            C, in0, in1, in2, in3, B, dof, local_rot, body_rot);
     else
-        hipLaunchKernelGGL((k_solve_sides<KIND, PRECISE>), dim3(grid_for(B, kSideFrames)), dim3(256), 0, s, C,
+        hipLaunchKernelGGL((k_solve_sides<KIND, PRECISE, false>), dim3(grid_for(B, kSideFrames)), dim3(256), 0, s, C,
                            in0, in1, in2, in3, B, dof, local_rot, body_rot);
 }
 
 hipError_t launch_retarget(int kind, int precise, const SolverConsts &C, const float *in0, const float *in1,
-                           const float *in2, const float *in3, int64_t B, float *dof, float *local_rot,
+                           const float *in2, const float *in3, int64_t B, int layout, float *dof, float *local_rot,
                            float *body_rot, hipStream_t s)
 {
     switch (kind) {
     case RTG_SOLVER_FULL_BODY_POS:
-        if (precise) launch_kind<RTG_SOLVER_FULL_BODY_POS, true>(C, in0, in1, in2, in3, B, dof, local_rot, body_rot, s);
-        else launch_kind<RTG_SOLVER_FULL_BODY_POS, false>(C, in0, in1, in2, in3, B, dof, local_rot, body_rot, s);
+        if (precise) launch_kind<RTG_SOLVER_FULL_BODY_POS, true>(C, in0, in1, in2, in3, B, layout, dof, local_rot, body_rot, s);
+        else launch_kind<RTG_SOLVER_FULL_BODY_POS, false>(C, in0, in1, in2, in3, B, layout, dof, local_rot, body_rot, s);
         break;
     case RTG_SOLVER_UPPER_BODY:
-        launch_kind<RTG_SOLVER_UPPER_BODY, false>(C, in0, in1, in2, in3, B, dof, local_rot, body_rot, s);
+        launch_kind<RTG_SOLVER_UPPER_BODY, false>(C, in0, in1, in2, in3, B, layout, dof, local_rot, body_rot, s);
         break;
     case RTG_SOLVER_FULL_BODY_ROT:
-        launch_kind<RTG_SOLVER_FULL_BODY_ROT, false>(C, in0, in1, in2, in3, B, dof, local_rot, body_rot, s);
+        launch_kind<RTG_SOLVER_FULL_BODY_ROT, false>(C, in0, in1, in2, in3, B, layout, dof, local_rot, body_rot, s);
         break;
     default:
-        launch_kind<RTG_SOLVER_BODY_ROT, false>(C, in0, in1, in2, in3, B, dof, local_rot, body_rot, s);
+        launch_kind<RTG_SOLVER_BODY_ROT, false>(C, in0, in1, in2, in3, B, layout, dof, local_rot, body_rot, s);
         break;
     }
     return hipGetLastError();
@@ -1591,10 +1648,11 @@ hipError_t launch_rebuild_vtrdyn(const TopoView &T, const float *motion, int64_t
     return hipGetLastError();
 }
 
-hipError_t launch_ingest_vtrdyn(const float *bp, const float *lhp, const float *rhp, int64_t B, float *body,
-                                float *lh, float *rh, uint8_t *valid, hipStream_t s)
+hipError_t launch_ingest_vtrdyn(const float *bp, const float *lhp, const float *rhp, int64_t B, int layout,
+                                float *body, float *lh, float *rh, uint8_t *valid, hipStream_t s)
 {
-    hipLaunchKernelGGL(k_ingest_vtrdyn, dim3(grid_for(B, 256)), dim3(256), 0, s, bp, lhp, rhp, B, body, lh, rh, valid);
+    hipLaunchKernelGGL(k_ingest_vtrdyn, dim3(grid_for(B, 256)), dim3(256), 0, s, bp, lhp, rhp, B, body, lh, rh, valid,
+                       layout == RTG_LAYOUT_SOA);
     return hipGetLastError();
 }
 
@@ -1629,10 +1687,11 @@ hipError_t launch_quat_in_xyz_axis(const float *q, int s0, int s1, int s2, int e
 }
 
 hipError_t launch_synth_full_body(const TopoView &T, uint64_t seed, int64_t off, int64_t B, float *body, float *lh,
-                                  float *rh, float *body_rot, hipStream_t s)
+                                  float *rh, float *body_rot, int layout, hipStream_t s)
 {
     hipLaunchKernelGGL(k_synth_full_body, dim3(grid_for(B, 64)), dim3(64), 0, s, T, seed, off, B, body, lh, rh,
-                       body_rot);
+                       body_rot,
+                       layout == RTG_LAYOUT_SOA);
     return hipGetLastError();
 }
 

@@ -14,7 +14,11 @@ PKG_ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 LIB_PATH = os.environ.get("RTG_LIB", os.path.join(PKG_ROOT, "librtg_hip.so"))
 
 RTG_OK = 0
-ABI_VERSION = 1
+ABI_VERSION = 2
+
+# rtg_layout (input frame-batch layout of the solvers / producers)
+LAYOUT_AOS = 0
+LAYOUT_SOA = 1
 
 # rtg_solver_kind
 SOLVER_FULL_BODY_POS = 0
@@ -74,8 +78,8 @@ SIGNATURES = {
     "rtg_dof_model_create": (c_int, [c_void_p, POINTER(c_int32), POINTER(c_float), POINTER(c_float),
                                      POINTER(c_void_p)]),
     "rtg_dof_model_destroy": (c_int, [c_void_p]),
-    "rtg_ingest_vtrdyn_f32": (c_int, [c_void_p, c_void_p, c_void_p, c_int64, c_void_p, c_void_p, c_void_p, c_void_p,
-                                      c_void_p]),
+    "rtg_ingest_vtrdyn_f32": (c_int, [c_void_p, c_void_p, c_void_p, c_int64, c_int, c_void_p, c_void_p, c_void_p,
+                                      c_void_p, c_void_p]),
     "rtg_rescale_motion_f32": (c_int, [c_void_p, c_void_p, c_int64, POINTER(c_float), c_void_p, c_void_p]),
     "rtg_quat_between_f32": (c_int, [c_void_p, c_void_p, c_int64, c_void_p, c_void_p, c_void_p]),
     "rtg_rebuild_vtrdyn_f32": (c_int, [c_void_p, c_void_p, c_int64, c_void_p, c_void_p, c_void_p, c_void_p]),
@@ -83,8 +87,8 @@ SIGNATURES = {
     "rtg_solver_create": (c_int, [c_int, POINTER(c_float), POINTER(c_float), POINTER(c_int32), c_int32, c_int,
                                   POINTER(c_void_p)]),
     "rtg_solver_destroy": (c_int, [c_void_p]),
-    "rtg_retarget_f32": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int64, c_void_p, c_void_p,
-                                 c_void_p, c_void_p]),
+    "rtg_retarget_f32": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int64, c_int, c_void_p,
+                                 c_void_p, c_void_p, c_void_p]),
     "rtg_quat_op_f32": (c_int, [c_int, c_void_p, c_void_p, c_void_p, c_int64, c_void_p, c_void_p]),
     "rtg_cal_joint_quat_f32": (c_int, [c_void_p, c_void_p, c_int32, c_int64, c_void_p, c_void_p]),
     "rtg_quat_in_xyz_axis_f32": (c_int, [c_void_p, c_char_p, c_int64, c_void_p, c_void_p]),
@@ -92,8 +96,8 @@ SIGNATURES = {
                                         c_void_p, c_void_p]),
     "rtg_angular_velocity_f32": (c_int, [c_void_p, c_int64, c_int64, c_int64, c_float, c_void_p, c_int32, c_void_p,
                                          c_void_p, c_void_p]),
-    "rtg_synth_full_body_f32": (c_int, [c_void_p, c_uint64, c_int64, c_int64, c_void_p, c_void_p, c_void_p, c_void_p,
-                                        c_void_p]),
+    "rtg_synth_full_body_f32": (c_int, [c_void_p, c_uint64, c_int64, c_int64, c_int, c_void_p, c_void_p, c_void_p,
+                                        c_void_p, c_void_p]),
 }
 
 _lib = None

@@ -24,8 +24,8 @@ from typing import Any, Dict, Optional
 import numpy as np
 import torch
 
-from ._lib import check, lib
-from .runtime import dev_f32, ptr, stream_handle
+from ._lib import LAYOUT_SOA, check, lib
+from .runtime import dev_f32, layout_code, ptr, stream_handle
 from .safe_pickle import Call, Global, Obj, _run_vm
 
 # sim_full_body_teleop.py:109 (23 -> 21) and :111-112 (hand point order)
@@ -160,20 +160,23 @@ def get_vtrdyn_full_rotation(df) -> np.ndarray:
 
 
 # ---------------------------------------------------------------- batched device reindex
-def reindex_frames(body23, left20, right20):
+def reindex_frames(body23, left20, right20, layout="aos"):
     """(B,23,3), (B,20,3), (B,20,3) raw broadcast frames -> solver inputs (B,21,3), (B,20,3), (B,20,3) and a
-    (B,) bool "frame carries data" flag (not np.allclose(body_pos, 0)), gathered on the device."""
+    (B,) bool "frame carries data" flag (not np.allclose(body_pos, 0)), gathered on the device.  ``layout="soa"``
+    emits the solver inputs as component planes (21,3,B), (20,3,B), (20,3,B) directly (rtg.h rtg_layout)."""
     b = dev_f32(body23, (23, 3), "body_pos")
     lh = dev_f32(left20, (20, 3), "left_hand_pos")
     rh = dev_f32(right20, (20, 3), "right_hand_pos")
     B = int(b.shape[0])
     if lh.shape[0] != B or rh.shape[0] != B:
         raise ValueError("frame batches differ in length")
-    ob = torch.empty((B, 21, 3), device=b.device, dtype=torch.float32)
-    ol = torch.empty((B, 20, 3), device=b.device, dtype=torch.float32)
-    orr = torch.empty((B, 20, 3), device=b.device, dtype=torch.float32)
+    code = layout_code(layout)
+    soa = code == LAYOUT_SOA
+    ob = torch.empty((21, 3, B) if soa else (B, 21, 3), device=b.device, dtype=torch.float32)
+    ol = torch.empty((20, 3, B) if soa else (B, 20, 3), device=b.device, dtype=torch.float32)
+    orr = torch.empty((20, 3, B) if soa else (B, 20, 3), device=b.device, dtype=torch.float32)
     valid = torch.empty((B,), device=b.device, dtype=torch.uint8)
-    check(lib().rtg_ingest_vtrdyn_f32(ptr(b), ptr(lh), ptr(rh), B, ptr(ob), ptr(ol), ptr(orr), ptr(valid),
+    check(lib().rtg_ingest_vtrdyn_f32(ptr(b), ptr(lh), ptr(rh), B, code, ptr(ob), ptr(ol), ptr(orr), ptr(valid),
                                       stream_handle()))
     return ob, ol, orr, valid.bool()
 

@@ -13,7 +13,7 @@ import torch
 
 from . import _lib
 from ._lib import check, lib
-from .runtime import Topology, dev_f32, ptr, require_gpu, stream_handle
+from .runtime import Topology, dev_f32, layout_code, ptr, require_gpu, stream_handle
 
 
 def _flat(t: torch.Tensor, tail: int) -> torch.Tensor:
@@ -309,8 +309,13 @@ def forward_kinematics_multi(segments: Sequence[tuple]):
     for i, (topo, lr, rt) in enumerate(segments):
         J = topo.num_joints
         lr = dev_f32(lr, (J, 4), "local_rot")
+        if lr.dim() != 3:
+            raise ValueError(f"segment {i}: local_rot must be (B, {J}, 4), got {tuple(lr.shape)}")
         B = int(lr.shape[0])
         rt = dev_f32(rt, (3,), "root_t")
+        if rt.dim() > 2 or (rt.dim() == 2 and rt.shape[0] not in (1, B)):
+            raise ValueError(f"segment {i}: root_t must broadcast to ({B}, 3), got {tuple(rt.shape)}")
+        rt = rt.expand(B, 3).contiguous()   # a (3,) / (1,3) root translation is shared by every frame
         g_rot = torch.empty((B, J, 4), device=lr.device, dtype=torch.float32)
         g_pos = torch.empty((B, J, 3), device=lr.device, dtype=torch.float32)
         segs[i] = _lib.FkSegment(topo.handle.value, lr.data_ptr(), rt.data_ptr(), g_rot.data_ptr(), g_pos.data_ptr(), B)
@@ -370,16 +375,22 @@ def motion_angular_velocity(r, dt: float, smooth: bool = True):
 
 
 def synth_full_body(topo_full: Topology, B: int, seed: int = 1234, frame_offset: int = 0, want_rot: bool = False,
-                    out=None):
-    """Synthetic VTRDyn frames generated on the device (rtg_synth_full_body_f32)."""
+                    out=None, layout="aos"):
+    """Synthetic VTRDyn frames generated on the device (rtg_synth_full_body_f32), as (B,P,C) rows (``"aos"``)
+    or (P,C,B) component planes (``"soa"``)."""
     dev = require_gpu()
+    code = layout_code(layout)
+    shp = (lambda P, C: (P, C, B)) if code == _lib.LAYOUT_SOA else (lambda P, C: (B, P, C))
     if out is None:
-        body = torch.empty((B, 21, 3), device=dev, dtype=torch.float32)
-        lh = torch.empty((B, 20, 3), device=dev, dtype=torch.float32)
-        rh = torch.empty((B, 20, 3), device=dev, dtype=torch.float32)
+        body = torch.empty(shp(21, 3), device=dev, dtype=torch.float32)
+        lh = torch.empty(shp(20, 3), device=dev, dtype=torch.float32)
+        rh = torch.empty(shp(20, 3), device=dev, dtype=torch.float32)
     else:
         body, lh, rh = out
-    rot = torch.empty((B, 21, 4), device=dev, dtype=torch.float32) if want_rot else None
-    check(lib().rtg_synth_full_body_f32(topo_full.handle, ctypes.c_uint64(seed), frame_offset, B, ptr(body), ptr(lh),
-                                        ptr(rh), ptr(rot), stream_handle()))
+        for t, want in ((body, shp(21, 3)), (lh, shp(20, 3)), (rh, shp(20, 3))):
+            if tuple(t.shape) != want or not t.is_contiguous() or t.dtype != torch.float32:
+                raise ValueError(f"synth_full_body: output buffer {tuple(t.shape)} != {want}")
+    rot = torch.empty(shp(21, 4), device=dev, dtype=torch.float32) if want_rot else None
+    check(lib().rtg_synth_full_body_f32(topo_full.handle, ctypes.c_uint64(seed), frame_offset, B, code, ptr(body),
+                                        ptr(lh), ptr(rh), ptr(rot), stream_handle()))
     return (body, lh, rh, rot) if want_rot else (body, lh, rh)

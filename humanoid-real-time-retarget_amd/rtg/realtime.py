@@ -18,7 +18,7 @@ import torch
 from ._lib import check, lib
 from .runtime import Solver, ptr, require_gpu, stream_handle
 
-_IN_TAILS = {0: [(21, 3), (20, 3), (20, 3)], 1: [(21, 3)], 2: [(21, 4), (21, 3), (20, 3), (20, 3)], 3: [(21, 4)]}
+from .runtime import IN_TAILS as _IN_TAILS
 
 
 class FrameGraph:
@@ -56,7 +56,7 @@ class FrameGraph:
     def _step(self):
         self.d_in.copy_(self.h_in, non_blocking=True)
         ins: List = [ptr(t) for t in self._ins] + [None] * (4 - len(self._ins))
-        check(lib().rtg_retarget_f32(self.solver.handle, ins[0], ins[1], ins[2], ins[3], 1, ptr(self._dof),
+        check(lib().rtg_retarget_f32(self.solver.handle, ins[0], ins[1], ins[2], ins[3], 1, 0, ptr(self._dof),
                                      ptr(self._lr), ptr(self._br), stream_handle()))
         self.h_out.copy_(self.d_out, non_blocking=True)
 

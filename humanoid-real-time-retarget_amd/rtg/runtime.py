@@ -128,11 +128,26 @@ class DofModel:
             self._h = None
 
 
+# per-frame input rows of each solver kind (rtg.h rtg_solver_kind): (points, components)
+IN_TAILS = {_lib.SOLVER_FULL_BODY_POS: [(21, 3), (20, 3), (20, 3)], _lib.SOLVER_UPPER_BODY: [(21, 3)],
+            _lib.SOLVER_FULL_BODY_ROT: [(21, 4), (21, 3), (20, 3), (20, 3)], _lib.SOLVER_BODY_ROT: [(21, 4)]}
+LAYOUTS = {"aos": _lib.LAYOUT_AOS, "soa": _lib.LAYOUT_SOA}
+
+
+def layout_code(layout) -> int:
+    if isinstance(layout, str):
+        if layout not in LAYOUTS:
+            raise ValueError(f"layout must be one of {sorted(LAYOUTS)}, got {layout!r}")
+        return LAYOUTS[layout]
+    if int(layout) not in LAYOUTS.values():
+        raise ValueError(f"bad layout {layout!r}")
+    return int(layout)
+
+
 class Solver:
     """A retarget solver (``rtg_solver_t``) of one of the four reference kinds."""
 
-    N_INPUTS = {_lib.SOLVER_FULL_BODY_POS: 3, _lib.SOLVER_UPPER_BODY: 1, _lib.SOLVER_FULL_BODY_ROT: 4,
-                _lib.SOLVER_BODY_ROT: 1}
+    N_INPUTS = {k: len(v) for k, v in IN_TAILS.items()}
 
     def __init__(self, kind: int, src_local_t, src_global_t=None, src_parents=None, precise_gripper=False):
         require_gpu()
@@ -147,31 +162,49 @@ class Solver:
         self._h = h
         self.kind = int(kind)
         self.precise_gripper = bool(precise_gripper)
+        self.device = torch.device("cuda", torch.cuda.current_device())   # owns the angle table (rtg.h)
 
     @property
     def handle(self) -> ctypes.c_void_p:
         return self._h
 
     def retarget(self, inputs: Sequence[torch.Tensor], want_local_rot=False, want_body_rot=False,
-                 out_dof: Optional[torch.Tensor] = None, stream=None):
-        """Batched solve.  ``inputs``: device float32 tensors in the order of rtg.h.
+                 out_dof: Optional[torch.Tensor] = None, stream=None, layout="aos"):
+        """Batched solve.  ``inputs``: contiguous float32 tensors on the solver's device, in the order of rtg.h,
+        shaped (B, P, C) per IN_TAILS (``layout="aos"``, the reference's rows) or (P, C, B) (``"soa"``).
 
         Returns (dof (B,30), local_rot (B,31,4) | None, body_rot (B,59,4) | None).
         """
         n = self.N_INPUTS[self.kind]
         if len(inputs) != n:
             raise ValueError(f"solver kind {self.kind} takes {n} inputs, got {len(inputs)}")
-        B = int(inputs[0].shape[0])
-        for t in inputs:
-            if not (t.is_cuda and t.dtype == torch.float32 and t.is_contiguous()) or int(t.shape[0]) != B:
-                raise ValueError("inputs must be contiguous float32 device tensors with one batch size")
-        dev = inputs[0].device
-        dof = out_dof if out_dof is not None else torch.empty((B, 30), device=dev, dtype=torch.float32)
+        code = layout_code(layout)
+        tails = IN_TAILS[self.kind]
+        soa = code == _lib.LAYOUT_SOA
+        B = int(inputs[0].shape[-1] if soa else inputs[0].shape[0]) if inputs[0].dim() == 3 else -1
+        for i, (t, tail) in enumerate(zip(inputs, tails)):
+            want = tuple(tail) + (B,) if soa else (B,) + tuple(tail)
+            if not isinstance(t, torch.Tensor) or tuple(t.shape) != want:
+                raise ValueError(f"input {i}: expected shape {want} ({'SoA' if soa else 'AoS'}), got "
+                                 f"{tuple(t.shape) if isinstance(t, torch.Tensor) else type(t).__name__}")
+            if not (t.is_cuda and t.dtype == torch.float32 and t.is_contiguous()):
+                raise ValueError(f"input {i}: must be a contiguous float32 device tensor")
+            if t.device != self.device:
+                raise ValueError(f"input {i} is on {t.device}; this solver lives on {self.device}")
+        dev = self.device
+        if out_dof is not None:
+            if not (isinstance(out_dof, torch.Tensor) and tuple(out_dof.shape) == (B, 30) and
+                    out_dof.dtype == torch.float32 and out_dof.is_contiguous() and out_dof.device == dev):
+                raise ValueError(f"out_dof must be a contiguous float32 ({B}, 30) tensor on {dev}")
+            dof = out_dof
+        else:
+            dof = torch.empty((B, 30), device=dev, dtype=torch.float32)
         lr = torch.empty((B, 31, 4), device=dev, dtype=torch.float32) if want_local_rot else None
         br = torch.empty((B, 59, 4), device=dev, dtype=torch.float32) if want_body_rot else None
         ins = [ptr(t) for t in inputs] + [None] * (4 - n)
-        check(lib().rtg_retarget_f32(self._h, ins[0], ins[1], ins[2], ins[3], B, ptr(dof), ptr(lr), ptr(br),
-                                     stream_handle(stream)))
+        s = stream if stream is not None else torch.cuda.current_stream(dev)
+        check(lib().rtg_retarget_f32(self._h, ins[0], ins[1], ins[2], ins[3], B, code, ptr(dof), ptr(lr), ptr(br),
+                                     stream_handle(s)))
         return dof, lr, br
 
     def __del__(self):

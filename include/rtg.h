@@ -28,7 +28,7 @@
 extern "C" {
 #endif
 
-#define RTG_ABI_VERSION 1
+#define RTG_ABI_VERSION 2   /* 2: the input-layout argument of rtg_retarget_f32 / rtg_ingest_vtrdyn_f32 / rtg_synth_full_body_f32 */
 
 typedef enum rtg_status {
     RTG_OK = 0,
@@ -37,6 +37,12 @@ typedef enum rtg_status {
     RTG_ERR_OUT_OF_MEMORY = 3,
     RTG_ERR_UNSUPPORTED = 4
 } rtg_status;
+
+/* Frame-batch layout of solver inputs.  AOS: the reference's (B, P, C) rows (e.g. body
+ * (B,21,3)), what sim_full_body_teleop.py:109-119 hands over.  SOA: component planes (P, C, B) -- element
+ * (frame f, point j, component c) at [(j*C + c)*B + f] -- so a wavefront's load of one component of 64
+ * consecutive frames is one 256-byte contiguous read.  The batched producers (ingest, synth) emit either. */
+typedef enum rtg_layout { RTG_LAYOUT_AOS = 0, RTG_LAYOUT_SOA = 1 } rtg_layout;
 
 typedef struct rtg_topology_s *rtg_topology_t;
 typedef struct rtg_solver_s *rtg_solver_t;
@@ -113,9 +119,10 @@ int rtg_dof_fk_f32(rtg_dof_model_t model, const float *dof, const float *root_ro
  * ---------------------------------------------------------------------- */
 /* Raw broadcast frames body_pos (B,23,3), left/right_hand_pos (B,20,3) -> solver inputs body (B,21,3)
  * (23 -> 21 joint reindex), hands (B,20,3) (point reorder), and valid (B) uint8: 0 where every body value
- * is within 1e-8 of 0 (np.allclose(body_pos, 0): the teleop loop keeps the previous DOFs), else 1. */
+ * is within 1e-8 of 0 (np.allclose(body_pos, 0): the teleop loop keeps the previous DOFs), else 1.
+ * layout: of the outputs body / lh / rh (the raw inputs are the reference's rows). */
 int rtg_ingest_vtrdyn_f32(const float *body_pos, const float *left_hand, const float *right_hand, int64_t B,
-                          float *body, float *lh, float *rh, uint8_t *valid, rtg_stream_t stream);
+                          int layout, float *body, float *lh, float *rh, uint8_t *valid, rtg_stream_t stream);
 
 /* ------------------------------------------------------------------------
  * Motion-level prep of the legacy motion path (retarget/main.py)
@@ -170,9 +177,12 @@ int rtg_solver_destroy(rtg_solver_t solver);
 
 /* Batched retarget of B frames.  dof (B,30) required; local_rot (B,31,4) and
  * body_rot (B,59,4, FULL_BODY_POS only: the returned body_global_rotation) may
- * be NULL.  Unused in* must be NULL. */
+ * be NULL.  Unused in* must be NULL.  layout (rtg_layout) describes the inputs
+ * only; the outputs are always (B, ...) rows.  Replaces the per-frame
+ * .retarget calls of sim_full_body_teleop.py:115-119 / sim_teleop_mujoco.py:104-108
+ * / sim_teleop.py:102. */
 int rtg_retarget_f32(rtg_solver_t solver, const float *in0, const float *in1, const float *in2,
-                     const float *in3, int64_t B, float *dof, float *local_rot, float *body_rot,
+                     const float *in3, int64_t B, int layout, float *dof, float *local_rot, float *body_rot,
                      rtg_stream_t stream);
 
 /* ------------------------------------------------------------------------
@@ -232,10 +242,10 @@ int rtg_angular_velocity_f32(const float *r, int64_t nseq, int64_t L, int64_t J,
  * rotations, generated on the device from a counter-based RNG.
  * topo must be the 59-joint VTRDYN_FULL topology.  Frame f uses stream
  * (seed, frame_offset + f).  Outputs body (B,21,3), lh (B,20,3), rh (B,20,3)
- * and optionally body_rot (B,21,4).
+ * and optionally body_rot (B,21,4), in the given layout.
  * ---------------------------------------------------------------------- */
-int rtg_synth_full_body_f32(rtg_topology_t topo, uint64_t seed, int64_t frame_offset, int64_t B, float *body,
-                            float *lh, float *rh, float *body_rot, rtg_stream_t stream);
+int rtg_synth_full_body_f32(rtg_topology_t topo, uint64_t seed, int64_t frame_offset, int64_t B, int layout,
+                            float *body, float *lh, float *rh, float *body_rot, rtg_stream_t stream);
 
 #ifdef __cplusplus
 }

@@ -212,6 +212,34 @@ def quat_to_exp_map(q):
     return _unary("oracle_quat_to_exp_map", q, (len(q), 3))
 
 
+def quat_to_angle_axis(q):
+    """rotation3d.py:587-608 -> (n,4) [angle, axis xyz]."""
+    return _unary("oracle_quat_to_angle_axis", _c32(q).reshape(-1, 4), (int(np.size(q)) // 4, 4))
+
+
+def normalize_angle(x):
+    x = _c32(x).reshape(-1)
+    out = np.empty_like(x)
+    lib().oracle_normalize_angle(_fp(x), _i64(len(x)), _fp(out))
+    return out
+
+
+def quat_abs(q):
+    q = _c32(q).reshape(-1, 4)
+    out = np.empty(len(q), np.float32)
+    lib().oracle_quat_abs(_fp(q), _i64(len(q)), _fp(out))
+    return out
+
+
+def quat_unit(q):
+    return _unary("oracle_quat_unit", _c32(q).reshape(-1, 4), (int(np.size(q)) // 4, 4))
+
+
+def quat_angle_axis(q):
+    """rotation3d.py:230-240 -> (n,4) [angle, axis xyz]."""
+    return _unary("oracle_quat_angle_axis", _c32(q).reshape(-1, 4), (int(np.size(q)) // 4, 4))
+
+
 def quat_to_dof_pos(q31):
     q31 = _c32(q31)
     out = np.empty((q31.shape[0], 30), np.float32)

@@ -308,6 +308,27 @@ def test_kabsch_sgesdd_random_and_degenerate_vs_oracle(gpu):
         assert not bad.any(), (npts, int(bad.sum()), np.nonzero(bad)[0][:8])
 
 
+@pytest.mark.parametrize("name,inp", [("quat_to_exp_map", "em_q"), ("quat_to_angle_axis", "em_q"),
+                                      ("normalize_angle", "na_x"), ("quat_abs", "qa_q"), ("quat_unit", "qa_q"),
+                                      ("quat_angle_axis", "qaa_q")])
+def test_expmap_family_vs_oracle_and_reference(gpu, name, inp):
+    """RTG_OP 7, 13-17 (rotation3d.py:41-56, 230-240, 582-627) through rtg_quat_op_f32: bit-exact vs the oracle
+    on the golden inputs (w < 0, w = +-1, the 1e-5 sin_theta deadzone, w = 0.25 and its neighbours -- the angle
+    table's edge), and within VML's ulp of the reference."""
+    import oracle as orc
+    from rtg import ops
+    g = golden("expmap")
+    x = g[inp]
+    dev = ops.__dict__[name](x)
+    if isinstance(dev, tuple):
+        dev = torch.cat([dev[0].unsqueeze(-1), dev[1]], -1)
+    got = _np(dev).reshape(len(x), -1)
+    o = getattr(orc, name)(x).reshape(len(x), -1)
+    np.testing.assert_array_equal(got, o)
+    s = frame_stats(got, g[name].reshape(got.shape))
+    assert s["max"] <= 8e-7, s
+
+
 def test_proj_in_plane_and_reference(gpu):
     from rtg import ops
     p = golden("primitives")
@@ -408,6 +429,65 @@ def test_solver_batch_invariance(gpu, name, kind):
     dof_s, lr_s, _ = S.retarget(small, want_local_rot=True)
     dof_b, lr_b, _ = S.retarget(big, want_local_rot=True)
     assert torch.equal(dof_b, dof_s[idx]) and torch.equal(lr_b, lr_s[idx])
+
+
+def test_config2_batch4096_vs_oracle(gpu):
+    """BASELINE config 2: one 4096-frame batch (device-generated) through the drop-in batched path, every frame
+    bit-exact with the oracle."""
+    import oracle as orc
+    from rtg import _lib, ops
+    zp = golden("zero_pose")
+    body, lh, rh = ops.synth_full_body(_topo("vtrdyn_full"), 4096, seed=4096)
+    S = _solver(_lib.SOLVER_FULL_BODY_POS, True)
+    dof, _, _ = S.retarget([body, lh, rh])
+    odof, _, _ = orc.full_body_pos(zp["vtrdyn_full_local_t"], zp["vtrdyn_full_global_t"], _np(body), _np(lh),
+                                   _np(rh), True, want_rot=False)
+    np.testing.assert_array_equal(_np(dof), odof)
+
+
+@pytest.mark.parametrize("kind", [0, 1, 2, 3])
+def test_soa_layout_matches_aos(gpu, kind):
+    """RTG_LAYOUT_SOA inputs ((P, C, B) component planes) give the same bits as the reference's (B, P, C) rows,
+    for every solver kind; the synthetic producer emits SoA directly, bit-identical to its AoS output."""
+    from rtg import _lib, ops
+    T = _topo("vtrdyn_full")
+    B = 128 * 37 + 5
+    body, lh, rh, rot = ops.synth_full_body(T, B, seed=7, want_rot=True)
+    sb, sl, sr, srot = ops.synth_full_body(T, B, seed=7, want_rot=True, layout="soa")
+    for a, s in ((body, sb), (lh, sl), (rh, sr), (rot, srot)):
+        assert torch.equal(a.permute(1, 2, 0), s)
+    ins = {0: ([body, lh, rh], [sb, sl, sr]), 1: ([body], [sb]), 2: ([rot, body, lh, rh], [srot, sb, sl, sr]),
+           3: ([rot], [srot])}[kind]
+    S = _solver(kind, True) if kind == 0 else _solver(kind)
+    d_aos, lr_aos, _ = S.retarget(ins[0], want_local_rot=True)
+    d_soa, lr_soa, _ = S.retarget(ins[1], want_local_rot=True, layout="soa")
+    assert torch.equal(d_aos, d_soa) and torch.equal(lr_aos, lr_soa)
+
+
+def test_solver_rejects_bad_out_dof_and_device(gpu):
+    """out_dof must be a contiguous float32 (B,30) tensor on the solver's device."""
+    from rtg import _lib, ops
+    body, lh, rh = ops.synth_full_body(_topo("vtrdyn_full"), 64, seed=1)
+    S = _solver(_lib.SOLVER_FULL_BODY_POS, True)
+    for bad in (torch.empty(64, 29, device="cuda"), torch.empty(64, 30, device="cuda", dtype=torch.float64),
+                torch.empty(30, 64, device="cuda").t(), torch.empty(64, 30)):
+        with pytest.raises(ValueError):
+            S.retarget([body, lh, rh], out_dof=bad)
+    with pytest.raises(ValueError):
+        S.retarget([body.cpu(), lh.cpu(), rh.cpu()])
+
+
+def test_ingest_soa_matches_aos(gpu):
+    from rtg import ingest
+    rng = np.random.default_rng(3)
+    B = 1000
+    b23 = rng.standard_normal((B, 23, 3)).astype(np.float32)
+    l20, r20 = (rng.standard_normal((B, 20, 3)).astype(np.float32) for _ in range(2))
+    a = ingest.reindex_frames(b23, l20, r20)
+    s = ingest.reindex_frames(b23, l20, r20, layout="soa")
+    for x, y in zip(a[:3], s[:3]):
+        assert torch.equal(x.permute(1, 2, 0), y)
+    assert torch.equal(a[3], s[3])
 
 
 def test_solver_full_size_properties(gpu):

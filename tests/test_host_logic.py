@@ -54,7 +54,7 @@ def test_solver_and_op_validation():
     assert lib.rtg_quat_in_xyz_axis_f32(None, b"XXZ", 1, None, None) == 1          # repeated axis
     assert lib.rtg_quat_op_f32(99, None, None, None, 1, None, None) == 1
     assert lib.rtg_cal_joint_quat_f32(None, None, 9, 1, None, None) == 4
-    assert lib.rtg_retarget_f32(None, None, None, None, None, 1, None, None, None, None) == 1
+    assert lib.rtg_retarget_f32(None, None, None, None, None, 1, 0, None, None, None, None) == 1
 
 
 def test_dof_model_validation():
@@ -121,3 +121,40 @@ def test_synthetic_generator_deterministic():
     for x, y in zip(a, b):
         np.testing.assert_array_equal(x, y)
     assert a[0].shape == (8, 21, 3) and a[1].shape == (8, 20, 3) and a[0].dtype == np.float32
+
+
+def _fake_solver(kind):
+    """A Solver shell (no device handle) to exercise the host-side argument checks without a GPU."""
+    import torch
+    from rtg.runtime import Solver
+    s = Solver.__new__(Solver)
+    s._h, s.kind, s.precise_gripper, s.device = None, kind, True, torch.device("cuda", 0)
+    return s
+
+
+def test_solver_rejects_bad_input_shapes():
+    """trailing shapes are checked against the kind's rows before anything reaches the C ABI (which
+    cannot see shapes): a raw (B,23,3) broadcast body, short hands, mismatched batches, a bad layout."""
+    import torch
+    from rtg import _lib
+    s = _fake_solver(_lib.SOLVER_FULL_BODY_POS)
+    B = 4
+    good = [torch.zeros(B, 21, 3), torch.zeros(B, 20, 3), torch.zeros(B, 20, 3)]
+    cases = [
+        [torch.zeros(B, 23, 3), good[1], good[2]],           # raw 23-joint broadcast body
+        [good[0], torch.zeros(B, 19, 3), good[2]],            # short hand
+        [good[0], good[1], torch.zeros(B + 1, 20, 3)],        # batch mismatch
+        [good[0], good[1]],                                   # missing input
+    ]
+    for ins in cases:
+        with pytest.raises(ValueError):
+            s.retarget(ins)
+    with pytest.raises(ValueError):
+        s.retarget(good, layout="planar")
+    with pytest.raises(ValueError):   # AoS tensors handed over as SoA
+        s.retarget(good, layout="soa")
+    with pytest.raises(ValueError):   # CPU tensors of the right shape: not device tensors
+        s.retarget(good)
+    r = _fake_solver(_lib.SOLVER_FULL_BODY_ROT)
+    with pytest.raises(ValueError):   # rotations need 4 components
+        r.retarget([torch.zeros(B, 21, 3), torch.zeros(B, 21, 3), torch.zeros(B, 20, 3), torch.zeros(B, 20, 3)])

@@ -231,6 +231,23 @@ def test_full_body_pos_with_reference_kabsch_injected():
     assert s["frac_frames_gt_1e5"] <= 0.02 and s["max"] <= 1e-4 and s["exact_elems"] >= 0.8, s
 
 
+EXPMAP_CASES = [("quat_to_exp_map", "em_q"), ("quat_to_angle_axis", "em_q"), ("normalize_angle", "na_x"),
+                 ("quat_abs", "qa_q"), ("quat_unit", "qa_q"), ("quat_angle_axis", "qaa_q")]
+
+
+@pytest.mark.parametrize("name,inp", EXPMAP_CASES)
+def test_expmap_family_vs_reference(name, inp):
+    """rotation3d.py's exp-map family (tests/golden/expmap.npz, edge cases incl. w < 0, w = +-1, the sin_theta
+    deadzone, w = 0.25): bit-exact where no VML transcendental is involved (quat_abs, quat_unit), otherwise
+    within VML's ulp (<= 3 ulp of pi)."""
+    g = golden("expmap")
+    got = getattr(orc, name)(g[inp])
+    want = g[name].reshape(got.shape)
+    s = frame_stats(got, want)
+    exact_ops = ("quat_abs", "quat_unit")
+    assert s["max"] <= (0.0 if name in exact_ops else 8e-7) and s["exact_elems"] >= (1.0 if name in exact_ops else 0.9), s
+
+
 def test_rotation_test_kat():
     """retarget/rotation_test.py:95-152 known-answer test restated."""
     k = golden("kat_rotation_test")

@@ -16,6 +16,7 @@ Fixtures (all float32 unless noted):
   primitives.npz             per-primitive vectors incl. edge cases
   kat_rotation_test.npz      retarget/rotation_test.py known-answer test, restated
   zero_pose.npz              zero-pose global translations as the reference computes them
+  expmap.npz                 the rotation3d exp-map family (quat_to_exp_map ... quat_angle_axis) with edge cases
 """
 from __future__ import annotations
 
@@ -328,6 +329,55 @@ def gen_primitives(ref, torch):
     return out
 
 
+def gen_expmap(ref, torch):
+    """quat_to_exp_map / quat_to_angle_axis / normalize_angle / quat_abs / quat_unit / quat_angle_axis
+    (rotation3d.py:41-56, 230-240, 582-627), called on chunks of 16 like the reference's per-frame use (torch
+    takes glibc's scalar atan2f below 32 elements).  Edge cases: w < 0, w = +-1, the 1e-5 sin_theta deadzone,
+    the angle table's w = 0.25 boundary, angles at +-pi, zero / tiny quaternions."""
+    r3 = ref.rotation3d
+    rng = np.random.default_rng(17)
+    n = 2048
+    q = _rand_quats(rng, n)
+    q[: n // 4] *= -1.0                                             # w < 0
+    w_edge = np.float32([1.0, -1.0, 0.0, 0.25, np.nextafter(np.float32(0.25), np.float32(0)),
+                         np.nextafter(np.float32(0.25), np.float32(1)), np.float32(1) - np.float32(2 ** -24),
+                         np.float32(1) - np.float32(2 ** -23), 0.9999999, 0.99999994, 1 - 5e-11, 1 - 1e-10,
+                         0.5, -0.5, 0.70710677, 0.9999, 0.999999])
+    m = len(w_edge)
+    ax = rng.standard_normal((m, 3)).astype(np.float32)
+    ax /= np.linalg.norm(ax, axis=1, keepdims=True)
+    s = np.sqrt(np.maximum(0.0, 1.0 - w_edge.astype(np.float64) ** 2)).astype(np.float32)
+    q[n // 4: n // 4 + m] = np.concatenate([ax * s[:, None], w_edge[:, None]], 1)
+    tiny = rng.standard_normal((64, 3)).astype(np.float32) * np.float32(3e-6)    # |xyz| around the deadzone
+    q[n // 2: n // 2 + 64] = np.concatenate([tiny, np.sqrt(1 - (tiny ** 2).sum(1, keepdims=True))], 1)
+    out = {"em_q": q}
+    chunks = [torch.from_numpy(q[i:i + 16]) for i in range(0, n, 16)]
+    out["quat_to_exp_map"] = np.concatenate([t2n(r3.quat_to_exp_map(c)) for c in chunks])
+    aa = [r3.quat_to_angle_axis(c) for c in chunks]
+    out["quat_to_angle_axis"] = np.concatenate([np.concatenate([t2n(a)[:, None], t2n(x)], 1) for a, x in aa])
+    x = np.concatenate([rng.uniform(-10, 10, 1536), np.float32([0.0, -0.0, np.pi, -np.pi, 2 * np.pi, 3 * np.pi,
+                                                                1e-7, -1e-7, 7.0, -7.0])]).astype(np.float32)
+    x = np.concatenate([x, rng.uniform(-10, 10, (-len(x)) % 16).astype(np.float32)])
+    out["na_x"] = x
+    out["normalize_angle"] = np.concatenate([t2n(r3.normalize_angle(torch.from_numpy(x[i:i + 16])))
+                                             for i in range(0, len(x), 16)])
+    g = _rand_quats(rng, 512) * rng.uniform(1e-3, 3.0, (512, 1)).astype(np.float32)
+    g[:4] = 0.0
+    g[4:8] *= np.float32(1e-10)                                     # below the 1e-9 clamp
+    out["qa_q"] = g
+    out["quat_abs"] = np.concatenate([t2n(r3.quat_abs(torch.from_numpy(g[i:i + 16]))) for i in range(0, 512, 16)])
+    out["quat_unit"] = np.concatenate([t2n(r3.quat_unit(torch.from_numpy(g[i:i + 16]))) for i in range(0, 512, 16)])
+    u = _rand_quats(rng, 512)
+    u[:2] = np.float32([[0, 0, 0, 1], [0, 0, 0, -1]])
+    out["qaa_q"] = u
+    res = []
+    for i in range(0, 512, 16):
+        a, xyz = r3.quat_angle_axis(torch.from_numpy(u[i:i + 16].copy()))   # the reference divides in place
+        res.append(np.concatenate([t2n(a)[:, None], t2n(xyz)], 1))
+    out["quat_angle_axis"] = np.concatenate(res)
+    return out
+
+
 def gen_kat(ref, torch):
     """retarget/rotation_test.py:95-152 restated as data: arm segments from known joint angles."""
     r3 = ref.rotation3d
@@ -378,6 +428,7 @@ def main() -> None:
         "kat_rotation_test": lambda: gen_kat(ref, torch),
         "dof_fk": lambda: gen_dof_fk(ref, torch, 128),
         "motion_prep": lambda: gen_motion_prep(ref, torch),
+        "expmap": lambda: gen_expmap(ref, torch),
     }
     only = set(sys.argv[1:])
     for name, fn in jobs.items():
