@@ -235,3 +235,55 @@ def test_per_frame_graph_matches_batched(gpu):
         np.testing.assert_array_equal(lr.numpy(), lr_b[i].numpy())
         np.testing.assert_array_equal(br.numpy(), br_b[i].numpy())
     assert hu.motion_length == n
+
+
+def test_main_retarget_from_global_translation(gpu):
+    """retarget/main.py RetargetHuV5fromMocap.retarget_from_global_translation (:169-279), unchanged call, against
+    the reference run end to end (tests/golden/main_retarget.npz, plot_skeleton_H captured) and against the oracle
+    composition of the same chain: coord_transform + rescale -> rebuild -> SkeletonState FK of the rebuilt motion
+    -> the arm maps on its rotation 10 and translations (quat_mul_three parent) -> SkeletonState(is_local=True)."""
+    import oracle as orc
+    import retarget.main as M
+    from robot_kinematics_model import RobotZeroPose
+    from rtg import assets, ops
+    g = golden("main_retarget")
+    zv, hu = RobotZeroPose.from_asset("vtrdyn"), RobotZeroPose.from_asset("hu_v5")
+    got = []
+    hook = M.plot_skeleton_H
+    M.plot_skeleton_H = lambda motions, *a, **k: got.extend(motions)
+    try:
+        r = M.RetargetHuV5fromMocap(zv, hu).retarget_from_global_translation(torch.from_numpy(g["x"]))
+    finally:
+        M.plot_skeleton_H = hook
+    assert r is None and len(got) == 2
+    mocap, robot = got
+    # oracle composition
+    par, zl = assets.parents("vtrdyn"), golden("zero_pose")["vtrdyn_local_t"]
+    tq = assets.tree_quat("vtrdyn")
+    x = orc.rescale_motion(par, zl, g["x"], dir=[-1.0, -1.0, 1.0])
+    gr, rt = orc.rebuild_vtrdyn(par, zl, x)
+    _, gp = orc.state_fk(par, tq, zl, orc.state_local_rotation(par, tq, gr), rt)
+    np.testing.assert_array_equal(mocap.global_rotation.numpy(), gr)
+    np.testing.assert_array_equal(mocap.global_translation.numpy(), gp)
+    L = len(gr)
+    lr = np.tile(np.float32([0, 0, 0, 1]), (L, 31, 1))
+    for links, (sh, el, wr) in (((12, 13, 14, 15), (18, 19, 20)), ((21, 22, 23, 24), (14, 15, 16))):
+        pr = orc.shoulder_pr(gp[:, el] - gp[:, sh], np.tile(zl[el], (L, 1)), gr[:, 10])
+        parent = orc.quat_mul(orc.quat_mul(gr[:, 10], pr[:, 0]), pr[:, 1])
+        ye = orc.elbow_py(gp[:, wr] - gp[:, el], np.tile(zl[wr], (L, 1)), parent)
+        for link, q in zip(links, (pr[:, 0], pr[:, 1], ye[:, 0], ye[:, 1])):
+            lr[:, link] = q
+    lr = orc.quat_normalize(lr.reshape(-1, 4)).reshape(L, 31, 4)
+    np.testing.assert_array_equal(robot.local_rotation.numpy(), lr)
+    hpar, htq, hzl = assets.parents("hu_v5"), assets.tree_quat("hu_v5"), assets.local_translation("hu_v5")
+    ogr, ogp = orc.state_fk(hpar, htq, hzl, lr, np.zeros((L, 3), np.float32))
+    np.testing.assert_array_equal(robot.global_rotation.numpy(), ogr)
+    np.testing.assert_array_equal(robot.global_translation.numpy(), ogp)
+    w, _ = ops.gaussian_taps()
+    np.testing.assert_array_equal(robot.global_velocity.numpy(), orc.linear_velocity(ogp, 1 / 30, w))
+    # against the reference itself: the mocap side is bit-exact but for VML sqrt's ulp in the Kabsch rows; the
+    # arm angles carry VML's acos/sin/cos ulps
+    assert frame_stats(mocap.global_rotation.numpy(), g["mocap_g_rot"])["max"] <= 6e-8
+    s = frame_stats(robot.local_rotation.numpy(), g["robot_local_rot"])
+    assert s["max"] <= 2e-5 and s["exact_elems"] >= 0.9, s
+    assert frame_stats(robot.global_translation.numpy(), g["robot_g_pos"])["max"] <= 2e-5

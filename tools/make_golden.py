@@ -16,6 +16,7 @@ Fixtures (all float32 unless noted):
   primitives.npz             per-primitive vectors incl. edge cases
   kat_rotation_test.npz      retarget/rotation_test.py known-answer test, restated
   zero_pose.npz              zero-pose global translations as the reference computes them
+  main_retarget.npz          retarget/main.py retarget_from_global_translation end to end (48 frames)
   expmap.npz                 the rotation3d exp-map family (quat_to_exp_map ... quat_angle_axis) with edge cases
 """
 from __future__ import annotations
@@ -201,6 +202,32 @@ def gen_motion_prep(ref, torch, L=64):
     qb0 = ref.transform3d.quat_between_two_vecs(torch.from_numpy(v1[:4]), torch.zeros(4, 3))
     return {"raw": x, "rescaled": t2n(rescaled), "g_rot": t2n(motion.global_rotation),
             "root_t": t2n(motion.root_translation), "qb_v1": v1, "qb_v2": v2, "qb": t2n(qb), "qb_zero": t2n(qb0)}
+
+
+def gen_main_retarget(ref, torch, L=48):
+    """retarget/main.py RetargetHuV5fromMocap.retarget_from_global_translation (:169-279), the reference's own
+    code end to end: coord_transform -> rescale -> _rebuild_with_vtrdyn_zero_pose -> the per-frame arm maps on
+    the rebuilt motion -> SkeletonState(is_local=True) -> SkeletonMotion(fps=30).  Its last call,
+    plot_skeleton_H([mocap_motion, retargeted_motion]) (:280), is replaced by a capture of those two motions.
+    The target is Hu v5 from its pickled zero pose (asset/hu/hu_v5.urdf is not shipped)."""
+    main = rh.load_main_module(ref)
+    zv = rh.ref_zero_pose(ref, "vtrdyn")
+    hu = rh.ref_zero_pose(ref, "hu_v5")
+    x = synth.synth_upper_body_inputs(L, 5151)
+    g = np.random.default_rng(5152)
+    x = (x * g.uniform(0.8, 1.25, (L, 1, 1)) + g.normal(0, 0.01, x.shape)).astype(np.float32)
+    captured = []
+    main.plot_skeleton_H = lambda motions, *a, **k: captured.extend(motions)
+    import contextlib
+    import io
+    with contextlib.redirect_stdout(io.StringIO()):                  # it prints per-frame timings
+        main.RetargetHuV5fromMocap(zv, hu).retarget_from_global_translation(torch.from_numpy(x))
+    mocap, robot = captured
+    return {"x": x, "mocap_g_rot": t2n(mocap.global_rotation), "mocap_g_pos": t2n(mocap.global_translation),
+            "mocap_local_rot": t2n(mocap.local_rotation), "robot_local_rot": t2n(robot.local_rotation),
+            "robot_g_rot": t2n(robot.global_rotation), "robot_g_pos": t2n(robot.global_translation),
+            "robot_velocity": t2n(robot.global_velocity), "robot_angular_velocity": t2n(robot.global_angular_velocity),
+            "fps": np.array(robot.fps)}
 
 
 def _rand_quats(rng, n):
@@ -429,6 +456,7 @@ def main() -> None:
         "dof_fk": lambda: gen_dof_fk(ref, torch, 128),
         "motion_prep": lambda: gen_motion_prep(ref, torch),
         "expmap": lambda: gen_expmap(ref, torch),
+        "main_retarget": lambda: gen_main_retarget(ref, torch),
     }
     only = set(sys.argv[1:])
     for name, fn in jobs.items():
