@@ -57,12 +57,16 @@ def dist_setup(args):
     return world, rank, local
 
 
-def barrier(world):
-    import torch
+def barrier(world, backend=None):
+    """Barrier + device synchronise on both sides of the timed region."""
     if world > 1:
         import torch.distributed as dist
         dist.barrier()
-    torch.cuda.synchronize()
+    if backend is not None:
+        backend.sync()
+    else:
+        import torch
+        torch.cuda.synchronize()
 
 
 def cpu_share() -> int:
@@ -161,7 +165,7 @@ def pmc_traffic(B):
 def secondary_configs(solver, sets, stream):
     """BASELINE configs 2 and 5 on the same GPU (reported beside the headline line, not as `value`):
     config 2 = 4096 frames per launch (latency-bound regime), kernel-only and PCIe-inclusive (pinned host
-    frames in, DOFs back); config 5 = FK of 4 robot_config skeletons x 65536 frames in one launch."""
+    frames in, DOFs back); config 5 = FK plus inverse FK of 4 robot_config skeletons x 65536 frames, one launch."""
     import torch
     from rtg import assets, ops, synth
     from rtg.runtime import Topology
@@ -192,24 +196,27 @@ def secondary_configs(solver, sets, stream):
     e2e_ms = (time.perf_counter() - t0) * 1e3 / 50
     out["config2_batch4096"] = {"kernel_ms": k_ms, "frames_per_s": n / (k_ms * 1e-3), "e2e_pcie_ms": e2e_ms,
                                 "e2e_pcie_frames_per_s": n / (e2e_ms * 1e-3)}
-    segs, nbytes = [], 0
+    fk, inv, nbytes = [], [], 0
     for i, name in enumerate(["hu_v5", "vtrdyn", "vtrdyn_full", "noitom"]):
         t = Topology(assets.parents(name), assets.local_translation(name), assets.tree_quat(name))
         J = t.num_joints
-        segs.append((t, torch.from_numpy(synth.random_local_quats(65536, J, 10 + i)).cuda(),
-                     torch.zeros((65536, 3), device="cuda")))
-        nbytes += 65536 * (J * 16 + 12 + J * 28)
+        lr = torch.from_numpy(synth.random_local_quats(65536, J, 10 + i)).cuda()
+        fk.append((t, lr, torch.zeros((65536, 3), device="cuda")))
+        nbytes += 65536 * (J * 16 + 12 + J * 28)        # FK: local rotations + root in, rotations + positions out
+        inv.append((t, ops.forward_kinematics(t, lr, torch.zeros((65536, 3), device="cuda"))[0]))
+        nbytes += 65536 * (J * 16 + J * 16)             # inverse FK: global rotations in, local rotations out
     for _ in range(5):
-        ops.forward_kinematics_multi(segs)
+        ops.kinematics_multi(fk, inv)
     e0.record(stream)
     for _ in range(50):
-        ops.forward_kinematics_multi(segs)
+        ops.kinematics_multi(fk, inv)
     e1.record(stream)
     e1.synchronize()
     ms = e0.elapsed_time(e1) / 50
-    out["config5_mixed_fk_4x65536"] = {"kernel_ms": ms, "frames_per_s": 4 * 65536 / (ms * 1e-3),
-                                       "GBs_algorithmic": nbytes / (ms * 1e-3) / 1e9,
-                                       "hbm_frac": nbytes / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS}
+    out["config5_mixed_fk_and_inverse_4x65536"] = {
+        "kernel_ms": ms, "frames_per_s": 4 * 65536 / (ms * 1e-3), "GBs_algorithmic": nbytes / (ms * 1e-3) / 1e9,
+        "hbm_frac": nbytes / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS,
+        "launch": "rtg_kinematics_multi_f32: 4 FK + 4 inverse-FK segments in one launch"}
     return out
 
 
@@ -265,70 +272,124 @@ def parity_vs_reference():
     return out
 
 
+def source_setup():
+    """Rank 0's inputs to the setup broadcast: the VTRDYN_FULL source skeleton (parents, local translations,
+    tree quaternions) from the package assets."""
+    from rtg import assets
+    return (assets.parents("vtrdyn_full"), assets.local_translation("vtrdyn_full"), assets.tree_quat("vtrdyn_full"))
+
+
+class DeviceBackend:
+    """The product path of one rank: librtg_hip.so on this rank's GPU (RCCL for the collectives)."""
+
+    def __init__(self, dev):
+        import torch
+        self.torch = torch
+        self.dev = dev
+        self.comm_device = dev
+        self.stream = torch.cuda.current_stream()
+
+    def zero_global(self, parents, lt, tq):
+        """The source zero pose's global translations (SkeletonState FK of the identity pose, on the device)."""
+        from rtg import ops
+        from rtg.runtime import Topology
+        T = Topology(parents, lt, tq)
+        J = len(parents)
+        ident = self.torch.tensor([[0, 0, 0, 1.0]]).expand(1, J, 4)
+        return ops.forward_kinematics(T, ident, self.torch.zeros(1, 3), state=True)[1][0].cpu().numpy()
+
+    def build(self, parents, lt, tq, zg):
+        from rtg import _lib
+        from rtg.runtime import Solver, Topology
+        return Topology(parents, lt, tq), Solver(_lib.SOLVER_FULL_BODY_POS, lt, zg, parents, precise_gripper=True)
+
+    def synth(self, topo, B, seed, offset):
+        from rtg import ops
+        return ops.synth_full_body(topo, B, seed=seed, frame_offset=offset)
+
+    def new_dof(self, B):
+        return self.torch.empty((B, 30), device=self.dev, dtype=self.torch.float32)
+
+    def solve(self, solver, b, l, r, d):
+        solver.retarget([b, l, r], out_dof=d)
+
+    def sync(self):
+        self.torch.cuda.synchronize()
+
+    def start(self):
+        # kernel time: one HIP event pair around the K launches on the launch stream (a pair per launch would add
+        # each event's own packet and cache release to every launch, ~10 us, which rocprofv3's trace does not see)
+        self._e0 = self.torch.cuda.Event(enable_timing=True)
+        self._e1 = self.torch.cuda.Event(enable_timing=True)
+        self._e0.record(self.stream)
+
+    def stop(self):
+        self._e1.record(self.stream)
+
+    def elapsed_ms(self):
+        self._e1.synchronize()
+        return self._e0.elapsed_time(self._e1)
+
+
+def rank_flow(world, rank, backend, B, steps, warmup, ring):
+    """One rank of the bench: setup broadcast -> own shard of B frames generated locally (seed
+    1234 + rank) -> K timed solves between barriers -> max over ranks -> untimed DOF gather to rank 0."""
+    from rtg import shard
+    setup = None
+    if rank == 0:
+        parents, lt, tq = source_setup()
+        setup = (parents, lt, tq, backend.zero_global(parents, lt, tq))
+    if world > 1:   # topology + zero pose from rank 0: the other ranks read no assets
+        parents, lt, tq, zg = shard.broadcast_setup(setup, max_joints=64, device=backend.comm_device)
+    else:
+        parents, lt, tq, zg = setup
+    topo, solver = backend.build(parents, lt, tq, zg)
+    sets = []
+    for r in range(ring):
+        b, l, r_ = backend.synth(topo, B, 1234 + rank, r * B)
+        sets.append((b, l, r_, backend.new_dof(B)))
+    backend.sync()
+    for i in range(warmup):
+        b, l, r_, d = sets[i % ring]
+        backend.solve(solver, b, l, r_, d)
+    barrier(world, backend)
+    t0 = time.perf_counter()
+    backend.start()
+    for i in range(steps):
+        b, l, r_, d = sets[i % ring]
+        backend.solve(solver, b, l, r_, d)
+    backend.stop()
+    barrier(world, backend)
+    wall = time.perf_counter() - t0
+    kern_ms = backend.elapsed_ms() / max(1, steps)
+    if world > 1:
+        wall = shard.max_over_ranks(wall, backend.comm_device)
+    out = {"wall": wall, "kern_ms": kern_ms, "frames": world * B * steps, "sets": sets, "topo": topo,
+           "solver": solver, "zl": lt, "zg": zg, "parents": parents}
+    if world > 1:   # final DOF gather to rank 0 (untimed region, reported separately)
+        d = sets[(steps - 1) % ring][3]
+        backend.sync()
+        tg = time.perf_counter()
+        out["gathered"] = shard.gather_shards(d, [B] * world, dst=0)
+        backend.sync()
+        out["gather_ms"] = (time.perf_counter() - tg) * 1e3
+    return out
+
+
 def main():
     args = parse()
     import torch
     world, rank, local = dist_setup(args)
-    from rtg import _lib, assets, ops
-    from rtg.runtime import Solver, Topology
-
     B = args.batch
     dev = torch.device("cuda", local)
-    # solver constants: rank 0 owns the zero pose; RCCL broadcast to the other ranks (setup, untimed)
-    from rtg import shard
-    topo_full = Topology(assets.parents("vtrdyn_full"), assets.local_translation("vtrdyn_full"),
-                         assets.tree_quat("vtrdyn_full"))
-    zl = zg = None
-    if rank == 0:
-        zl = torch.from_numpy(assets.local_translation("vtrdyn_full")).to(dev)
-        zg = ops.forward_kinematics(topo_full, torch.tensor([[0, 0, 0, 1.0]]).expand(1, 59, 4),
-                                    torch.zeros(1, 3), state=True)[1][0].to(dev)
-    if world > 1:
-        zl, zg = shard.broadcast_solver_consts(zl, zg, max_joints=64, device=dev)
-    solver = Solver(_lib.SOLVER_FULL_BODY_POS, zl.cpu().numpy(), zg.cpu().numpy(), assets.parents("vtrdyn_full"),
-                    precise_gripper=True)
-
+    backend = DeviceBackend(dev)
     bytes_per_set = B * (63 + 60 + 60 + 30) * 4
     ring = args.ring or max(2, int(np.ceil(2 * 256 * 2**20 / bytes_per_set)))
-    sets = []
-    for r in range(ring):
-        body, lh, rh = ops.synth_full_body(topo_full, B, seed=1234 + rank, frame_offset=r * B)
-        dof = torch.empty((B, 30), device=dev, dtype=torch.float32)
-        sets.append((body, lh, rh, dof))
-    torch.cuda.synchronize()
-
-    stream = torch.cuda.current_stream()
-    for i in range(args.warmup):
-        b, l, r_, d = sets[i % ring]
-        solver.retarget([b, l, r_], out_dof=d)
-    barrier(world)
-    # kernel time: one HIP event pair around the K launches on the launch stream (a pair per launch would add each
-    # event's own packet and cache release to every launch, ~10 us, which rocprofv3's kernel trace does not see)
-    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    t0 = time.perf_counter()
-    ev0.record(stream)
-    for i in range(args.steps):
-        b, l, r_, d = sets[i % ring]
-        solver.retarget([b, l, r_], out_dof=d)
-    ev1.record(stream)
-    barrier(world)
-    wall = time.perf_counter() - t0
-    kern_ms = ev0.elapsed_time(ev1) / args.steps
-    if world > 1:
-        wall = shard.max_over_ranks(wall, dev)
-    frames = world * B * args.steps
-    value = frames / wall
+    res = rank_flow(world, rank, backend, B, args.steps, args.warmup, ring)
+    wall, kern_ms = res["wall"], res["kern_ms"]
+    value = res["frames"] / wall
     ms_per_step = wall * 1e3 / args.steps
-
-    gather_ms = None
-    if world > 1:   # final DOF gather to rank 0 over RCCL (untimed region, reported separately)
-        d = sets[(args.steps - 1) % ring][3]
-        torch.cuda.synchronize()
-        tg = time.perf_counter()
-        shard.gather_shards(d, [B] * world, dst=0)
-        torch.cuda.synchronize()
-        gather_ms = (time.perf_counter() - tg) * 1e3
-
+    stream = backend.stream
     if rank == 0:
         achieved = BYTES_PER_FRAME * B / (kern_ms * 1e-3) / 1e9
         line = {
@@ -343,16 +404,17 @@ def main():
                          "kernel": "k_solve_sides<FULL_BODY_POS>", "kernel_ms": kern_ms,
                          "bytes_per_frame": BYTES_PER_FRAME, "traffic_unit": "bytes/launch (rocprofv3 PMC)"},
         }
-        if gather_ms is not None:
-            line["gather_ms"] = gather_ms
+        if "gather_ms" in res:
+            line["gather_ms"] = res["gather_ms"]
         if world == 1:
+            solver, sets = res["solver"], res["sets"]
             try:
                 line["secondary"] = secondary_configs(solver, sets, stream)
             except Exception as e:  # noqa: BLE001
                 line["secondary"] = {"error": repr(e)}
             try:
                 del sets[1:]
-                line["secondary"]["config3_soa_layout"] = soa_line(solver, topo_full, B, rank, ring, args.steps,
+                line["secondary"]["config3_soa_layout"] = soa_line(solver, res["topo"], B, rank, ring, args.steps,
                                                                    stream)
             except Exception as e:  # noqa: BLE001
                 line["secondary"]["config3_soa_layout"] = {"error": repr(e)}
@@ -361,10 +423,11 @@ def main():
         except Exception as e:  # noqa: BLE001
             line["parity_vs_reference"] = {"error": repr(e)}
         if world == 1 and not args.no_cpu_baseline:
-            b, l, r_, _ = sets[0]
+            b, l, r_, _ = res["sets"][0]
             n = min(B, 65536)
             line["cpu_baseline"] = cpu_baseline(b[:n].cpu().numpy(), l[:n].cpu().numpy(), r_[:n].cpu().numpy(),
-                                                zl.cpu().numpy(), zg.cpu().numpy(), args.cpu_seconds)
+                                                np.asarray(res["zl"], np.float32), np.asarray(res["zg"], np.float32),
+                                                args.cpu_seconds)
         print(json.dumps(line), flush=True)
     if world > 1:
         import torch.distributed as dist

@@ -224,10 +224,41 @@ int rtg_fk_multi_f32(const rtg_fk_segment *segs, int32_t n, rtg_stream_t stream)
         const rtg_fk_segment &s = segs[i];
         int rc = check_fk(s.topo, s.local_rot, s.root_t, s.g_rot, s.g_pos, s.B, "rtg_fk_multi_f32");
         if (rc != RTG_OK) return rc;
-        A.seg[i] = FkSeg{s.topo->view(), s.local_rot, s.root_t, s.g_rot, s.g_pos, s.B};
+        A.seg[i] = FkSeg{s.topo->view(), s.local_rot, s.root_t, s.g_rot, s.g_pos, s.B, 0};
     }
     RTG_TRY(launch_fk_multi(A, as_stream(stream)), "k_fk_multi");
     return RTG_OK;
+}
+
+int rtg_kinematics_multi_f32(const rtg_fk_segment *fk, int32_t n_fk, const rtg_local_rotation_segment *inv,
+                             int32_t n_inv, rtg_stream_t stream)
+{
+    if (n_fk < 0 || n_inv < 0 || n_fk + n_inv > RTG_MAX_SEGMENTS)
+        return fail(RTG_ERR_INVALID_ARGUMENT, "rtg_kinematics_multi_f32: %d + %d segments (max %d in total)", n_fk,
+                    n_inv, RTG_MAX_SEGMENTS);
+    if ((n_fk > 0 && !fk) || (n_inv > 0 && !inv))
+        return fail(RTG_ERR_INVALID_ARGUMENT, "rtg_kinematics_multi_f32: NULL segments");
+    FkMultiArgs A{};
+    A.n = n_fk + n_inv;
+    for (int i = 0; i < n_fk; ++i) {
+        const rtg_fk_segment &s = fk[i];
+        int rc = check_fk(s.topo, s.local_rot, s.root_t, s.g_rot, s.g_pos, s.B, "rtg_kinematics_multi_f32");
+        if (rc != RTG_OK) return rc;
+        A.seg[i] = FkSeg{s.topo->view(), s.local_rot, s.root_t, s.g_rot, s.g_pos, s.B, 0};
+    }
+    for (int i = 0; i < n_inv; ++i) {
+        const rtg_local_rotation_segment &s = inv[i];
+        int rc = check_fk(s.topo, s.g_rot, s.local_rot, s.g_rot, s.local_rot, s.B, "rtg_kinematics_multi_f32");
+        if (rc != RTG_OK) return rc;
+        A.seg[n_fk + i] = FkSeg{s.topo->view(), s.g_rot, nullptr, s.local_rot, nullptr, s.B, 1};
+    }
+    RTG_TRY(launch_fk_multi(A, as_stream(stream)), "k_fk_multi");
+    return RTG_OK;
+}
+
+int rtg_local_rotation_multi_f32(const rtg_local_rotation_segment *segs, int32_t n, rtg_stream_t stream)
+{
+    return rtg_kinematics_multi_f32(nullptr, 0, segs, n, stream);
 }
 
 // ---------------------------------------------------------------- joint-angle forward model

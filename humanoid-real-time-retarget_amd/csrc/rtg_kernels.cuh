@@ -48,11 +48,12 @@ struct DofView {
 
 struct FkSeg {
     TopoView T;
-    const float *local_rot;
-    const float *root_t;
-    float *g_rot;
-    float *g_pos;
+    const float *local_rot;   // op 1 (inverse FK): the global rotations in
+    const float *root_t;      // op 1: unused
+    float *g_rot;             // op 1: the local rotations out
+    float *g_pos;             // op 1: unused
     int64_t B;
+    int32_t op;               // 0: FK (kinematics.py:13-39), 1: inverse FK (kinematics.py:41-63)
 };
 struct FkMultiArgs {
     FkSeg seg[RTG_MAX_SEGMENTS];

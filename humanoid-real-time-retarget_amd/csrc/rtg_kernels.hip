@@ -681,7 +681,18 @@ static_assert(kFkChunk == 4 || kFkChunk == 8, "window of 4 or 8 joints");
 constexpr int kRotPitch = 4 * (kFkChunk + 1);   // floats per frame row (LDS)
 constexpr int kPosPitch = 3 * kFkChunk + 1;
 
+#ifndef RTG_FK_POS_REGS
+#define RTG_FK_POS_REGS 1   // 1 (measured +3-4 %, bit-exact): positions held in registers and staged through the rotation window after it is
+                            //    stored (no separate position window: 12.8 instead of 19.2 KiB per wave)
+#endif
+constexpr int kPosWin = RTG_FK_POS_REGS ? 0 : kFkTile * kPosPitch;   // floats of the separate position window
+
 static inline size_t fk_stream_lds_bytes(int nslots)
+{
+    return sizeof(float) * ((size_t)kFkTile * kRotPitch + (size_t)kPosWin + (size_t)nslots * 7 * kFkTile);
+}
+// k_dof_fk keeps its separate position window whatever RTG_FK_POS_REGS says
+static inline size_t dof_fk_lds_bytes(int nslots)
 {
     return sizeof(float) * ((size_t)kFkTile * (kRotPitch + kPosPitch) + (size_t)nslots * 7 * kFkTile);
 }
@@ -779,12 +790,13 @@ RTG_DEV void fk_stream_tile(const TopoView &T, const float *__restrict__ local_r
     const int J = T.J;
     const int nfr = (int)((B - f0) < kFkTile ? (B - f0) : kFkTile);
     float *rot = lds;                                   // [64][kRotPitch]
-    float *pos = lds + kFkTile * kRotPitch;             // [64][kPosPitch]
-    float *slots = pos + kFkTile * kPosPitch;           // [nslots][7][64]
+    float *pos = lds + kFkTile * kRotPitch;             // [64][kPosPitch] (RTG_FK_POS_REGS: none)
+    float *slots = pos + kPosWin;                       // [nslots][7][64]
     const int lane = threadIdx.x;
     const bool active = lane < nfr;
     Q g = qident();
     V t = V{0.0f, 0.0f, 0.0f};
+    V pk[kFkChunk];   // RTG_FK_POS_REGS: the window's positions (constant indices: registers)
     const V root = ld3(root_t + (f0 + (active ? lane : 0)) * 3);   // before the prefetches (vmcnt order)
     ChunkRegs next;
     chunk_load(next, local_rot, f0, nfr, J, 0, J < kFkChunk ? J : kFkChunk);
@@ -819,7 +831,8 @@ RTG_DEV void fk_stream_tile(const TopoView &T, const float *__restrict__ local_r
                     nt = V{rv.x + t.x, rv.y + t.y, rv.z + t.z};
                 }
                 R[4 * k] = ng.x; R[4 * k + 1] = ng.y; R[4 * k + 2] = ng.z; R[4 * k + 3] = ng.w;
-                P[3 * k] = nt.x; P[3 * k + 1] = nt.y; P[3 * k + 2] = nt.z;
+                if (RTG_FK_POS_REGS) pk[k] = nt;
+                else { P[3 * k] = nt.x; P[3 * k + 1] = nt.y; P[3 * k + 2] = nt.z; }
                 if (((sc >> 8) & 0xFF) != kNoSlot) slot_put(slots, (sc >> 8) & 0xFF, ng, nt);
                 g = ng;
                 t = nt;
@@ -827,7 +840,19 @@ RTG_DEV void fk_stream_tile(const TopoView &T, const float *__restrict__ local_r
         }
         wave_sync();
         chunk_store<4>(g_rot, rot, kRotPitch, f0, nfr, J, c0, nC);
-        chunk_store<3>(g_pos, pos, kPosPitch, f0, nfr, J, c0, nC);
+        if (RTG_FK_POS_REGS) {   // the rotation rows are out: reuse the window for the positions
+            wave_sync();
+            if (active) {
+                float *P = rot + lane * kRotPitch;
+#pragma unroll
+                for (int k = 0; k < kFkChunk; ++k)
+                    if (k < nC) { P[3 * k] = pk[k].x; P[3 * k + 1] = pk[k].y; P[3 * k + 2] = pk[k].z; }
+            }
+            wave_sync();
+            chunk_store<3>(g_pos, rot, kRotPitch, f0, nfr, J, c0, nC);
+        } else {
+            chunk_store<3>(g_pos, pos, kPosPitch, f0, nfr, J, c0, nC);
+        }
         wave_sync();
     }
 }
@@ -844,15 +869,13 @@ __global__ __launch_bounds__(kFkTile) void k_fk_stream(TopoView T, const float *
 // inverse FK, streamed the same way: local[j] = normalise(conj(g[p]) * g[j]) (kinematics.py:41-63).
 // The previous joint's global rotation stays in registers; branch parents come from slots.
 template <bool STATE>
-__global__ __launch_bounds__(kFkTile) void k_local_rotation_stream(TopoView T, const float *__restrict__ g_rot,
-                                                                   int64_t B, float *__restrict__ local_rot)
+RTG_DEV void local_rotation_tile(const TopoView &T, const float *__restrict__ g_rot, int64_t B, int64_t f0,
+                                 float *__restrict__ local_rot, float *fk_lds)
 {
-    extern __shared__ __attribute__((aligned(16))) float fk_lds[];
     const int J = T.J;
-    const int64_t f0 = (int64_t)blockIdx.x * kFkTile;
     const int nfr = (int)((B - f0) < kFkTile ? (B - f0) : kFkTile);
     float *win = fk_lds;                                 // [64][kRotPitch]
-    float *slots = fk_lds + kFkTile * (kRotPitch + kPosPitch);
+    float *slots = fk_lds + kFkTile * kRotPitch + kPosWin;   // the same slot offset as fk_stream_tile
     const int lane = threadIdx.x;
     Q prev = qident();
     V unused = V{0.0f, 0.0f, 0.0f};
@@ -891,6 +914,16 @@ __global__ __launch_bounds__(kFkTile) void k_local_rotation_stream(TopoView T, c
     }
 }
 
+template <bool STATE>
+__global__ __launch_bounds__(kFkTile) void k_local_rotation_stream(TopoView T, const float *__restrict__ g_rot,
+                                                                   int64_t B, float *__restrict__ local_rot)
+{
+    extern __shared__ __attribute__((aligned(16))) float fk_lds[];
+    local_rotation_tile<STATE>(T, g_rot, B, (int64_t)blockIdx.x * kFkTile, local_rot, fk_lds);
+}
+
+// Mixed-target kinematics (BASELINE config 5): every 64-frame tile of every segment is one wave; a segment is FK
+// (op 0) or inverse FK (op 1), so FK and inverse FK of several skeletons share one launch.
 __global__ __launch_bounds__(kFkTile) void k_fk_multi_stream(FkMultiArgs A)
 {
     extern __shared__ __attribute__((aligned(16))) float fk_lds[];
@@ -899,8 +932,9 @@ __global__ __launch_bounds__(kFkTile) void k_fk_multi_stream(FkMultiArgs A)
     for (int i = 1; i < RTG_MAX_SEGMENTS; ++i)
         if (i < A.n && (int64_t)blockIdx.x >= A.block_start[i]) s = i;
     const FkSeg &S = A.seg[s];
-    fk_stream_tile<false>(S.T, S.local_rot, S.root_t, S.B, ((int64_t)blockIdx.x - A.block_start[s]) * kFkTile,
-                          S.g_rot, S.g_pos, fk_lds);
+    const int64_t f0 = ((int64_t)blockIdx.x - A.block_start[s]) * kFkTile;
+    if (S.op == 0) fk_stream_tile<false>(S.T, S.local_rot, S.root_t, S.B, f0, S.g_rot, S.g_pos, fk_lds);
+    else local_rotation_tile<false>(S.T, S.local_rot, S.B, f0, S.g_rot, fk_lds);
 }
 
 // Joint-angle FK (HuForwardModel.forward_kinematics, hu_forward_model.py:17-33): the streaming tile of
@@ -1222,8 +1256,15 @@ __global__ __launch_bounds__(256) void k_fk_multi(FkMultiArgs A)
     const FkSeg &S = A.seg[s];
     const int64_t f = ((int64_t)blockIdx.x - A.block_start[s]) * blockDim.x + threadIdx.x;
     if (f >= S.B) return;
-    fk_frame<false>(S.T, S.local_rot + f * S.T.J * 4, S.root_t + f * 3, S.g_rot + f * S.T.J * 4,
-                    S.g_pos + f * S.T.J * 3);
+    if (S.op == 0) {
+        fk_frame<false>(S.T, S.local_rot + f * S.T.J * 4, S.root_t + f * 3, S.g_rot + f * S.T.J * 4,
+                        S.g_pos + f * S.T.J * 3);
+        return;
+    }
+    const float *g = S.local_rot + f * S.T.J * 4;   // inverse FK, kinematics.py:41-63
+    float *l = S.g_rot + f * S.T.J * 4;
+    st4(l, ld4(g));
+    for (int j = 1; j < S.T.J; ++j) st4(l + 4 * j, qmul_norm(qconj(ld4(g + 4 * S.T.parents[j])), ld4(g + 4 * j)));
 }
 
 // ----------------------------------------------------------------------------
@@ -1615,7 +1656,7 @@ hipError_t launch_dof_fk(const TopoView &T, const DofView &D, bool clip, const f
 {
     if (T.nslots > kMaxFkSlots) return hipErrorInvalidValue;   // rejected at rtg_dof_model_create
     const dim3 g(grid_for(B, kFkTile)), b(kFkTile);
-    const size_t lds = fk_stream_lds_bytes(T.nslots);
+    const size_t lds = dof_fk_lds_bytes(T.nslots);
     if (clip) hipLaunchKernelGGL(k_dof_fk<true>, g, b, lds, s, T, D, dof, root_rot, root_t, B, gr, gp);
     else hipLaunchKernelGGL(k_dof_fk<false>, g, b, lds, s, T, D, dof, root_rot, root_t, B, gr, gp);
     return hipGetLastError();

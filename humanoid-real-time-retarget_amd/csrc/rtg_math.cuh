@@ -876,8 +876,16 @@ RTG_DEV void la_gesdd3(float a[9], Svd3 &z)
 }
 // transform3d.py:40-45: R = U Vt ((p0 + p1) + p2, torch's bmm order); det(R) < 0 -> Vt[-1,:] *= -1; R = U Vt.
 // A and R row-major.  det only decides a sign (|det| = 1 up to rounding), taken in float64.
+#ifndef RTG_EXP_STUB_SVD
+#define RTG_EXP_STUB_SVD 0   // measurement knob (tools/build_variants.sh): R = identity-ish, wrong answers
+#endif
 RTG_DEV void kabsch_rot(const float A[9], float R[9])
 {
+#if RTG_EXP_STUB_SVD
+#pragma unroll
+    for (int i = 0; i < 9; ++i) R[i] = (i % 4 == 0) ? 1.0f : A[i] * 1e-3f;
+    return;
+#endif
     float a[9];
 #pragma unroll
     for (int i = 0; i < 3; ++i)

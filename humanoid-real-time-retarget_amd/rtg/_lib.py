@@ -62,6 +62,10 @@ class FkSegment(ctypes.Structure):
                 ("g_pos", c_void_p), ("B", c_int64)]
 
 
+class LocalRotationSegment(ctypes.Structure):
+    _fields_ = [("topo", c_void_p), ("g_rot", c_void_p), ("local_rot", c_void_p), ("B", c_int64)]
+
+
 # name -> (restype, argtypes); every symbol rtg.h declares
 SIGNATURES = {
     "rtg_abi_version": (c_int, []),
@@ -75,6 +79,9 @@ SIGNATURES = {
     "rtg_state_fk_f32": (c_int, [c_void_p, c_void_p, c_void_p, c_int64, c_void_p, c_void_p, c_void_p]),
     "rtg_state_local_rotation_f32": (c_int, [c_void_p, c_void_p, c_int64, c_void_p, c_void_p]),
     "rtg_fk_multi_f32": (c_int, [POINTER(FkSegment), c_int32, c_void_p]),
+    "rtg_local_rotation_multi_f32": (c_int, [POINTER(LocalRotationSegment), c_int32, c_void_p]),
+    "rtg_kinematics_multi_f32": (c_int, [POINTER(FkSegment), c_int32, POINTER(LocalRotationSegment), c_int32,
+                                         c_void_p]),
     "rtg_dof_model_create": (c_int, [c_void_p, POINTER(c_int32), POINTER(c_float), POINTER(c_float),
                                      POINTER(c_void_p)]),
     "rtg_dof_model_destroy": (c_int, [c_void_p]),

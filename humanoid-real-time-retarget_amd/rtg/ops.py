@@ -325,6 +325,54 @@ def forward_kinematics_multi(segments: Sequence[tuple]):
     return outs
 
 
+def _inv_segments(segments):
+    segs = (_lib.LocalRotationSegment * max(1, len(segments)))()
+    keep, outs = [], []
+    for i, (topo, g) in enumerate(segments):
+        J = topo.num_joints
+        g = dev_f32(g, (J, 4), "g_rot")
+        if g.dim() != 3:
+            raise ValueError(f"segment {i}: g_rot must be (B, {J}, 4), got {tuple(g.shape)}")
+        out = torch.empty_like(g)
+        segs[i] = _lib.LocalRotationSegment(topo.handle.value, g.data_ptr(), out.data_ptr(), int(g.shape[0]))
+        keep.append(g)
+        outs.append(out)
+    return segs, keep, outs
+
+
+def local_rotation_multi(segments: Sequence[tuple]):
+    """One launch of cal_local_rotation (kinematics.py:41-63) over several (topology, g_rot (B,J,4)) segments."""
+    require_gpu()
+    if len(segments) > _lib.MAX_SEGMENTS:
+        raise ValueError(f"at most {_lib.MAX_SEGMENTS} segments per launch")
+    segs, keep, outs = _inv_segments(segments)
+    check(lib().rtg_local_rotation_multi_f32(segs, len(segments), stream_handle()))
+    return outs
+
+
+def kinematics_multi(fk_segments: Sequence[tuple], inv_segments: Sequence[tuple]):
+    """FK segments (topology, local_rot, root_t) and inverse-FK segments (topology, g_rot) in ONE launch
+    (BASELINE config 5).  Returns ([(g_rot, g_pos)...], [local_rot...])."""
+    require_gpu()
+    if len(fk_segments) + len(inv_segments) > _lib.MAX_SEGMENTS:
+        raise ValueError(f"at most {_lib.MAX_SEGMENTS} segments per launch")
+    fsegs = (_lib.FkSegment * max(1, len(fk_segments)))()
+    keep, fouts = [], []
+    for i, (topo, lr, rt) in enumerate(fk_segments):
+        J = topo.num_joints
+        lr = dev_f32(lr, (J, 4), "local_rot")
+        B = int(lr.shape[0])
+        rt = dev_f32(rt, (3,), "root_t").expand(B, 3).contiguous()
+        g_rot = torch.empty((B, J, 4), device=lr.device, dtype=torch.float32)
+        g_pos = torch.empty((B, J, 3), device=lr.device, dtype=torch.float32)
+        fsegs[i] = _lib.FkSegment(topo.handle.value, lr.data_ptr(), rt.data_ptr(), g_rot.data_ptr(), g_pos.data_ptr(), B)
+        keep += [lr, rt]
+        fouts.append((g_rot, g_pos))
+    isegs, ikeep, iouts = _inv_segments(inv_segments)
+    check(lib().rtg_kinematics_multi_f32(fsegs, len(fk_segments), isegs, len(inv_segments), stream_handle()))
+    return fouts, iouts
+
+
 def gaussian_taps(sigma: float = 2.0, truncate: float = 4.0):
     """scipy.ndimage.gaussian_filter1d's taps (float64), as the reference applies them (sigma 2)."""
     import numpy as np

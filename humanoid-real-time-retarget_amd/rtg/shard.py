@@ -64,6 +64,50 @@ def broadcast_solver_consts(zero_local_t: Optional[torch.Tensor], zero_global_t:
     return unpack_solver_consts(buf[:1 + 6 * js])
 
 
+def pack_setup(parents, local_t, tree_quat, zero_global_t) -> torch.Tensor:
+    """Everything a rank needs to build its topology and solver, as one float32 blob:
+    [J, parents (J, exact small integers), local_t (J*3), tree_quat (J*4), zero_global_t (J*3)]."""
+    p = torch.as_tensor(parents).reshape(-1)
+    J = int(p.numel())
+    lt, tq, zg = (torch.as_tensor(x).reshape(J, k).float() for x, k in ((local_t, 3), (tree_quat, 4), (zero_global_t, 3)))
+    if int(p.min()) < -1 or int(p.max()) >= J:
+        raise ValueError("parent indices out of range")
+    dev = lt.device
+    return torch.cat([torch.tensor([float(J)], device=dev), p.float().to(dev), lt.reshape(-1), tq.to(dev).reshape(-1),
+                      zg.to(dev).reshape(-1)])
+
+
+def unpack_setup(blob: torch.Tensor):
+    """-> (parents int32 (J,), local_t (J,3), tree_quat (J,4), zero_global_t (J,3)) as numpy arrays."""
+    import numpy as np
+    b = blob.detach().cpu()
+    J = int(b[0].item())
+    if b.numel() != 1 + 11 * J:
+        raise ValueError("malformed setup blob")
+    o = 1
+    parents = b[o:o + J].numpy().astype(np.int32); o += J
+    lt = b[o:o + 3 * J].reshape(J, 3).numpy(); o += 3 * J
+    tq = b[o:o + 4 * J].reshape(J, 4).numpy(); o += 4 * J
+    zg = b[o:o + 3 * J].reshape(J, 3).numpy()
+    return parents, lt, tq, zg
+
+
+def broadcast_setup(setup: Optional[tuple], max_joints: int, device: torch.device):
+    """Rank 0 holds (parents, local_t, tree_quat, zero_global_t) of the source skeleton; one broadcast gives every
+    rank the same four arrays, so non-root ranks need no local assets (the topology broadcast)."""
+    import torch.distributed as dist
+    cap = 1 + 11 * max_joints
+    buf = torch.zeros(cap, dtype=torch.float32, device=device)
+    if dist.get_rank() == 0:
+        blob = pack_setup(*setup).to(device)
+        if blob.numel() > cap:
+            raise ValueError(f"skeleton has more than {max_joints} joints")
+        buf[:blob.numel()] = blob
+    dist.broadcast(buf, src=0)
+    J = int(buf[0].item())
+    return unpack_setup(buf[:1 + 11 * J])
+
+
 def max_over_ranks(x: float, device: torch.device) -> float:
     """The bench clock: the slowest rank's elapsed time."""
     import torch.distributed as dist

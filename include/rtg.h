@@ -96,6 +96,19 @@ typedef struct rtg_fk_segment {
     int64_t B;
 } rtg_fk_segment;
 int rtg_fk_multi_f32(const rtg_fk_segment *segments, int32_t n_segments, rtg_stream_t stream);
+/* Mixed-target inverse FK (cal_local_rotation, kinematics.py:41-63): up to RTG_MAX_SEGMENTS (topology, batch)
+ * segments in one launch. */
+typedef struct rtg_local_rotation_segment {
+    rtg_topology_t topo;
+    const float *g_rot;     /* (B,J,4) */
+    float *local_rot;       /* (B,J,4) */
+    int64_t B;
+} rtg_local_rotation_segment;
+int rtg_local_rotation_multi_f32(const rtg_local_rotation_segment *segments, int32_t n_segments, rtg_stream_t stream);
+/* FK segments and inverse-FK segments together in ONE launch (BASELINE config 5: "FK plus inverse FK" on the
+ * four robot_config skeletons); n_fk + n_inv <= RTG_MAX_SEGMENTS. */
+int rtg_kinematics_multi_f32(const rtg_fk_segment *fk, int32_t n_fk, const rtg_local_rotation_segment *inv,
+                             int32_t n_inv, rtg_stream_t stream);
 
 /* ------------------------------------------------------------------------
  * Joint-angle forward model: HuForwardModel (robot_kinematics_model/

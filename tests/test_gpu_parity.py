@@ -61,6 +61,31 @@ def test_fk_multi_one_launch_bit_exact(gpu):
         np.testing.assert_array_equal(_np(gp), k[f"{n}_g_pos"])
 
 
+def test_kinematics_multi_fk_and_inverse_one_launch(gpu):
+    """BASELINE config 5 as one launch: FK of the four robot_config skeletons plus inverse FK of the four
+    (rtg_kinematics_multi_f32), and inverse FK alone (rtg_local_rotation_multi_f32): bit-exact vs the reference's
+    goldens, ragged batch sizes, every segment independent."""
+    import oracle as orc
+    from rtg import assets, ops, synth
+    k = golden("kinematics")
+    fk = [(_topo(n), k[f"{n}_local_rot"], k[f"{n}_root_t"]) for n in TOPOS]
+    inv = [(_topo(n), k[f"{n}_g_rot"]) for n in TOPOS]
+    fouts, iouts = ops.kinematics_multi(fk, inv)
+    for n, (gr, gp), loc in zip(TOPOS, fouts, iouts):
+        np.testing.assert_array_equal(_np(gr), k[f"{n}_g_rot"])
+        np.testing.assert_array_equal(_np(gp), k[f"{n}_g_pos"])
+        np.testing.assert_array_equal(_np(loc), k[f"{n}_inv_local"])
+    sizes = [1, 63, 65, 1000]
+    segs = []
+    for n, B in zip(TOPOS, sizes):
+        segs.append((_topo(n), synth.random_local_quats(B, len(assets.parents(n)), B)))
+    outs = ops.local_rotation_multi(segs)
+    for n, (t, g), o in zip(TOPOS, segs, outs):
+        np.testing.assert_array_equal(_np(o), orc.local_rotation(assets.parents(n), g))
+    with pytest.raises(ValueError):
+        ops.kinematics_multi(fk * 2, inv)
+
+
 def test_fk_large_batch_vs_oracle(gpu):
     import oracle as orc
     from rtg import assets, ops, synth

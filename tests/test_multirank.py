@@ -129,3 +129,93 @@ def test_sharded_solve_matches_single_rank():
     ref, _, _ = orc.full_body_pos(zp["vtrdyn_full_local_t"], zp["vtrdyn_full_global_t"], body, lh, rh, True,
                                   want_rot=False)
     np.testing.assert_array_equal(res[0], ref)
+
+
+class HostBackend:
+    """bench.DeviceBackend's interface with the oracle standing in for the device launch (gloo, CPU tensors):
+    exercises bench.rank_flow -- the bench's own N>1 flow -- without a GPU."""
+
+    def __init__(self):
+        self.comm_device = torch.device("cpu")
+
+    def zero_global(self, parents, lt, tq):
+        import oracle as orc
+        J = len(parents)
+        _, gp = orc.state_fk(parents, tq, lt, np.tile(np.float32([0, 0, 0, 1]), (1, J, 1)), np.zeros((1, 3), np.float32))
+        return gp[0]
+
+    def build(self, parents, lt, tq, zg):
+        return ("topo", np.asarray(parents)), ("solver", np.asarray(lt, np.float32), np.asarray(zg, np.float32))
+
+    def synth(self, topo, B, seed, offset):
+        from rtg import synth
+        return tuple(torch.from_numpy(a) for a in synth.synth_full_body_inputs(B, seed=seed * 1000 + offset))
+
+    def new_dof(self, B):
+        return torch.empty((B, 30), dtype=torch.float32)
+
+    def solve(self, solver, b, l, r, d):
+        import oracle as orc
+        dof, _, _ = orc.full_body_pos(solver[1], solver[2], b.numpy(), l.numpy(), r.numpy(), True, want_rot=False)
+        d.copy_(torch.from_numpy(dof))
+
+    def sync(self):
+        pass
+
+    def start(self):
+        self._t = 0.0
+
+    def stop(self):
+        pass
+
+    def elapsed_ms(self):
+        return 1.0
+
+
+def _bench_flow(rank, world):
+    import bench
+    from rtg import assets
+    if rank != 0:   # non-root ranks must get the skeleton from the broadcast, not from local assets
+        def _no_assets(*a, **k):
+            raise AssertionError("rank > 0 read a local asset")
+        for name in ("parents", "local_translation", "tree_quat"):
+            setattr(assets, name, _no_assets)
+    res = bench.rank_flow(world, rank, HostBackend(), B=23, steps=3, warmup=1, ring=2)
+    g = res.get("gathered")
+    return {"gathered": None if g is None else g.numpy(), "wall": res["wall"], "frames": res["frames"],
+            "zg": np.asarray(res["zg"]), "parents": np.asarray(res["parents"])}
+
+
+def test_bench_rank_flow_world2():
+    """bench.py's N>1 flow (rank_flow) at world 2 over gloo with a host stand-in for the device launch: the setup
+    broadcast carries the topology (rank 1 reads no assets), each rank solves its own seeded shard, the clock is
+    the max over ranks, and rank 0's gather equals solving both shards on one rank."""
+    import oracle as orc
+    from rtg import assets, synth
+    res = _run(_bench_flow)
+    assert res[0]["wall"] == res[1]["wall"] and res[0]["frames"] == res[1]["frames"] == 2 * 23 * 3
+    np.testing.assert_array_equal(res[0]["parents"], assets.parents("vtrdyn_full"))
+    np.testing.assert_array_equal(res[1]["parents"], assets.parents("vtrdyn_full"))
+    np.testing.assert_array_equal(res[0]["zg"], res[1]["zg"])
+    np.testing.assert_array_equal(res[0]["zg"], np.load(os.path.join(os.path.dirname(__file__), "golden",
+                                                                     "zero_pose.npz"))["vtrdyn_full_global_t"])
+    assert res[1]["gathered"] is None
+    zg, zl = res[0]["zg"], assets.local_translation("vtrdyn_full")
+    want = []
+    for rank in (0, 1):   # the last timed step used ring set (3 - 1) % 2 = 0: frame offset 0
+        b, l, r = synth.synth_full_body_inputs(23, seed=(1234 + rank) * 1000)
+        want.append(orc.full_body_pos(zl, zg, b, l, r, True, want_rot=False)[0])
+    np.testing.assert_array_equal(res[0]["gathered"], np.concatenate(want))
+
+
+def test_setup_blob_roundtrip():
+    from rtg import assets
+    p, lt, tq = assets.parents("vtrdyn_full"), assets.local_translation("vtrdyn_full"), assets.tree_quat("vtrdyn_full")
+    zg = np.arange(177, dtype=np.float32).reshape(59, 3)
+    a, b, c, d = shard.unpack_setup(shard.pack_setup(p, lt, tq, zg))
+    np.testing.assert_array_equal(a, p)
+    np.testing.assert_array_equal(b, lt)
+    np.testing.assert_array_equal(c, tq)
+    np.testing.assert_array_equal(d, zg)
+    with pytest.raises(ValueError):
+        shard.pack_setup(np.int32([-1, 0, 5]), lt[:3], tq[:3], zg[:3])
