@@ -148,18 +148,35 @@ def cpu_baseline(body, lh, rh, zl, zg, seconds):
     return out
 
 
-def pmc_traffic(B):
-    """HBM bytes per k_solve_sides<FULL_BODY_POS> launch from the committed rocprofv3 FETCH_SIZE + WRITE_SIZE passes
-    (profiles/pmc_traffic.json, written by tools/pmc_summary.py), when they were taken at this batch.  rocprofv3's
-    grid counts threads: two per frame (one wave per side of each 64-frame tile)."""
-    path = os.path.join(REPO, "profiles", "pmc_traffic.json")
+PMC_JSON = os.path.join(REPO, "profiles", "pmc_r02.json")
+PMC_KERNEL = "rtg::k_solve_sides<0, true, false>"
+VALU_PEAK_LANE_OPS = 256 * 4 * 32 * 2.4e9   # MI355X: CUs x SIMDs x lanes issued per cycle x 2.4 GHz (78.6 T/s)
+
+
+def pmc_record(B):
+    """The committed rocprofv3 PMC summary of the headline kernel (tools/profile_round.sh -> tools/pmc_summary.py),
+    when it was taken at this batch (rocprofv3's grid counts threads: two per frame, one wave per side)."""
     try:
-        rec = json.load(open(path)).get("rtg::k_solve_sides<0, true>")
+        rec = json.load(open(PMC_JSON)).get(PMC_KERNEL)
     except (OSError, ValueError):
         return None
     if not rec or rec.get("grid") != 2 * B:
         return None
-    return rec["traffic_bytes"]
+    return rec
+
+
+def compute_roofline(rec, kern_ms):
+    """VALU side of the roofline: the kernel's VALU instructions per launch (SQ_INSTS_VALU, PMC) x 64 lanes over the
+    measured kernel time, against the 78.6 T lane-op/s issue peak; `frac_issue_weighted` charges f64 ops 2 issue
+    slots and transcendentals 4 (f32) / 8 (f64) -- the cycle cost the kernel actually pays."""
+    if not rec or "valu_insts" not in rec:
+        return None
+    t = kern_ms * 1e-3
+    achieved = rec["valu_insts"] * 64 / t
+    return {"bound": "valu", "achieved": achieved / 1e12, "peak": VALU_PEAK_LANE_OPS / 1e12, "unit": "T lane-ops/s",
+            "frac": achieved / VALU_PEAK_LANE_OPS,
+            "frac_issue_weighted": rec["valu_issue_weighted"] * 64 / t / VALU_PEAK_LANE_OPS,
+            "valu_insts_per_launch": rec["valu_insts"], "valu_insts_per_frame": rec["valu_insts"] / (rec["grid"] / 2)}
 
 
 def secondary_configs(solver, sets, stream):
@@ -392,6 +409,7 @@ def main():
     stream = backend.stream
     if rank == 0:
         achieved = BYTES_PER_FRAME * B / (kern_ms * 1e-3) / 1e9
+        rec = pmc_record(B)
         line = {
             "metric": METRIC, "value": value, "unit": "frames/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": ms_per_step, "higher_is_better": True, "scaling": "weak",
@@ -400,9 +418,14 @@ def main():
                        "frames_per_gpu_per_step": B, "global_batch": B * world, "parallelism": f"dp{world}",
                        "input_ring_sets": ring, "precise_gripper": True},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": achieved / HBM_PEAK_GBS, "traffic": pmc_traffic(B),
+                         "frac": achieved / HBM_PEAK_GBS, "traffic": rec["traffic_bytes"] if rec else None,
                          "kernel": "k_solve_sides<FULL_BODY_POS>", "kernel_ms": kern_ms,
-                         "bytes_per_frame": BYTES_PER_FRAME, "traffic_unit": "bytes/launch (rocprofv3 PMC)"},
+                         "bytes_per_frame": BYTES_PER_FRAME,
+                         "traffic_unit": "bytes/launch (rocprofv3 FETCH_SIZE x calibration + WRITE_SIZE)",
+                         "traffic_detail": {k: rec[k] for k in ("fetch_size_raw", "fetch_correction", "fetch_bytes",
+                                                                "write_bytes", "angle_table_fetch_bytes") if k in rec}
+                         if rec else None,
+                         "compute": compute_roofline(rec, kern_ms)},
         }
         if "gather_ms" in res:
             line["gather_ms"] = res["gather_ms"]
