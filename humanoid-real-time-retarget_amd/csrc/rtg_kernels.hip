@@ -422,18 +422,37 @@ RTG_DEV Q fbp_wrist_fit(const SolverConsts &C, const View &H)
     return cal_joint_quat<5>(SIDE ? C.Zr : C.Zl, M);
 }
 
-template <bool PRECISE, int SIDE, typename View>
-RTG_DEV void solve_fbp_side(const SolverConsts &C, const View &b, const View &H, Q R10, Q W, const Emit &E,
+// A side's body points (shoulder, elbow, wrist) and hand points for the gripper (0 and the tips 4,8,12,16,19),
+// loaded where the kernel chooses (RTG_PRELOAD_*: next to the other loads of the same rows, so the rows' lines are
+// still in L2 -- see DESIGN.md §5 on the re-fetch of evicted rows).
+struct ArmPts { V sh, el, wr; };
+struct TipPts { V h0, t[5]; };
+template <int SIDE, typename View>
+RTG_DEV ArmPts load_arm(const View &b)
+{
+    return ArmPts{b.p3(SIDE ? 14 : 18), b.p3(SIDE ? 15 : 19), b.p3(SIDE ? 16 : 20)};
+}
+template <typename View>
+RTG_DEV TipPts load_tips(const View &H)
+{
+    return TipPts{H.p3(0), {H.p3(4), H.p3(8), H.p3(12), H.p3(16), H.p3(19)}};
+}
+#ifndef RTG_PRELOAD_ARM
+#define RTG_PRELOAD_ARM 1    // (measured -4 %) 1: a side's arm points load at kernel start, with the torso / wrist-fit loads
+#endif
+#ifndef RTG_PRELOAD_TIPS
+#define RTG_PRELOAD_TIPS 0   // 1: the gripper's hand points load with the wrist-fit points
+#endif
+
+template <bool PRECISE, int SIDE>
+RTG_DEV void solve_fbp_side(const SolverConsts &C, const ArmPts &ap, const TipPts &tp, Q R10, Q W, const Emit &E,
                             float *__restrict__ brow)
 {
     constexpr int L0 = SIDE ? 21 : 12, E0 = SIDE ? 25 : 16, D0 = SIDE ? 27 : 18, WROW = SIDE ? 39 : 14;
-    constexpr int SH = SIDE ? 14 : 18, EL = SIDE ? 15 : 19, WR = SIDE ? 16 : 20;
-    const V bel = b.p3(EL);
-    const Q chain = solve_arm<L0>(E, vsub(bel, b.p3(SH)), vsub(b.p3(WR), bel), SIDE ? C.rsh : C.lsh,
+    const Q chain = solve_arm<L0>(E, vsub(ap.el, ap.sh), vsub(ap.wr, ap.el), SIDE ? C.rsh : C.lsh,
                                   SIDE ? C.rel : C.lel, R10);
     emit_euler_xyz<E0>(E, qmul_norm(qconj(qmul_norm(R10, chain)), W));
-    constexpr int tips[5] = {4, 8, 12, 16, 19};
-    const float a = hand_x_mean(qconj(W), H, tips);
+    const float a = hand_x_mean(qconj(W), tp.h0, tp.t);
     if (PRECISE) {
         const float sc = clamp_lohi(a / C.orig - 0.5f, 0.0f, 0.5f) / 0.5f;
         E.row[D0] = sc * 0.044f;
@@ -544,12 +563,17 @@ __global__ __launch_bounds__(256, RTG_SIDES_WAVES) void k_solve_sides(SolverCons
         // (FULL_BODY_POS; nothing to overlap for UPPER_BODY), then one block barrier hands R10 over LDS.
         const auto b = view(in0, 63);   // body (FULL_BODY_POS) / mocap points (UPPER_BODY), both (B, 21, 3)
         Q R10 = qident(), W = qident();
+        ArmPts ap{};
+        TipPts tp{};
         if (live) {
+            if (KIND == RTG_SOLVER_FULL_BODY_POS && RTG_PRELOAD_ARM) ap = side ? load_arm<1>(b) : load_arm<0>(b);
             if (!side) {
                 R10 = KIND == RTG_SOLVER_FULL_BODY_POS ? fbp_torso(C, b) : upper_torso(C, b);
                 storso[r] = make_float4(R10.x, R10.y, R10.z, R10.w);
             } else if (KIND == RTG_SOLVER_FULL_BODY_POS) {
-                W = fbp_wrist_fit<1>(C, view(in2, 60));
+                const auto H = view(in2, 60);
+                if (RTG_PRELOAD_TIPS) tp = load_tips(H);
+                W = fbp_wrist_fit<1>(C, H);
             }
         }
         __syncthreads();
@@ -562,8 +586,17 @@ __global__ __launch_bounds__(256, RTG_SIDES_WAVES) void k_solve_sides(SolverCons
             }
             if (KIND == RTG_SOLVER_FULL_BODY_POS) {
                 float *brow = body_rot ? body_rot + f * 236 : nullptr;
-                if (side) solve_fbp_side<PRECISE, 1>(C, b, view(in2, 60), R10, W, E, brow);
-                else solve_fbp_side<PRECISE, 0>(C, b, view(in1, 60), R10, fbp_wrist_fit<0>(C, view(in1, 60)), E, brow);
+                if (!RTG_PRELOAD_ARM) ap = side ? load_arm<1>(b) : load_arm<0>(b);
+                if (side) {
+                    if (!RTG_PRELOAD_TIPS) tp = load_tips(view(in2, 60));
+                    solve_fbp_side<PRECISE, 1>(C, ap, tp, R10, W, E, brow);
+                } else {
+                    const auto H = view(in1, 60);
+                    if (RTG_PRELOAD_TIPS) tp = load_tips(H);
+                    W = fbp_wrist_fit<0>(C, H);
+                    if (!RTG_PRELOAD_TIPS) tp = load_tips(H);
+                    solve_fbp_side<PRECISE, 0>(C, ap, tp, R10, W, E, brow);
+                }
             } else {
                 if (side) solve_upper_side<1>(C, b, R10, E);
                 else solve_upper_side<0>(C, b, R10, E);
@@ -594,6 +627,82 @@ __global__ __launch_bounds__(256, RTG_SIDES_WAVES) void k_solve_sides(SolverCons
         *reinterpret_cast<float4 *>(dst + i) = make_float4(at(i), at(i + 1), at(i + 2), at(i + 3));
     }
     for (int i = (nvec << 2) + threadIdx.x; i < nvals; i += 256) dst[i] = at(i);
+}
+
+// ----------------------------------------------------------------------------
+// FULL_BODY_POS for small batches (the teleop / config-2 latency path): three waves per 64-frame tile, one per
+// Kabsch fit.  The torso fit and the two wrist fits are independent (full_body_pos_retargeter.py:69-70, 137-140,
+// 160-163), so they run concurrently; after one barrier the wrist waves each run their side (arm, Euler split,
+// gripper) while the torso wave writes the fixed links; the exp-map read-out is split three ways.  A frame's
+// critical path loses one SVD against k_solve_sides (which runs the torso and the left wrist fit on one wave).
+// The same device functions in the same order per value: the same bits (test_solver_batch_invariance).
+// Large batches keep k_solve_sides: there the third wave idles after its fit and costs throughput.
+// ----------------------------------------------------------------------------
+#ifndef RTG_LATENCY_MAX_B
+#define RTG_LATENCY_MAX_B 32768   // batches up to this size use k_fbp_latency (the GPU is not full anyway)
+#endif
+constexpr int kLatFrames = 64;
+
+template <bool PRECISE, bool SOA>
+__global__ __launch_bounds__(192) void k_fbp_latency(SolverConsts C, const float *__restrict__ in0,
+                                                     const float *__restrict__ in1, const float *__restrict__ in2,
+                                                     int64_t B, float *__restrict__ dof, float *__restrict__ local_rot,
+                                                     float *__restrict__ body_rot)
+{
+    __shared__ float sdof[kLatFrames * kDofStride];
+    __shared__ float4 sfit[3][kLatFrames];   // R10, W_left, W_right
+    __shared__ float2 sst[14 * kLatFrames];
+    const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int64_t f0 = (int64_t)blockIdx.x * kLatFrames, f = f0 + lane;
+    const bool live = f < B;
+    const Emit E{sdof + lane * kDofStride, live && local_rot ? local_rot + f * 124 : nullptr, C.ang_tab, sst + lane,
+                 kLatFrames};
+    auto view = [&](const float *base, int row_floats) { return frame_view<SOA>(base, f, row_floats, B); };
+    const auto b = view(in0, 63);
+    ArmPts ap{};
+    TipPts tp{};
+    if (live) {
+        Q q;
+        if (w == 0) {
+            q = fbp_torso(C, b);
+        } else {
+            const auto H = view(w == 1 ? in1 : in2, 60);
+            ap = w == 1 ? load_arm<0>(b) : load_arm<1>(b);
+            q = w == 1 ? fbp_wrist_fit<0>(C, H) : fbp_wrist_fit<1>(C, H);
+            tp = load_tips(H);
+        }
+        sfit[w][lane] = make_float4(q.x, q.y, q.z, q.w);
+    }
+    __syncthreads();
+    if (live) {
+        const float4 t = sfit[0][lane];
+        const Q R10{t.x, t.y, t.z, t.w};
+        float *brow = body_rot ? body_rot + f * 236 : nullptr;
+        if (w == 0) {
+            emit_fixed_links(E);
+        } else {
+            const float4 u = sfit[w][lane];
+            const Q W{u.x, u.y, u.z, u.w};
+            if (w == 1) solve_fbp_side<PRECISE, 0>(C, ap, tp, R10, W, E, brow);
+            else solve_fbp_side<PRECISE, 1>(C, ap, tp, R10, W, E, brow);
+        }
+    }
+    __syncthreads();
+    if (live) E.finalize(w == 0 ? 0 : (w == 1 ? 5 : 10), w == 2 ? 4 : 5);
+    __syncthreads();
+    const int64_t nrows = (B - f0) < kLatFrames ? (B - f0) : kLatFrames;
+    const int nvals = (int)nrows * 30;
+    float *dst = dof + f0 * 30;
+    auto at = [&](int i) {
+        const int rr = i / 30;
+        return sdof[rr * kDofStride + (i - rr * 30)];
+    };
+    const int nvec = nvals >> 2;   // f0 * 30 floats = 16-byte aligned (f0 is a multiple of 64)
+    for (int v = threadIdx.x; v < nvec; v += 192) {
+        const int i = v << 2;
+        *reinterpret_cast<float4 *>(dst + i) = make_float4(at(i), at(i + 1), at(i + 2), at(i + 3));
+    }
+    for (int i = (nvec << 2) + threadIdx.x; i < nvals; i += 192) dst[i] = at(i);
 }
 
 // ----------------------------------------------------------------------------
@@ -1567,7 +1676,14 @@ static void launch_kind(const SolverConsts &C, const float *in0, const float *in
                         const float *in3, int64_t B, int layout, float *dof, float *local_rot, float *body_rot,
                         hipStream_t s)
 {
-    if (layout == RTG_LAYOUT_SOA)
+    if (KIND == RTG_SOLVER_FULL_BODY_POS && B <= RTG_LATENCY_MAX_B) {
+        if (layout == RTG_LAYOUT_SOA)
+            hipLaunchKernelGGL((k_fbp_latency<PRECISE, true>), dim3(grid_for(B, kLatFrames)), dim3(192), 0, s, C, in0,
+                               in1, in2, B, dof, local_rot, body_rot);
+        else
+            hipLaunchKernelGGL((k_fbp_latency<PRECISE, false>), dim3(grid_for(B, kLatFrames)), dim3(192), 0, s, C, in0,
+                               in1, in2, B, dof, local_rot, body_rot);
+    } else if (layout == RTG_LAYOUT_SOA)
         hipLaunchKernelGGL((k_solve_sides<KIND, PRECISE, true>), dim3(grid_for(B, kSideFrames)), dim3(256), 0, s, C,
                            in0, in1, in2, in3, B, dof, local_rot, body_rot);
     else if (!RTG_SOLVER_SIDES)
