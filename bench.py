@@ -176,7 +176,8 @@ def compute_roofline(rec, kern_ms):
     return {"bound": "valu", "achieved": achieved / 1e12, "peak": VALU_PEAK_LANE_OPS / 1e12, "unit": "T lane-ops/s",
             "frac": achieved / VALU_PEAK_LANE_OPS,
             "frac_issue_weighted": rec["valu_issue_weighted"] * 64 / t / VALU_PEAK_LANE_OPS,
-            "valu_insts_per_launch": rec["valu_insts"], "valu_insts_per_frame": rec["valu_insts"] / (rec["grid"] / 2)}
+            "valu_wave_insts_per_launch": rec["valu_insts"],
+            "valu_lane_ops_per_frame": rec["valu_insts"] * 64 / (rec["grid"] / 2)}
 
 
 def secondary_configs(solver, sets, stream):
