@@ -38,6 +38,10 @@ def parse():
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--batch", type=int, default=262144, help="frames per GPU per step")
     ap.add_argument("--ring", type=int, default=0, help="input buffer sets (0 = enough to exceed 256 MiB x 2)")
+    ap.add_argument("--layout", choices=("soa", "aos"), default="soa",
+                    help="input layout of the timed frames: SoA component planes as the device producer emits them "
+                         "(default, north_star), or the reference's AoS rows; the other one is reported as a "
+                         "secondary line")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     return ap.parse_args()
@@ -149,15 +153,15 @@ def cpu_baseline(body, lh, rh, zl, zg, seconds):
 
 
 PMC_JSON = os.path.join(REPO, "profiles", "pmc_r02.json")
-PMC_KERNEL = "rtg::k_solve_sides<0, true, false>"
+PMC_KERNELS = {"soa": "rtg::k_solve_sides<0, true, true>", "aos": "rtg::k_solve_sides<0, true, false>"}
 VALU_PEAK_LANE_OPS = 256 * 4 * 32 * 2.4e9   # MI355X: CUs x SIMDs x lanes issued per cycle x 2.4 GHz (78.6 T/s)
 
 
-def pmc_record(B):
+def pmc_record(B, layout="soa"):
     """The committed rocprofv3 PMC summary of the headline kernel (tools/profile_round.sh -> tools/pmc_summary.py),
     when it was taken at this batch (rocprofv3's grid counts threads: two per frame, one wave per side)."""
     try:
-        rec = json.load(open(PMC_JSON)).get(PMC_KERNEL)
+        rec = json.load(open(PMC_JSON)).get(PMC_KERNELS[layout])
     except (OSError, ValueError):
         return None
     if not rec or rec.get("grid") != 2 * B:
@@ -188,10 +192,9 @@ def secondary_configs(solver, sets, stream):
     from rtg import assets, ops, synth
     from rtg.runtime import Topology
     out = {}
-    b, l, r_, _ = sets[0]
     n = 4096
-    xb, xl, xr = b[:n].contiguous(), l[:n].contiguous(), r_[:n].contiguous()
-    d = torch.empty((n, 30), device=b.device)
+    xb, xl, xr = sets   # 4096 AoS frames (the per-frame callers' rows)
+    d = torch.empty((n, 30), device=xb.device)
     for _ in range(10):
         solver.retarget([xb, xl, xr], out_dof=d)
     reps = 200
@@ -238,30 +241,30 @@ def secondary_configs(solver, sets, stream):
     return out
 
 
-def soa_line(solver, topo_full, B, rank, ring, steps, stream):
-    """The same workload with RTG_LAYOUT_SOA inputs ((P,C,B) component planes, emitted directly by the device
-    producer): every wave load of one component is 256 contiguous bytes instead of 64 row-strided 12-byte
-    reads.  Reported beside the AoS headline (the reference's own layout), not as `value`."""
+def layout_line(solver, topo_full, B, rank, ring, steps, stream, layout):
+    """The same workload in the other input layout, reported beside the headline (not as `value`):
+    AoS = the reference's (B, P, 3) rows, each wave load of a point a 64-line gather of 12-byte pieces;
+    SoA = (P, C, B) component planes emitted directly by the device producer, each load 256 contiguous bytes."""
     import torch
     from rtg import ops
     sets = []
     for r in range(ring):
-        b, l, r_ = ops.synth_full_body(topo_full, B, seed=1234 + rank, frame_offset=r * B, layout="soa")
+        b, l, r_ = ops.synth_full_body(topo_full, B, seed=1234 + rank, frame_offset=r * B, layout=layout)
         sets.append((b, l, r_, torch.empty((B, 30), device=b.device)))
     for i in range(5):
         b, l, r_, d = sets[i % ring]
-        solver.retarget([b, l, r_], out_dof=d, layout="soa")
+        solver.retarget([b, l, r_], out_dof=d, layout=layout)
     torch.cuda.synchronize()
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     e0.record(stream)
     for i in range(steps):
         b, l, r_, d = sets[i % ring]
-        solver.retarget([b, l, r_], out_dof=d, layout="soa")
+        solver.retarget([b, l, r_], out_dof=d, layout=layout)
     e1.record(stream)
     e1.synchronize()
     ms = e0.elapsed_time(e1) / steps
     gbs = BYTES_PER_FRAME * B / (ms * 1e-3) / 1e9
-    return {"layout": "soa", "kernel_ms": ms, "frames_per_s": B / (ms * 1e-3), "achieved_GBs": gbs,
+    return {"layout": layout, "kernel_ms": ms, "frames_per_s": B / (ms * 1e-3), "achieved_GBs": gbs,
             "hbm_frac": gbs / HBM_PEAK_GBS, "input_ring_sets": ring}
 
 
@@ -300,10 +303,11 @@ def source_setup():
 class DeviceBackend:
     """The product path of one rank: librtg_hip.so on this rank's GPU (RCCL for the collectives)."""
 
-    def __init__(self, dev):
+    def __init__(self, dev, layout="soa"):
         import torch
         self.torch = torch
         self.dev = dev
+        self.layout = layout
         self.comm_device = dev
         self.stream = torch.cuda.current_stream()
 
@@ -323,13 +327,13 @@ class DeviceBackend:
 
     def synth(self, topo, B, seed, offset):
         from rtg import ops
-        return ops.synth_full_body(topo, B, seed=seed, frame_offset=offset)
+        return ops.synth_full_body(topo, B, seed=seed, frame_offset=offset, layout=self.layout)
 
     def new_dof(self, B):
         return self.torch.empty((B, 30), device=self.dev, dtype=self.torch.float32)
 
     def solve(self, solver, b, l, r, d):
-        solver.retarget([b, l, r], out_dof=d)
+        solver.retarget([b, l, r], out_dof=d, layout=self.layout)
 
     def sync(self):
         self.torch.cuda.synchronize()
@@ -400,7 +404,7 @@ def main():
     world, rank, local = dist_setup(args)
     B = args.batch
     dev = torch.device("cuda", local)
-    backend = DeviceBackend(dev)
+    backend = DeviceBackend(dev, args.layout)
     bytes_per_set = B * (63 + 60 + 60 + 30) * 4
     ring = args.ring or max(2, int(np.ceil(2 * 256 * 2**20 / bytes_per_set)))
     res = rank_flow(world, rank, backend, B, args.steps, args.warmup, ring)
@@ -410,17 +414,17 @@ def main():
     stream = backend.stream
     if rank == 0:
         achieved = BYTES_PER_FRAME * B / (kern_ms * 1e-3) / 1e9
-        rec = pmc_record(B)
+        rec = pmc_record(B, args.layout)
         line = {
             "metric": METRIC, "value": value, "unit": "frames/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": ms_per_step, "higher_is_better": True, "scaling": "weak",
             "vs_baseline": None, "dtype": "f32", "data": "synthetic (device-generated VTRDyn frames, seed 1234+rank)",
             "config": {"workload": "VtrdynFullBodyPosRetargeter batched solve, Hu v5 target (BASELINE config 3)",
                        "frames_per_gpu_per_step": B, "global_batch": B * world, "parallelism": f"dp{world}",
-                       "input_ring_sets": ring, "precise_gripper": True},
+                       "input_layout": args.layout, "input_ring_sets": ring, "precise_gripper": True},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": rec["traffic_bytes"] if rec else None,
-                         "kernel": "k_solve_sides<FULL_BODY_POS>", "kernel_ms": kern_ms,
+                         "kernel": f"k_solve_sides<FULL_BODY_POS, {args.layout.upper()}>", "kernel_ms": kern_ms,
                          "bytes_per_frame": BYTES_PER_FRAME,
                          "traffic_unit": "bytes/launch (rocprofv3 FETCH_SIZE x calibration + WRITE_SIZE)",
                          "traffic_detail": {k: rec[k] for k in ("fetch_size_raw", "fetch_correction", "fetch_bytes",
@@ -430,26 +434,28 @@ def main():
         }
         if "gather_ms" in res:
             line["gather_ms"] = res["gather_ms"]
+        from rtg import ops
+        aos = ops.synth_full_body(res["topo"], min(B, 65536), seed=1234 + rank)   # rows for config 2 / the CPU leg
         if world == 1:
             solver, sets = res["solver"], res["sets"]
             try:
-                line["secondary"] = secondary_configs(solver, sets, stream)
+                line["secondary"] = secondary_configs(solver, [t[:4096].contiguous() for t in aos], stream)
             except Exception as e:  # noqa: BLE001
                 line["secondary"] = {"error": repr(e)}
+            other = "aos" if args.layout == "soa" else "soa"
             try:
-                del sets[1:]
-                line["secondary"]["config3_soa_layout"] = soa_line(solver, res["topo"], B, rank, ring, args.steps,
-                                                                   stream)
+                del sets[:]
+                line["secondary"][f"config3_{other}_layout"] = layout_line(solver, res["topo"], B, rank, ring,
+                                                                           args.steps, stream, other)
             except Exception as e:  # noqa: BLE001
-                line["secondary"]["config3_soa_layout"] = {"error": repr(e)}
+                line["secondary"][f"config3_{other}_layout"] = {"error": repr(e)}
         try:
             line["parity_vs_reference"] = parity_vs_reference()
         except Exception as e:  # noqa: BLE001
             line["parity_vs_reference"] = {"error": repr(e)}
         if world == 1 and not args.no_cpu_baseline:
-            b, l, r_, _ = res["sets"][0]
-            n = min(B, 65536)
-            line["cpu_baseline"] = cpu_baseline(b[:n].cpu().numpy(), l[:n].cpu().numpy(), r_[:n].cpu().numpy(),
+            b, l, r_ = aos
+            line["cpu_baseline"] = cpu_baseline(b.cpu().numpy(), l.cpu().numpy(), r_.cpu().numpy(),
                                                 np.asarray(res["zl"], np.float32), np.asarray(res["zg"], np.float32),
                                                 args.cpu_seconds)
         print(json.dumps(line), flush=True)

@@ -394,12 +394,12 @@ __global__ __launch_bounds__(kSolverBlock) void k_retarget(SolverConsts C, const
 constexpr int kSideFrames = 128;   // frames per 256-thread block
 
 // torso fit R10 (full_body_pos_retargeter.py:69-70 / retarget_solver.py:49-50)
-template <typename View>
-RTG_DEV Q fbp_torso(const SolverConsts &C, const View &b)
+template <typename View, typename Hook = NoHook>
+RTG_DEV Q fbp_torso(const SolverConsts &C, const View &b, const Hook &hook = Hook{})
 {
     const V b10 = b.p3(10);
     const V Mt[3] = {vsub(b.p3(17), b10), vsub(b.p3(13), b10), vsub(b.p3(11), b10)};
-    return cal_joint_quat<3>(C.Zt, Mt);
+    return cal_joint_quat<3>(C.Zt, Mt, hook);
 }
 RTG_DEV Q upper_pt_sign(V v) { return Q{v.x * -1.0f, v.y * -1.0f, v.z * 1.0f, 0.0f}; }   // coord_transform :41
 template <typename View>
@@ -414,12 +414,12 @@ RTG_DEV Q upper_torso(const SolverConsts &C, const View &x)
     return cal_joint_quat<3>(C.Zt, Mt);
 }
 // wrist fit W (full_body_pos_retargeter.py:137-140 left, :160-163 right)
-template <int SIDE, typename View>
-RTG_DEV Q fbp_wrist_fit(const SolverConsts &C, const View &H)
+template <int SIDE, typename View, typename Hook = NoHook>
+RTG_DEV Q fbp_wrist_fit(const SolverConsts &C, const View &H, const Hook &hook = Hook{})
 {
     const V h0 = H.p3(0);
     const V M[5] = {vsub(H.p3(2), h0), vsub(H.p3(6), h0), vsub(H.p3(10), h0), vsub(H.p3(14), h0), vsub(H.p3(17), h0)};
-    return cal_joint_quat<5>(SIDE ? C.Zr : C.Zl, M);
+    return cal_joint_quat<5>(SIDE ? C.Zr : C.Zl, M, hook);
 }
 
 // A side's body points (shoulder, elbow, wrist) and hand points for the gripper (0 and the tips 4,8,12,16,19),
@@ -444,14 +444,16 @@ RTG_DEV TipPts load_tips(const View &H)
 #define RTG_PRELOAD_TIPS 0   // 1: the gripper's hand points load with the wrist-fit points
 #endif
 
-template <bool PRECISE, int SIDE>
+template <bool PRECISE, int SIDE, typename Hook = NoHook>
 RTG_DEV void solve_fbp_side(const SolverConsts &C, const ArmPts &ap, const TipPts &tp, Q R10, Q W, const Emit &E,
-                            float *__restrict__ brow)
+                            float *__restrict__ brow, const Hook &hook = Hook{})
 {
     constexpr int L0 = SIDE ? 21 : 12, E0 = SIDE ? 25 : 16, D0 = SIDE ? 27 : 18, WROW = SIDE ? 39 : 14;
     const Q chain = solve_arm<L0>(E, vsub(ap.el, ap.sh), vsub(ap.wr, ap.el), SIDE ? C.rsh : C.lsh,
                                   SIDE ? C.rel : C.lel, R10);
+    hook(2);
     emit_euler_xyz<E0>(E, qmul_norm(qconj(qmul_norm(R10, chain)), W));
+    hook(3);
     const float a = hand_x_mean(qconj(W), tp.h0, tp.t);
     if (PRECISE) {
         const float sc = clamp_lohi(a / C.orig - 0.5f, 0.0f, 0.5f) / 0.5f;
@@ -642,6 +644,9 @@ __global__ __launch_bounds__(256, RTG_SIDES_WAVES) void k_solve_sides(SolverCons
 #define RTG_LATENCY_MAX_B 32768   // batches up to this size use k_fbp_latency (the GPU is not full anyway)
 #endif
 constexpr int kLatFrames = 64;
+#ifndef RTG_EXP_TIMESTAMPS
+#define RTG_EXP_TIMESTAMPS 0   // measurement knob: block 0's lane 0 of each wave records the 100 MHz wall clock at
+#endif                         // each phase into body_rot (as u32 pairs) -- wrong body_rot, tools/latency_phases.py
 
 template <bool PRECISE, bool SOA>
 __global__ __launch_bounds__(192) void k_fbp_latency(SolverConsts C, const float *__restrict__ in0,
@@ -655,6 +660,21 @@ __global__ __launch_bounds__(192) void k_fbp_latency(SolverConsts C, const float
     const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int64_t f0 = (int64_t)blockIdx.x * kLatFrames, f = f0 + lane;
     const bool live = f < B;
+#if RTG_EXP_TIMESTAMPS
+    float *const tsb = body_rot;
+    body_rot = nullptr;
+    auto TS = [&](int k) {
+        if (tsb && blockIdx.x == 0 && lane == 0) {
+            const uint64_t t = wall_clock64();
+            reinterpret_cast<uint32_t *>(tsb)[2 * (16 * w + k)] = (uint32_t)t;
+            reinterpret_cast<uint32_t *>(tsb)[2 * (16 * w + k) + 1] = (uint32_t)(t >> 32);
+        }
+    };
+#else
+    auto TS = [](int) {};
+#endif
+    auto hook = [&](int k) { TS(8 + k); };   // 8: A formed, 9: SVD + R done, 10: arm, 11: Euler
+    TS(0);
     const Emit E{sdof + lane * kDofStride, live && local_rot ? local_rot + f * 124 : nullptr, C.ang_tab, sst + lane,
                  kLatFrames};
     auto view = [&](const float *base, int row_floats) { return frame_view<SOA>(base, f, row_floats, B); };
@@ -664,16 +684,18 @@ __global__ __launch_bounds__(192) void k_fbp_latency(SolverConsts C, const float
     if (live) {
         Q q;
         if (w == 0) {
-            q = fbp_torso(C, b);
+            q = fbp_torso(C, b, hook);
         } else {
             const auto H = view(w == 1 ? in1 : in2, 60);
             ap = w == 1 ? load_arm<0>(b) : load_arm<1>(b);
-            q = w == 1 ? fbp_wrist_fit<0>(C, H) : fbp_wrist_fit<1>(C, H);
+            q = w == 1 ? fbp_wrist_fit<0>(C, H, hook) : fbp_wrist_fit<1>(C, H, hook);
             tp = load_tips(H);
         }
         sfit[w][lane] = make_float4(q.x, q.y, q.z, q.w);
     }
+    TS(1);
     __syncthreads();
+    TS(2);
     if (live) {
         const float4 t = sfit[0][lane];
         const Q R10{t.x, t.y, t.z, t.w};
@@ -683,13 +705,17 @@ __global__ __launch_bounds__(192) void k_fbp_latency(SolverConsts C, const float
         } else {
             const float4 u = sfit[w][lane];
             const Q W{u.x, u.y, u.z, u.w};
-            if (w == 1) solve_fbp_side<PRECISE, 0>(C, ap, tp, R10, W, E, brow);
-            else solve_fbp_side<PRECISE, 1>(C, ap, tp, R10, W, E, brow);
+            if (w == 1) solve_fbp_side<PRECISE, 0>(C, ap, tp, R10, W, E, brow, hook);
+            else solve_fbp_side<PRECISE, 1>(C, ap, tp, R10, W, E, brow, hook);
         }
     }
+    TS(3);
     __syncthreads();
+    TS(4);
     if (live) E.finalize(w == 0 ? 0 : (w == 1 ? 5 : 10), w == 2 ? 4 : 5);
+    TS(5);
     __syncthreads();
+    TS(6);
     const int64_t nrows = (B - f0) < kLatFrames ? (B - f0) : kLatFrames;
     const int nvals = (int)nrows * 30;
     float *dst = dof + f0 * 30;
@@ -703,6 +729,7 @@ __global__ __launch_bounds__(192) void k_fbp_latency(SolverConsts C, const float
         *reinterpret_cast<float4 *>(dst + i) = make_float4(at(i), at(i + 1), at(i + 2), at(i + 3));
     }
     for (int i = (nvec << 2) + threadIdx.x; i < nvals; i += 192) dst[i] = at(i);
+    TS(7);
 }
 
 // ----------------------------------------------------------------------------
@@ -796,14 +823,36 @@ constexpr int kPosPitch = 3 * kFkChunk + 1;
 #endif
 constexpr int kPosWin = RTG_FK_POS_REGS ? 0 : kFkTile * kPosPitch;   // floats of the separate position window
 
+// Branch-parent slots: the first RTG_FK_REG_SLOTS live in registers (a slot is private to its lane, and its
+// index is launch-uniform, so the choice is a scalar branch), the rest in LDS.  Every shipped skeleton needs <= 2
+// slots, so their tiles use only the 9.2 KiB rotation window: 17 waves per CU instead of 12, and the 4096 tiles of
+// a 262144-frame batch fit the 256 CUs in one round.
+#ifndef RTG_FK_MIN_WAVES
+#define RTG_FK_MIN_WAVES 0   // >0: min waves per SIMD asked of the streaming FK kernels (4: <= 128 VGPRs, 16 waves/CU)
+#endif
+#if RTG_FK_MIN_WAVES > 0
+#define RTG_FK_WAVES __attribute__((amdgpu_waves_per_eu(RTG_FK_MIN_WAVES, 8)))
+#else
+#define RTG_FK_WAVES
+#endif
+#ifndef RTG_FK_REG_SLOTS
+#define RTG_FK_REG_SLOTS 0
+#endif
+#ifndef RTG_DOF_FK_POS_REGS
+#define RTG_DOF_FK_POS_REGS 1   // k_dof_fk positions staged through the rotation window (as RTG_FK_POS_REGS; measured +7-9 %)
+#endif
+static inline size_t lds_slot_floats(int nslots)
+{
+    return nslots > RTG_FK_REG_SLOTS ? (size_t)(nslots - RTG_FK_REG_SLOTS) * 7 * kFkTile : 0;
+}
 static inline size_t fk_stream_lds_bytes(int nslots)
 {
-    return sizeof(float) * ((size_t)kFkTile * kRotPitch + (size_t)kPosWin + (size_t)nslots * 7 * kFkTile);
+    return sizeof(float) * ((size_t)kFkTile * kRotPitch + (size_t)kPosWin + lds_slot_floats(nslots));
 }
-// k_dof_fk keeps its separate position window whatever RTG_FK_POS_REGS says
+constexpr int kDofPosWin = RTG_DOF_FK_POS_REGS ? 0 : kFkTile * kPosPitch;
 static inline size_t dof_fk_lds_bytes(int nslots)
 {
-    return sizeof(float) * ((size_t)kFkTile * (kRotPitch + kPosPitch) + (size_t)nslots * 7 * kFkTile);
+    return sizeof(float) * ((size_t)kFkTile * kRotPitch + (size_t)kDofPosWin + lds_slot_floats(nslots));
 }
 
 // A streaming tile is one wave, so ordering its LDS traffic needs no block
@@ -879,18 +928,30 @@ RTG_DEV void chunk_store(float *__restrict__ g, const float *lds, int pitch, int
     }
 }
 
-RTG_DEV void slot_put(float *slots, int s, Q q, V t)
+// slot s < RTG_FK_REG_SLOTS: registers (named members: an indexed array would be left in scratch); else LDS
+// [s - RTG_FK_REG_SLOTS][7][64].  s is launch-uniform (SGPR), so the selection is a scalar branch.
+struct Slots {
+    float *lds;
+    Q q0, q1;
+    V t0, t1;
+};
+RTG_DEV void slot_put(Slots &S, int s, Q q, V t)
 {
-    float *p = slots + s * 7 * kFkTile + threadIdx.x;
+    if (RTG_FK_REG_SLOTS > 0 && s == 0) { S.q0 = q; S.t0 = t; return; }
+    if (RTG_FK_REG_SLOTS > 1 && s == 1) { S.q1 = q; S.t1 = t; return; }
+    float *p = S.lds + (s - RTG_FK_REG_SLOTS) * 7 * kFkTile + threadIdx.x;
     p[0] = q.x; p[kFkTile] = q.y; p[2 * kFkTile] = q.z; p[3 * kFkTile] = q.w;
     p[4 * kFkTile] = t.x; p[5 * kFkTile] = t.y; p[6 * kFkTile] = t.z;
 }
-RTG_DEV void slot_get(const float *slots, int s, Q &q, V &t)
+RTG_DEV void slot_get(const Slots &S, int s, Q &q, V &t)
 {
-    const float *p = slots + s * 7 * kFkTile + threadIdx.x;
+    if (RTG_FK_REG_SLOTS > 0 && s == 0) { q = S.q0; t = S.t0; return; }
+    if (RTG_FK_REG_SLOTS > 1 && s == 1) { q = S.q1; t = S.t1; return; }
+    const float *p = S.lds + (s - RTG_FK_REG_SLOTS) * 7 * kFkTile + threadIdx.x;
     q = Q{p[0], p[kFkTile], p[2 * kFkTile], p[3 * kFkTile]};
     t = V{p[4 * kFkTile], p[5 * kFkTile], p[6 * kFkTile]};
 }
+static_assert(RTG_FK_REG_SLOTS >= 0 && RTG_FK_REG_SLOTS <= 2, "0..2 register slots");
 
 template <bool STATE>
 RTG_DEV void fk_stream_tile(const TopoView &T, const float *__restrict__ local_rot, const float *__restrict__ root_t,
@@ -900,7 +961,7 @@ RTG_DEV void fk_stream_tile(const TopoView &T, const float *__restrict__ local_r
     const int nfr = (int)((B - f0) < kFkTile ? (B - f0) : kFkTile);
     float *rot = lds;                                   // [64][kRotPitch]
     float *pos = lds + kFkTile * kRotPitch;             // [64][kPosPitch] (RTG_FK_POS_REGS: none)
-    float *slots = pos + kPosWin;                       // [nslots][7][64]
+    Slots slots{pos + kPosWin, qident(), qident(), V{0.0f, 0.0f, 0.0f}, V{0.0f, 0.0f, 0.0f}};
     const int lane = threadIdx.x;
     const bool active = lane < nfr;
     Q g = qident();
@@ -967,7 +1028,7 @@ RTG_DEV void fk_stream_tile(const TopoView &T, const float *__restrict__ local_r
 }
 
 template <bool STATE>
-__global__ __launch_bounds__(kFkTile) void k_fk_stream(TopoView T, const float *__restrict__ local_rot,
+__global__ __launch_bounds__(kFkTile) RTG_FK_WAVES void k_fk_stream(TopoView T, const float *__restrict__ local_rot,
                                                        const float *__restrict__ root_t, int64_t B,
                                                        float *__restrict__ g_rot, float *__restrict__ g_pos)
 {
@@ -984,7 +1045,8 @@ RTG_DEV void local_rotation_tile(const TopoView &T, const float *__restrict__ g_
     const int J = T.J;
     const int nfr = (int)((B - f0) < kFkTile ? (B - f0) : kFkTile);
     float *win = fk_lds;                                 // [64][kRotPitch]
-    float *slots = fk_lds + kFkTile * kRotPitch + kPosWin;   // the same slot offset as fk_stream_tile
+    Slots slots{fk_lds + kFkTile * kRotPitch + kPosWin, qident(), qident(), V{0.0f, 0.0f, 0.0f},
+                V{0.0f, 0.0f, 0.0f}};   // the same LDS slot offset as fk_stream_tile
     const int lane = threadIdx.x;
     Q prev = qident();
     V unused = V{0.0f, 0.0f, 0.0f};
@@ -1024,7 +1086,7 @@ RTG_DEV void local_rotation_tile(const TopoView &T, const float *__restrict__ g_
 }
 
 template <bool STATE>
-__global__ __launch_bounds__(kFkTile) void k_local_rotation_stream(TopoView T, const float *__restrict__ g_rot,
+__global__ __launch_bounds__(kFkTile) RTG_FK_WAVES void k_local_rotation_stream(TopoView T, const float *__restrict__ g_rot,
                                                                    int64_t B, float *__restrict__ local_rot)
 {
     extern __shared__ __attribute__((aligned(16))) float fk_lds[];
@@ -1033,7 +1095,7 @@ __global__ __launch_bounds__(kFkTile) void k_local_rotation_stream(TopoView T, c
 
 // Mixed-target kinematics (BASELINE config 5): every 64-frame tile of every segment is one wave; a segment is FK
 // (op 0) or inverse FK (op 1), so FK and inverse FK of several skeletons share one launch.
-__global__ __launch_bounds__(kFkTile) void k_fk_multi_stream(FkMultiArgs A)
+__global__ __launch_bounds__(kFkTile) RTG_FK_WAVES void k_fk_multi_stream(FkMultiArgs A)
 {
     extern __shared__ __attribute__((aligned(16))) float fk_lds[];
     int s = 0;
@@ -1070,7 +1132,7 @@ RTG_DEV float dof_get(const DofRegs &r, int k)
 }
 
 template <bool CLIP>
-__global__ __launch_bounds__(kFkTile) void k_dof_fk(TopoView T, DofView D, const float *__restrict__ dof,
+__global__ __launch_bounds__(kFkTile) RTG_FK_WAVES void k_dof_fk(TopoView T, DofView D, const float *__restrict__ dof,
                                                     const float *__restrict__ root_rot,
                                                     const float *__restrict__ root_t, int64_t B,
                                                     float *__restrict__ g_rot, float *__restrict__ g_pos)
@@ -1080,8 +1142,9 @@ __global__ __launch_bounds__(kFkTile) void k_dof_fk(TopoView T, DofView D, const
     const int64_t f0 = (int64_t)blockIdx.x * kFkTile;
     const int nfr = (int)((B - f0) < kFkTile ? (B - f0) : kFkTile);
     float *rot = fk_lds;
-    float *pos = fk_lds + kFkTile * kRotPitch;
-    float *slots = pos + kFkTile * kPosPitch;
+    float *pos = fk_lds + kFkTile * kRotPitch;   // [64][kPosPitch] (RTG_DOF_FK_POS_REGS: none)
+    Slots slots{pos + kDofPosWin, qident(), qident(), V{0.0f, 0.0f, 0.0f}, V{0.0f, 0.0f, 0.0f}};
+    V pk[kFkChunk];   // RTG_DOF_FK_POS_REGS: the window's positions
     const int lane = threadIdx.x;
     const bool active = lane < nfr;
     const int64_t f = f0 + (active ? lane : 0);
@@ -1126,7 +1189,8 @@ __global__ __launch_bounds__(kFkTile) void k_dof_fk(TopoView T, DofView D, const
                     nt = V{rv.x + t.x, rv.y + t.y, rv.z + t.z};
                 }
                 R[4 * k] = ng.x; R[4 * k + 1] = ng.y; R[4 * k + 2] = ng.z; R[4 * k + 3] = ng.w;
-                P[3 * k] = nt.x; P[3 * k + 1] = nt.y; P[3 * k + 2] = nt.z;
+                if (RTG_DOF_FK_POS_REGS) pk[k] = nt;
+                else { P[3 * k] = nt.x; P[3 * k + 1] = nt.y; P[3 * k + 2] = nt.z; }
                 if (((sc >> 8) & 0xFF) != kNoSlot) slot_put(slots, (sc >> 8) & 0xFF, ng, nt);
                 g = ng;
                 t = nt;
@@ -1134,7 +1198,19 @@ __global__ __launch_bounds__(kFkTile) void k_dof_fk(TopoView T, DofView D, const
         }
         wave_sync();
         chunk_store<4>(g_rot, rot, kRotPitch, f0, nfr, J, c0, nC);
-        chunk_store<3>(g_pos, pos, kPosPitch, f0, nfr, J, c0, nC);
+        if (RTG_DOF_FK_POS_REGS) {   // the rotation rows are out: reuse the window for the positions
+            wave_sync();
+            if (active) {
+                float *P = rot + lane * kRotPitch;
+#pragma unroll
+                for (int k = 0; k < kFkChunk; ++k)
+                    if (k < nC) { P[3 * k] = pk[k].x; P[3 * k + 1] = pk[k].y; P[3 * k + 2] = pk[k].z; }
+            }
+            wave_sync();
+            chunk_store<3>(g_pos, rot, kRotPitch, f0, nfr, J, c0, nC);
+        } else {
+            chunk_store<3>(g_pos, pos, kPosPitch, f0, nfr, J, c0, nC);
+        }
         wave_sync();
     }
 }

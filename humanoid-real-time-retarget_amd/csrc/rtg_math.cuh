@@ -646,27 +646,20 @@ RTG_DEV void la_bdsqr3(float &d1, float &d2, float &d3, float e1, float e2, Svd3
     const float thresh = fmaxf(tol * sminoa, 6.0f * (3.0f * (3.0f * unfl)));
     int m = 3, iter = -1, iterdivn = 0;
     bool mir = false, fresh = true;   // mir: IDIR = 2; fresh: (ll, m) = (1, 3) differs from (oldll, oldm)
+    // A lane whose last step is a 2x2 block leaves the loop with blk set, and the block (SLASV2 + its two
+    // rotations) runs once after the loop for every such lane: the lanes of a wave finish at different sweeps,
+    // and inside the loop the block would execute once per distinct exit sweep.  Same operations, same values.
+    bool blk = false, p1 = false;
     for (;;) {
         if (m <= 1) break;
         if (iter >= 3) { iter -= 3; if (++iterdivn >= 18) break; }   // no convergence: INFO > 0 (never seen)
-        bool blk = false, p1 = false;
         if (m == 2) {                       // block (1, 2)
             if (fabsf(e1) <= thresh) break;
             blk = true;
-        } else {
-            if (fabsf(e2) <= thresh) { e2 = 0.0f; m = 2; continue; }
-            if (fabsf(e1) <= thresh) { e1 = 0.0f; blk = true; p1 = true; }   // split at E(1): block (2, 3)
-        }
-        if (blk) {   // 2x2 block (p1 ? 2 : 1, +1)
-            float sigmn, sigmx, sinr, cosr, sinl, cosl;
-            la_lasv2(p1 ? d2 : d1, p1 ? e2 : e1, p1 ? d3 : d2, sigmn, sigmx, sinr, cosr, sinl, cosl);
-            d1 = p1 ? d1 : sigmx;
-            d2 = p1 ? sigmx : sigmn;
-            d3 = p1 ? sigmn : d3;
-            vt_rot(z, p1, cosr, sinr);
-            u_rot(z, p1, cosl, sinl);
             break;
         }
+        if (fabsf(e2) <= thresh) { e2 = 0.0f; m = 2; continue; }
+        if (fabsf(e1) <= thresh) { e1 = 0.0f; blk = true; p1 = true; break; }   // split at E(1): block (2, 3)
         const float smax = fmaxf(fmaxf(fabsf(d3), fmaxf(fabsf(d2), fabsf(e2))), fmaxf(fabsf(d1), fabsf(e1)));
         if (fresh) { mir = !(fabsf(d1) >= fabsf(d3)); fresh = false; }
         // the IDIR = 1 form on (D1, D2, D3; E1, E2) = mir ? (d3, d2, d1; e2, e1) : (d1, d2, d3; e1, e2)
@@ -746,6 +739,15 @@ RTG_DEV void la_bdsqr3(float &d1, float &d2, float &d3, float e1, float e2, Svd3
         vt_rot(z, !mir, mir ? dc : cc, mir ? -ds : cs);
         u_rot(z, mir, mir ? ac : bc, mir ? -as : bs);
         u_rot(z, !mir, mir ? cc : dc, mir ? -cs : ds);
+    }
+    if (blk) {   // 2x2 block (p1 ? 2 : 1, +1)
+        float sigmn, sigmx, sinr, cosr, sinl, cosl;
+        la_lasv2(p1 ? d2 : d1, p1 ? e2 : e1, p1 ? d3 : d2, sigmn, sigmx, sinr, cosr, sinl, cosl);
+        d1 = p1 ? d1 : sigmx;
+        d2 = p1 ? sigmx : sigmn;
+        d3 = p1 ? sigmn : d3;
+        vt_rot(z, p1, cosr, sinr);
+        u_rot(z, p1, cosl, sinl);
     }
     // singular values made positive (VT rows negated), then sorted decreasing (SBDSQR :160-190)
     if (d1 < 0.0f) { d1 = -d1; z.vt[0] = -z.vt[0]; z.vt[3] = -z.vt[3]; z.vt[6] = -z.vt[6]; }
@@ -912,9 +914,13 @@ RTG_DEV void kabsch_rot(const float A[9], float R[9])
     }
 }
 
-// cal_joint_quat (transform3d.py:31-50): A = M^T Z by einsum (sequential in j, no FMA)
-template <int N>
-RTG_DEV Q cal_joint_quat(const V (&Z)[N], const V (&M)[N])
+// cal_joint_quat (transform3d.py:31-50): A = M^T Z by einsum (sequential in j, no FMA).  `hook(k)` marks the
+// stages (0: A formed, 1: rotation) for the latency-phase measurement knob; a no-op otherwise.
+struct NoHook {
+    RTG_DEV void operator()(int) const {}
+};
+template <int N, typename Hook = NoHook>
+RTG_DEV Q cal_joint_quat(const V (&Z)[N], const V (&M)[N], const Hook &hook = Hook{})
 {
     float A[9];
 #pragma unroll
@@ -931,8 +937,10 @@ RTG_DEV Q cal_joint_quat(const V (&Z)[N], const V (&M)[N])
             }
             A[i * 3 + k] = acc;
         }
+    hook(0);
     float R[9];
     kabsch_rot(A, R);
+    hook(1);
     return qfrom_rotmat(R);
 }
 

@@ -51,8 +51,32 @@ def load(d: str):
     return out
 
 
-SOLVER = "rtg::k_solve_sides<0, true, false>"
+SOLVERS = ("rtg::k_solve_sides<0, true, true>",    # SoA inputs (the bench headline)
+           "rtg::k_solve_sides<0, true, false>")   # AoS rows (the reference's layout, secondary line)
 VALU_PEAK_LANE_OPS = 256 * 4 * 32 * 2.4e9    # CUs x SIMDs x lanes/cycle x clock (fp32 FMA-issue rate)
+
+
+def solver_record(SOLVER, fetch, write, sq, nt, factor, kb):
+    """Calibrated traffic and the SQ instruction mix of one solver kernel."""
+    rec = {"kernel": SOLVER, "grid": fetch[SOLVER]["grid"], "fetch_size_raw": fetch[SOLVER]["FETCH_SIZE"] * kb,
+           "write_bytes": write[SOLVER]["WRITE_SIZE"] * kb, "fetch_correction": factor,
+           "fetch_correction_source": "tools/fetch_calib.hip k_stream16 (counter unit: 128-B requests at 64 B); "
+                                      "k_gather<63, 21> corroborates for the 12-byte gather shape"}
+    rec["fetch_bytes"] = rec["fetch_size_raw"] * factor
+    rec["traffic_bytes"] = rec["fetch_bytes"] + rec["write_bytes"]
+    if SOLVER in nt:
+        rec["fetch_bytes_no_angle_table"] = nt[SOLVER]["FETCH_SIZE"] * kb * factor
+        rec["angle_table_fetch_bytes"] = rec["fetch_bytes"] - rec["fetch_bytes_no_angle_table"]
+    s = sq.get(SOLVER, {})
+    if "SQ_INSTS_VALU" in s:
+        rec["valu_insts"] = s["SQ_INSTS_VALU"]
+        rec["waves"] = s.get("SQ_WAVES")
+        # issue weights: f64 add/mul/fma at half rate, f64 transcendentals at an eighth, f32 ones at a quarter
+        w64 = sum(s.get(f"SQ_INSTS_VALU_{k}_F64", 0.0) for k in ("ADD", "MUL", "FMA"))
+        rec["valu_issue_weighted"] = (s["SQ_INSTS_VALU"] + w64 + 7 * s.get("SQ_INSTS_VALU_TRANS_F64", 0.0) +
+                                      3 * s.get("SQ_INSTS_VALU_TRANS_F32", 0.0))
+        rec.update({k: v for k, v in s.items() if k.startswith("SQ_")})
+    return rec
 
 
 def main() -> None:
@@ -79,29 +103,15 @@ def main() -> None:
                 calib[k]["known_write_bytes"] = known[k]["write_bytes"]
         res["calibration"] = calib
     factor = calib.get("k_stream16", {}).get("known_over_counter", 2.0)
-    rec = {"kernel": SOLVER, "grid": fetch[SOLVER]["grid"], "fetch_size_raw": fetch[SOLVER]["FETCH_SIZE"] * kb,
-           "write_bytes": write[SOLVER]["WRITE_SIZE"] * kb, "fetch_correction": factor,
-           "fetch_correction_source": "tools/fetch_calib.hip k_stream16 (counter unit: 128-B requests at 64 B); "
-                                      "k_gather<63, 21> corroborates for the 12-byte gather shape"}
-    rec["fetch_bytes"] = rec["fetch_size_raw"] * factor
-    rec["traffic_bytes"] = rec["fetch_bytes"] + rec["write_bytes"]
     nt = load(os.path.join(d, "notab_fetch"))
-    if SOLVER in nt:
-        rec["fetch_bytes_no_angle_table"] = nt[SOLVER]["FETCH_SIZE"] * kb * factor
-        rec["angle_table_fetch_bytes"] = rec["fetch_bytes"] - rec["fetch_bytes_no_angle_table"]
-    s = sq.get(SOLVER, {})
-    if "SQ_INSTS_VALU" in s:
-        rec["valu_insts"] = s["SQ_INSTS_VALU"]
-        rec["waves"] = s.get("SQ_WAVES")
-        # issue weights: f64 add/mul/fma at half rate, f64 transcendentals at an eighth, f32 ones at a quarter
-        w64 = sum(s.get(f"SQ_INSTS_VALU_{k}_F64", 0.0) for k in ("ADD", "MUL", "FMA"))
-        rec["valu_issue_weighted"] = (s["SQ_INSTS_VALU"] + w64 + 7 * s.get("SQ_INSTS_VALU_TRANS_F64", 0.0) +
-                                      3 * s.get("SQ_INSTS_VALU_TRANS_F32", 0.0))
-        rec.update({k: v for k, v in s.items() if k.startswith("SQ_")})
-    res[SOLVER] = rec
+    for SOLVER in SOLVERS:
+        if SOLVER not in fetch:
+            continue
+        res[SOLVER] = rec = solver_record(SOLVER, fetch, write, sq, nt, factor, kb)
+        print(SOLVER)
+        print(json.dumps({k: (round(v / 1e6, 2) if isinstance(v, float) and v > 1e5 else v) for k, v in rec.items()},
+                         indent=1))
     json.dump(res, open(out_path, "w"), indent=1)
-    print(json.dumps({k: (round(v / 1e6, 2) if isinstance(v, float) and v > 1e5 else v) for k, v in rec.items()},
-                     indent=1))
     for k, v in calib.items():
         print(f"calib {k:18s} counter {v['fetch_size_bytes'] / 1e6:9.2f} MB  known {v['known_bytes'] / 1e6:9.2f} MB  "
               f"known/counter {v['known_over_counter']:.3f}")
