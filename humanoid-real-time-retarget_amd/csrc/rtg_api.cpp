@@ -487,6 +487,21 @@ int rtg_retarget_f32(rtg_solver_t s, const float *in0, const float *in1, const f
     return RTG_OK;
 }
 
+int rtg_frame_server_launch(rtg_solver_t s, const float *in, float *dof, float *local_rot, float *body_rot,
+                            uint32_t *ctl, uint32_t idle_ms, rtg_stream_t stream)
+{
+    if (!s) return fail(RTG_ERR_INVALID_ARGUMENT, "rtg_frame_server_launch: NULL solver");
+    if (s->kind != RTG_SOLVER_FULL_BODY_POS)
+        return fail(RTG_ERR_UNSUPPORTED, "rtg_frame_server_launch: only FULL_BODY_POS solvers are served per frame");
+    if (!in || !dof || !ctl) return fail(RTG_ERR_INVALID_ARGUMENT, "rtg_frame_server_launch: NULL in / dof / ctl");
+    if (idle_ms == 0 || idle_ms > 60000)
+        return fail(RTG_ERR_INVALID_ARGUMENT, "rtg_frame_server_launch: idle_ms=%u (1..60000)", idle_ms);
+    RTG_TRY(launch_frame_server(s->precise, s->consts, in, dof, local_rot, body_rot, ctl, (uint64_t)idle_ms * 100000u,
+                                as_stream(stream)),
+            "k_frame_server");
+    return RTG_OK;
+}
+
 // ---------------------------------------------------------------- primitives
 int rtg_quat_op_f32(int op, const float *a, const float *b, const float *c, int64_t n, float *out,
                     rtg_stream_t stream)

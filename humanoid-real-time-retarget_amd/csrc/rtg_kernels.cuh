@@ -63,6 +63,8 @@ struct FkMultiArgs {
 
 hipError_t launch_solver_prep(SolverConsts *dev_consts, hipStream_t s);
 hipError_t launch_build_ang_tab(uint32_t *tab, hipStream_t s);   // kAngTabWords words
+hipError_t launch_frame_server(int precise, const SolverConsts &C, const float *in, float *dof, float *local_rot,
+                               float *body_rot, uint32_t *ctl, uint64_t idle_ticks, hipStream_t s);
 hipError_t launch_retarget(int kind, int precise, const SolverConsts &C, const float *in0, const float *in1,
                            const float *in2, const float *in3, int64_t B, int layout, float *dof, float *local_rot,
                            float *body_rot, hipStream_t s);

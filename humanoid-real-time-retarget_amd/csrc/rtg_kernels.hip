@@ -733,6 +733,221 @@ __global__ __launch_bounds__(192) void k_fbp_latency(SolverConsts C, const float
 }
 
 // ----------------------------------------------------------------------------
+// FULL_BODY_POS latency kernel, five waves per 64-frame tile (RTG_LATENCY_WAVES = 5).  The arm chain
+// (shoulder_pr / elbow_py, full_body_pos_retargeter.py:75-93) needs only the torso fit R10, not the wrist fit, so
+// it runs on its own wave as soon as R10 is in LDS -- concurrently with the (longer) wrist SVDs -- instead of after a
+// block barrier that waits for all three fits (measured phase split, tools/latency_phases.py: torso fit 6-8 us,
+// wrist fits 9-13 us, arm 5-7 us, Euler 3-4 us).
+//   wave 0      torso fit -> R10 -> fixed links
+//   wave 1, 2   left / right wrist fit -> gripper; then (arm chain ready) Euler split, body_rot rows, exp-maps
+//   wave 3, 4   left / right arm points; (R10 ready) arm chain -> LDS; the arm links' exp-maps
+// Hand-over is by per-wave LDS flags (release / acquire at workgroup scope): a producer never waits on a consumer,
+// and all five waves of a workgroup are resident together, so the waits always end; each also has an iteration
+// cap.  Every value is computed by the same device function from the same operands as in k_fbp_latency /
+// k_solve_sides: the same bits (test_solver_batch_invariance covers both sizes).
+// ----------------------------------------------------------------------------
+#ifndef RTG_LATENCY_WAVES
+#define RTG_LATENCY_WAVES 5   // 5: k_fbp_latency5 (arm chain concurrent with the wrist fits); 3: k_fbp_latency
+#endif
+// A release is per lane, but the hand-over is per wave: the lanes that skipped the work (frames past B) must not
+// raise the flag on their own -- the compiler may run their path first (it did: the flag went up before the live
+// lanes' writes).  So the flag goes up after a convergent ballot, where the whole wave has rejoined and every
+// lane's LDS writes have issued, from one lane, with a release (s_waitcnt lgkmcnt(0) before the store).
+RTG_DEV void lds_signal(int *flag)
+{
+    const uint64_t joined = __builtin_amdgcn_ballot_w64(true);
+    if (joined != 0 && (threadIdx.x & 63) == (unsigned)__builtin_ctzll(joined))
+        __hip_atomic_store(flag, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+RTG_DEV void lds_wait(int *flag)
+{
+    for (int it = 0; it < (1 << 22); ++it) {   // ~0.1 s at s_sleep 1: a bound every wave reaches
+        if (__hip_atomic_load(flag, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP)) return;
+        __builtin_amdgcn_s_sleep(1);
+    }
+}
+
+// one 64-frame tile (frames f0..) by the 320 threads of a workgroup; shared by the batched latency kernel and the
+// per-frame server (k_frame_server)
+template <bool PRECISE, bool SOA>
+RTG_DEV void fbp_latency5_tile(const SolverConsts &C, const float *__restrict__ in0, const float *__restrict__ in1,
+                               const float *__restrict__ in2, int64_t B, int64_t f0, float *__restrict__ dof,
+                               float *__restrict__ local_rot, float *__restrict__ body_rot)
+{
+    __shared__ float sdof[kLatFrames * kDofStride];
+    __shared__ float4 sfit[kLatFrames];        // R10
+    __shared__ float4 schain[2][kLatFrames];   // quat_mul_four of each arm's links (the wrist parent chain)
+    __shared__ float2 sst[14 * kLatFrames];
+    __shared__ int sflag[3];                   // R10 ready, left arm ready, right arm ready
+    const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int64_t f = f0 + lane;
+    const bool live = f < B;
+    if (threadIdx.x < 3) sflag[threadIdx.x] = 0;
+    __syncthreads();
+#if RTG_EXP_TIMESTAMPS
+    float *const tsb = body_rot;
+    body_rot = nullptr;
+    auto TS = [&](int k) {
+        if (tsb && blockIdx.x == 0 && lane == 0) {
+            const uint64_t t = wall_clock64();
+            reinterpret_cast<uint32_t *>(tsb)[2 * (16 * w + k)] = (uint32_t)t;
+            reinterpret_cast<uint32_t *>(tsb)[2 * (16 * w + k) + 1] = (uint32_t)(t >> 32);
+        }
+    };
+#else
+    auto TS = [](int) {};
+#endif
+    auto hook = [&](int k) { TS(8 + k); };
+    TS(0);
+    const Emit E{sdof + lane * kDofStride, live && local_rot ? local_rot + f * 124 : nullptr, C.ang_tab, sst + lane,
+                 kLatFrames};
+    auto view = [&](const float *base, int row_floats) { return frame_view<SOA>(base, f, row_floats, B); };
+    const auto b = view(in0, 63);
+    if (w == 0) {
+        if (live) {
+            const Q q = fbp_torso(C, b, hook);
+            sfit[lane] = make_float4(q.x, q.y, q.z, q.w);
+        }
+        lds_signal(&sflag[0]);
+        TS(1);
+        if (live) emit_fixed_links(E);
+        TS(2);
+    } else if (w >= 3) {
+        const int side = w - 3;
+        ArmPts ap{};
+        if (live) ap = side ? load_arm<1>(b) : load_arm<0>(b);
+        TS(1);
+        lds_wait(&sflag[0]);
+        TS(2);
+        if (live) {
+            const float4 t = sfit[lane];
+            const Q R10{t.x, t.y, t.z, t.w};
+            const V up = vsub(ap.el, ap.sh), fo = vsub(ap.wr, ap.el);
+            const Q ch = side ? solve_arm<21>(E, up, fo, C.rsh, C.rel, R10) : solve_arm<12>(E, up, fo, C.lsh, C.lel, R10);
+            schain[side][lane] = make_float4(ch.x, ch.y, ch.z, ch.w);
+        }
+        lds_signal(&sflag[1 + side]);
+        TS(3);
+        if (live) E.finalize(side ? 7 : 0, 4);
+        TS(4);
+    } else {
+        const int side = w - 1;
+        const auto H = view(side ? in2 : in1, 60);
+        Q W = qident();
+        TipPts tp{};
+        if (live) {
+            W = side ? fbp_wrist_fit<1>(C, H, hook) : fbp_wrist_fit<0>(C, H, hook);
+            tp = load_tips(H);
+        }
+        TS(1);
+        float a = 0.0f;
+        if (live) a = hand_x_mean(qconj(W), tp.h0, tp.t);   // the gripper needs only W (:142-158 / :165-175)
+        TS(2);
+        lds_wait(&sflag[1 + side]);   // the arm waited for R10 first: both are visible (release / acquire chain)
+        TS(3);
+        if (live) {
+            const float4 t = sfit[lane], c = schain[side][lane];
+            const Q R10{t.x, t.y, t.z, t.w}, chain{c.x, c.y, c.z, c.w};
+            float *brow = body_rot ? body_rot + f * 236 : nullptr;
+            const int D0 = side ? 27 : 18;
+            if (PRECISE) {
+                const float sc = clamp_lohi(a / C.orig - 0.5f, 0.0f, 0.5f) / 0.5f;
+                E.row[D0] = sc * 0.044f;
+                E.row[D0 + 1] = sc * -0.044f;
+            } else {
+                const bool closed = a / C.orig < 0.7f;
+                E.row[D0] = closed ? 0.0f : 0.044f;
+                E.row[D0 + 1] = closed ? 0.0f : -0.044f;
+            }
+            const Q loc = qmul_norm(qconj(qmul_norm(R10, chain)), W);
+            if (side) emit_euler_xyz<25>(E, loc);
+            else emit_euler_xyz<16>(E, loc);
+            if (brow) {   // body_global_rotation rows (:116, :172-173), as solve_fbp_side
+                st4(brow + 4 * (side ? 39 : 14), W);
+                if (!side)
+                    for (int j = 0; j < 59; ++j)
+                        if (j != 14 && j != 39) st4(brow + 4 * j, j == 10 ? R10 : qident());
+            }
+            TS(4);
+            E.finalize(side ? 11 : 4, 3);
+        }
+    }
+    TS(5);
+    __syncthreads();
+    TS(6);
+    const int64_t nrows = (B - f0) < kLatFrames ? (B - f0) : kLatFrames;
+    const int nvals = (int)nrows * 30;
+    float *dst = dof + f0 * 30;
+    auto at = [&](int i) {
+        const int rr = i / 30;
+        return sdof[rr * kDofStride + (i - rr * 30)];
+    };
+    const int nvec = nvals >> 2;
+    for (int v = threadIdx.x; v < nvec; v += 320) {
+        const int i = v << 2;
+        *reinterpret_cast<float4 *>(dst + i) = make_float4(at(i), at(i + 1), at(i + 2), at(i + 3));
+    }
+    for (int i = (nvec << 2) + threadIdx.x; i < nvals; i += 320) dst[i] = at(i);
+    TS(7);
+}
+
+template <bool PRECISE, bool SOA>
+__global__ __launch_bounds__(320) void k_fbp_latency5(SolverConsts C, const float *__restrict__ in0,
+                                                      const float *__restrict__ in1, const float *__restrict__ in2,
+                                                      int64_t B, float *__restrict__ dof, float *__restrict__ local_rot,
+                                                      float *__restrict__ body_rot)
+{
+    fbp_latency5_tile<PRECISE, SOA>(C, in0, in1, in2, B, (int64_t)blockIdx.x * kLatFrames, dof, local_rot, body_rot);
+}
+
+// ----------------------------------------------------------------------------
+// Per-frame server (the teleop loop without a launch per frame; sim_full_body_teleop.py:109-119 calls the solver
+// once per captured frame).  One resident workgroup of k_fbp_latency5's shape serves FULL_BODY_POS frames from
+// host-mapped memory: the host writes a frame's rows (body | left hand | right hand, AoS) into `in` and then a new
+// sequence number into ctl[0]; thread 0 sees it (system-scope acquire), the tile runs at B = 1 reading `in` and
+// writing dof / local_rot / body_rot straight into host memory, every wave's stores are released at system scope,
+// and thread 0 publishes the sequence number in ctl[1].  The loop ends on ctl[0] == RTG_SERVER_QUIT, or when no
+// new frame arrives for idle_ticks (100 MHz wall clock) -- every wave reaches one of the two -- and sets ctl[2].
+// ----------------------------------------------------------------------------
+template <bool PRECISE>
+__global__ __launch_bounds__(320) void k_frame_server(SolverConsts C, const float *in, float *dof, float *local_rot,
+                                                      float *body_rot, uint32_t *ctl, uint64_t idle_ticks)
+{
+    __shared__ uint32_t scmd;
+    uint32_t last = 0;
+    if (threadIdx.x == 0) last = __hip_atomic_load(ctl + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    for (int frame = 0; frame < (1 << 30); ++frame) {
+        if (threadIdx.x == 0) {
+            const uint64_t t0 = wall_clock64();
+            uint32_t db;
+            for (;;) {
+                db = __hip_atomic_load(ctl, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM);
+                if (db != last) break;
+                if (wall_clock64() - t0 > idle_ticks) {
+                    db = RTG_SERVER_QUIT;
+                    break;
+                }
+                __builtin_amdgcn_s_sleep(2);
+            }
+            scmd = db;
+        }
+        __syncthreads();
+        const uint32_t cmd = scmd;
+        if (cmd == RTG_SERVER_QUIT) break;   // block-uniform
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");   // this wave's loads see the host's frame, not cached lines
+        fbp_latency5_tile<PRECISE, false>(C, in, in + 63, in + 123, 1, 0, dof, local_rot, body_rot);
+        __syncthreads();   // every lane of every wave has issued its output stores (a convergent point) ...
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");   // ... so this wave's release covers all of them
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            __hip_atomic_store(ctl + 1, cmd, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+            last = cmd;
+        }
+    }
+    if (threadIdx.x == 0) __hip_atomic_store(ctl + 2, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+// ----------------------------------------------------------------------------
 // forward kinematics -- one frame per lane, joints in topological (index) order.
 // The parent's global rotation / position is reused from registers when the
 // parent is the previous joint (chains), else re-read from the output rows this
@@ -838,6 +1053,9 @@ constexpr int kPosWin = RTG_FK_POS_REGS ? 0 : kFkTile * kPosPitch;   // floats o
 #ifndef RTG_FK_REG_SLOTS
 #define RTG_FK_REG_SLOTS 0
 #endif
+#ifndef RTG_FK_NT_STORE
+#define RTG_FK_NT_STORE 0   // 1: FK output rows leave with non-temporal stores (written once, never re-read here)
+#endif
 #ifndef RTG_DOF_FK_POS_REGS
 #define RTG_DOF_FK_POS_REGS 1   // k_dof_fk positions staged through the rotation window (as RTG_FK_POS_REGS; measured +7-9 %)
 #endif
@@ -910,10 +1128,19 @@ RTG_DEV void chunk_store(float *__restrict__ g, const float *lds, int pitch, int
         float *gp = g + ((f0 + fr) * J + c0 + k) * W;
         const float *lp = lds + fr * pitch + k * W;
         if (W == 4) {
-            *reinterpret_cast<float4 *>(gp) = *reinterpret_cast<const float4 *>(lp);
+            if (RTG_FK_NT_STORE) {
+                typedef float f4v __attribute__((ext_vector_type(4)));
+                const f4v v = *reinterpret_cast<const f4v *>(lp);
+                __builtin_nontemporal_store(v, reinterpret_cast<f4v *>(gp));
+            } else {
+                *reinterpret_cast<float4 *>(gp) = *reinterpret_cast<const float4 *>(lp);
+            }
         } else {
 #pragma unroll
-            for (int c = 0; c < W; ++c) gp[c] = lp[c];
+            for (int c = 0; c < W; ++c) {
+                if (RTG_FK_NT_STORE) __builtin_nontemporal_store(lp[c], gp + c);
+                else gp[c] = lp[c];
+            }
         }
     };
     if (nfr == kFkTile && nC == kFkChunk) {   // full window: unpredicated, LDS reads batch ahead of the stores
@@ -1752,7 +1979,14 @@ static void launch_kind(const SolverConsts &C, const float *in0, const float *in
                         const float *in3, int64_t B, int layout, float *dof, float *local_rot, float *body_rot,
                         hipStream_t s)
 {
-    if (KIND == RTG_SOLVER_FULL_BODY_POS && B <= RTG_LATENCY_MAX_B) {
+    if (KIND == RTG_SOLVER_FULL_BODY_POS && B <= RTG_LATENCY_MAX_B && RTG_LATENCY_WAVES == 5) {
+        if (layout == RTG_LAYOUT_SOA)
+            hipLaunchKernelGGL((k_fbp_latency5<PRECISE, true>), dim3(grid_for(B, kLatFrames)), dim3(320), 0, s, C,
+                               in0, in1, in2, B, dof, local_rot, body_rot);
+        else
+            hipLaunchKernelGGL((k_fbp_latency5<PRECISE, false>), dim3(grid_for(B, kLatFrames)), dim3(320), 0, s, C,
+                               in0, in1, in2, B, dof, local_rot, body_rot);
+    } else if (KIND == RTG_SOLVER_FULL_BODY_POS && B <= RTG_LATENCY_MAX_B) {
         if (layout == RTG_LAYOUT_SOA)
             hipLaunchKernelGGL((k_fbp_latency<PRECISE, true>), dim3(grid_for(B, kLatFrames)), dim3(192), 0, s, C, in0,
                                in1, in2, B, dof, local_rot, body_rot);
@@ -1768,6 +2002,18 @@ static void launch_kind(const SolverConsts &C, const float *in0, const float *in
     else
         hipLaunchKernelGGL((k_solve_sides<KIND, PRECISE, false>), dim3(grid_for(B, kSideFrames)), dim3(256), 0, s, C,
                            in0, in1, in2, in3, B, dof, local_rot, body_rot);
+}
+
+hipError_t launch_frame_server(int precise, const SolverConsts &C, const float *in, float *dof, float *local_rot,
+                               float *body_rot, uint32_t *ctl, uint64_t idle_ticks, hipStream_t s)
+{
+    if (precise)
+        hipLaunchKernelGGL((k_frame_server<true>), dim3(1), dim3(320), 0, s, C, in, dof, local_rot, body_rot, ctl,
+                           idle_ticks);
+    else
+        hipLaunchKernelGGL((k_frame_server<false>), dim3(1), dim3(320), 0, s, C, in, dof, local_rot, body_rot, ctl,
+                           idle_ticks);
+    return hipGetLastError();
 }
 
 hipError_t launch_retarget(int kind, int precise, const SolverConsts &C, const float *in0, const float *in1,

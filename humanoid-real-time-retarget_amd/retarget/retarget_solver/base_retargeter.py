@@ -45,13 +45,14 @@ class BaseHumanoidRetargeter(ABC):
 
     def _solve(self, inputs: Sequence, batched: bool, want_body_rot=False):
         """Run the device solver on (B, ...) or single-frame inputs; returns (local_rot, dof, body_rot).
-        A single frame of host inputs (the live teleop loop) replays a captured HIP graph (rtg.realtime)."""
+        A single frame of host inputs (the live teleop loop) goes to the resident frame server (FULL_BODY_POS) or a
+        one-launch frame call over pinned memory (rtg.realtime.per_frame_runner)."""
         dev = home_device(*inputs)
         if not batched and dev.type == "cpu":
             g = self._frame_graphs.get(bool(want_body_rot))
             if g is None:
-                from rtg.realtime import FrameGraph
-                g = self._frame_graphs[bool(want_body_rot)] = FrameGraph(self.solver, want_body_rot)
+                from rtg.realtime import per_frame_runner
+                g = self._frame_graphs[bool(want_body_rot)] = per_frame_runner(self.solver, want_body_rot)
             return g(*inputs)
         tails = [tuple(as_tensor(x).shape[-2:]) for x in inputs]
         xs = [dev_f32(as_tensor(x).reshape(-1, *t)) for x, t in zip(inputs, tails)]
@@ -60,6 +61,13 @@ class BaseHumanoidRetargeter(ABC):
             dof, lr = dof[0], lr[0]
             br = br[0] if br is not None else None
         return back(lr, dev), back(dof, dev), (back(br, dev) if br is not None else None)
+
+    def close(self):
+        """End the per-frame runners (a resident frame server occupies its stream until it ends or idles out)."""
+        for g in self._frame_graphs.values():
+            if hasattr(g, "close"):
+                g.close()
+        self._frame_graphs = {}
 
     def _record(self, local_rot, dof):
         self._motion_local_rotation.append(local_rot)

@@ -25,6 +25,7 @@ SOLVER_FULL_BODY_POS = 0
 SOLVER_UPPER_BODY = 1
 SOLVER_FULL_BODY_ROT = 2
 SOLVER_BODY_ROT = 3
+SERVER_QUIT = 0xFFFFFFFF   # rtg.h RTG_SERVER_QUIT
 
 # rtg_quat_op
 OP_QUAT_MUL = 0
@@ -96,6 +97,8 @@ SIGNATURES = {
     "rtg_solver_destroy": (c_int, [c_void_p]),
     "rtg_retarget_f32": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int64, c_int, c_void_p,
                                  c_void_p, c_void_p, c_void_p]),
+    "rtg_frame_server_launch": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, ctypes.c_uint32,
+                                        c_void_p]),
     "rtg_quat_op_f32": (c_int, [c_int, c_void_p, c_void_p, c_void_p, c_int64, c_void_p, c_void_p]),
     "rtg_cal_joint_quat_f32": (c_int, [c_void_p, c_void_p, c_int32, c_int64, c_void_p, c_void_p]),
     "rtg_quat_in_xyz_axis_f32": (c_int, [c_void_p, c_char_p, c_int64, c_void_p, c_void_p]),

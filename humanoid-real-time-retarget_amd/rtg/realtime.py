@@ -1,4 +1,9 @@
-"""Per-frame teleop path: one kernel launch over host-mapped pinned buffers.
+"""Per-frame teleop path: a resident frame server (FULL_BODY_POS) or one kernel launch over host-mapped pinned
+buffers (every kind).
+
+:class:`FrameServer` (rtg_frame_server_launch): one resident workgroup serves frames posted through a sequence
+number in pinned memory -- no launch per frame; 26 us median per frame on MI355X (tools/extra_bench.py latency),
+bit-identical to the batched solve.  The drop-in retargeters use it for host-input frames (per_frame_runner).
 
 The live loops (sim_full_body_teleop.py:115-119, sim_teleop.py:102) retarget one
 frame at a time from host arrays, so a call is launch- and copy-bound, not
@@ -19,6 +24,7 @@ nodes, bit-identical outputs.
 """
 from __future__ import annotations
 
+import os
 import time
 from typing import Sequence
 
@@ -92,3 +98,105 @@ class FrameGraph:
         dof = torch.from_numpy(out[124:154].copy())
         br = torch.from_numpy(out[154:].reshape(59, 4).copy()) if self.want_body_rot else None
         return lr, dof, br
+
+
+class FrameServer:
+    """FULL_BODY_POS frames served by one resident workgroup (rtg_frame_server_launch): no launch per frame.
+
+    Same call as :class:`FrameGraph` -- (body, left hand, right hand) host arrays -> (local_rot, dof[, body_rot])
+    host tensors, bit-identical -- but a frame is a host memcpy into pinned memory plus a sequence-number store; the
+    resident kernel sees it, writes the outputs into pinned memory and publishes the number back.  The server ends
+    on :meth:`close` (also at exit / garbage collection) or after ``idle_ms`` without a frame; a call after an
+    idle exit relaunches it (the pending frame is served by the new launch).  It runs on its own stream, which it
+    occupies until it ends: close it before a device-wide synchronize.
+    """
+
+    def __init__(self, solver: Solver, want_body_rot: bool = False, idle_ms: int = 200, timeout_s: float = 2.0):
+        dev = require_gpu()
+        if dev != solver.device:
+            raise ValueError(f"the solver lives on {solver.device}; the current device is {dev}")
+        from ._lib import SERVER_QUIT, SOLVER_FULL_BODY_POS
+        if solver.kind != SOLVER_FULL_BODY_POS:
+            raise ValueError("FrameServer serves FULL_BODY_POS solvers; use FrameGraph for the other kinds")
+        self._quit = np.uint32(SERVER_QUIT)
+        self.solver = solver
+        self.tails = _IN_TAILS[solver.kind]
+        self._in_offsets = np.cumsum([0] + [int(np.prod(t)) for t in self.tails])
+        self.want_body_rot = bool(want_body_rot)
+        self.h_in = torch.zeros(int(self._in_offsets[-1]), dtype=torch.float32).pin_memory()
+        self.h_out = torch.zeros(31 * 4 + 30 + (59 * 4 if want_body_rot else 0), dtype=torch.float32).pin_memory()
+        self.h_ctl = torch.zeros(4, dtype=torch.int32).pin_memory()
+        self._h_in_np = self.h_in.numpy()
+        self._ctl = self.h_ctl.numpy().view(np.uint32)
+        out = self.h_out.data_ptr()
+        self._args = [solver.handle, self.h_in.data_ptr(), out + 4 * 124, out, out + 4 * 154 if want_body_rot else None,
+                      self.h_ctl.data_ptr(), int(idle_ms)]
+        self.stream = torch.cuda.Stream(dev)
+        self.timeout_s = float(timeout_s)
+        self.seq = 0
+        self._running = False
+
+    def _launch(self):
+        self._ctl[2] = 0
+        check(lib().rtg_frame_server_launch(*self._args, stream_handle(self.stream)))
+        self._running = True
+
+    def _wait(self, seq):
+        ctl = self._ctl
+        spins, t0 = 0, None
+        while ctl[1] != seq:
+            spins += 1
+            if spins % 1024 == 0:
+                if ctl[2] and ctl[1] != seq and self.stream.query():   # ended on idle before it saw this frame
+                    self._launch()
+                    continue
+                t0 = t0 or time.perf_counter()
+                if time.perf_counter() - t0 > self.timeout_s:
+                    raise RtgError(-1, f"frame server: frame {seq} not served within {self.timeout_s} s")
+
+    def __call__(self, *inputs: Sequence):
+        if len(inputs) != len(self.tails):
+            raise ValueError(f"expected {len(self.tails)} inputs")
+        for x, a, b, t in zip(inputs, self._in_offsets[:-1], self._in_offsets[1:], self.tails):
+            arr = x.detach().numpy() if isinstance(x, torch.Tensor) else np.asarray(x)
+            if arr.size != b - a:
+                raise ValueError(f"input of {arr.size} values, expected shape {t}")
+            self._h_in_np[a:b] = arr.reshape(-1)
+        if not self._running or (self._ctl[2] and self.stream.query()):
+            self._launch()
+        self.seq = self.seq + 1 if self.seq + 1 < int(self._quit) else 1
+        self._ctl[0] = self.seq   # after the inputs (x86 stores are not reordered with older stores)
+        self._wait(self.seq)
+        out = self.h_out.numpy()
+        lr = torch.from_numpy(out[:124].reshape(31, 4).copy())
+        dof = torch.from_numpy(out[124:154].copy())
+        br = torch.from_numpy(out[154:].reshape(59, 4).copy()) if self.want_body_rot else None
+        return lr, dof, br
+
+    def close(self):
+        if self._running:
+            self._ctl[0] = self._quit
+            self.stream.synchronize()
+            self._running = False
+            self._ctl[0] = self._ctl[1] = self.seq
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+def per_frame_runner(solver: Solver, want_body_rot: bool = False):
+    """The per-frame call the drop-in retargeters use for host inputs: the resident :class:`FrameServer` for
+    FULL_BODY_POS (the teleop solver; RTG_FRAME_SERVER=0 turns it off), :class:`FrameGraph` otherwise."""
+    from ._lib import SOLVER_FULL_BODY_POS
+    if solver.kind == SOLVER_FULL_BODY_POS and os.environ.get("RTG_FRAME_SERVER", "1") != "0":
+        return FrameServer(solver, want_body_rot)
+    return FrameGraph(solver, want_body_rot)

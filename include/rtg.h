@@ -198,6 +198,21 @@ int rtg_retarget_f32(rtg_solver_t solver, const float *in0, const float *in1, co
                      const float *in3, int64_t B, int layout, float *dof, float *local_rot, float *body_rot,
                      rtg_stream_t stream);
 
+/* Per-frame server for the teleop loop (sim_full_body_teleop.py:109-119 retargets one captured frame per
+ * iteration through VtrdynFullBodyPosRetargeter.retarget, full_body_pos_retargeter.py:60-176): launches ONE
+ * resident workgroup that serves FULL_BODY_POS frames from host-mapped (pinned) memory without a launch per frame.
+ *   in        183 floats: body (21,3) | left hand (20,3) | right hand (20,3), rows as rtg_retarget_f32's AoS inputs
+ *   dof (30), local_rot (31,4, may be NULL), body_rot (59,4, may be NULL): written per frame
+ *   ctl       3 x uint32: [0] frame sequence number, written by the host after the frame's inputs;
+ *             [1] the last sequence number served, written by the device after that frame's outputs;
+ *             [2] set to 1 by the device when the server has ended.  Zero ctl[1], ctl[2] before the launch.
+ * Writing RTG_SERVER_QUIT into ctl[0] ends the server; so does idle_ms (1..60000) without a new frame.  All
+ * buffers must be device-accessible host memory (hipHostMalloc / pinned).  The stream is occupied until the
+ * server ends.  Outputs are bit-identical to rtg_retarget_f32 at B = 1. */
+#define RTG_SERVER_QUIT 0xFFFFFFFFu
+int rtg_frame_server_launch(rtg_solver_t solver, const float *in, float *dof, float *local_rot, float *body_rot,
+                            uint32_t *ctl, uint32_t idle_ms, rtg_stream_t stream);
+
 /* ------------------------------------------------------------------------
  * Elementwise primitives (poselib rotation3d.py, retarget transform3d.py)
  * ---------------------------------------------------------------------- */

@@ -237,6 +237,34 @@ def test_per_frame_graph_matches_batched(gpu):
     assert hu.motion_length == n
 
 
+def test_frame_server_matches_batched(gpu):
+    """The resident per-frame server (rtg_frame_server_launch, rtg.realtime.FrameServer) serves frame after frame
+    with exactly the batched solve's rows, relaunches itself after an idle exit, and ends on close()."""
+    import time
+
+    from retarget.retarget_solver import VtrdynFullBodyPosRetargeter
+    from robot_kinematics_model import RobotZeroPose
+    from rtg.realtime import FrameServer
+    g = golden("full_body_pos_precise")
+    hu = VtrdynFullBodyPosRetargeter(RobotZeroPose.from_asset("vtrdyn_full"), RobotZeroPose.from_asset("hu_v5"),
+                                     precise_gripper=True)
+    n = 48
+    lr_b, dof_b, br_b = hu.retarget_batch(torch.from_numpy(g["body"][:n]), torch.from_numpy(g["lh"][:n]),
+                                          torch.from_numpy(g["rh"][:n]), want_body_rot=True)
+    with FrameServer(hu.solver, want_body_rot=True, idle_ms=20) as fs:
+        for i in range(n):
+            if i == n // 2:
+                time.sleep(0.1)   # past idle_ms: the server has ended; the next call relaunches it
+                assert fs._ctl[2] == 1
+            lr, dof, br = fs(g["body"][i], g["lh"][i], g["rh"][i])
+            np.testing.assert_array_equal(dof.numpy(), dof_b[i].numpy())
+            np.testing.assert_array_equal(lr.numpy(), lr_b[i].numpy())
+            np.testing.assert_array_equal(br.numpy(), br_b[i].numpy())
+    assert not fs._running and fs._ctl[2] == 1
+    with pytest.raises(ValueError):
+        FrameServer(hu.solver, want_body_rot=True)(g["body"][0], g["lh"][0])
+
+
 def test_main_retarget_from_global_translation(gpu):
     """retarget/main.py RetargetHuV5fromMocap.retarget_from_global_translation (:169-279), unchanged call, against
     the reference run end to end (tests/golden/main_retarget.npz, plot_skeleton_H captured) and against the oracle

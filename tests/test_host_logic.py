@@ -55,6 +55,8 @@ def test_solver_and_op_validation():
     assert lib.rtg_quat_op_f32(99, None, None, None, 1, None, None) == 1
     assert lib.rtg_cal_joint_quat_f32(None, None, 9, 1, None, None) == 4
     assert lib.rtg_retarget_f32(None, None, None, None, None, 1, 0, None, None, None, None) == 1
+    assert lib.rtg_frame_server_launch(None, None, None, None, None, None, 200, None) == 1
+    assert b"NULL solver" in lib.rtg_last_error()
 
 
 def test_dof_model_validation():

@@ -78,11 +78,14 @@ def latency():
     hu = VtrdynFullBodyPosRetargeter(RobotZeroPose.from_asset("vtrdyn_full"), RobotZeroPose.from_asset("hu_v5"),
                                      precise_gripper=True)
     fb, fl, fr = (torch.from_numpy(np.ascontiguousarray(g[k][0])) for k in ("body", "lh", "rh"))
+    from rtg.realtime import FrameServer
     fg = FrameGraph(S, want_body_rot=False)
+    fsrv = FrameServer(S, want_body_rot=False)
     for name, fn in (("dropin_retarget_per_frame", lambda: hu.retarget(fb, fl, fr)),
                      ("dropin_batch_of_one_no_graph",
                       lambda: hu.retarget_batch(fb[None], fl[None], fr[None], want_body_rot=True)),
-                     ("frame_graph_dof_local_rot", lambda: fg(fb, fl, fr))):
+                     ("frame_graph_dof_local_rot", lambda: fg(fb, fl, fr)),
+                     ("frame_server_dof_local_rot", lambda: fsrv(fb, fl, fr))):
         for _ in range(20):
             fn()
         ts = []
@@ -91,6 +94,9 @@ def latency():
             fn()
             ts.append(time.perf_counter() - t0)
         out[name] = {"median_us": float(np.median(ts) * 1e6), "p99_us": float(np.quantile(ts, 0.99) * 1e6)}
+    a, b = fg(fb, fl, fr), fsrv(fb, fl, fr)
+    out["frame_server_bits_equal_frame_graph"] = bool(torch.equal(a[0], b[0]) and torch.equal(a[1], b[1]))
+    fsrv.close()
     return out
 
 

@@ -1,8 +1,9 @@
 """Where the per-frame (teleop) latency goes.
 
-  phases    -- needs a build with -DRTG_EXP_TIMESTAMPS=1 (RTG_LIB=...): block 0's lane 0 of each of the three
-               k_fbp_latency waves records the 100 MHz wall clock at 8 phase boundaries; prints the median phase
-               times (us) per wave at B=1 and B=4096
+  phases    -- needs a build with -DRTG_EXP_TIMESTAMPS=1 (RTG_LIB=...): block 0's lane 0 of each wave of
+               the latency kernel (k_fbp_latency5, or k_fbp_latency in an RTG_LATENCY_WAVES=3 build) records the
+               100 MHz wall clock at its stage boundaries; prints the median stage times (us) per wave at B=1 and
+               B=4096
   zerocopy  -- the B=1 call with the inputs and outputs in pinned host memory that the kernel reads / writes
                directly (no copy nodes), as a direct launch and as a one-node graph, next to the FrameGraph path
 """
@@ -42,6 +43,16 @@ def inputs(B, pinned=False, device=True):
     return [torch.from_numpy(a).pin_memory() if pinned else torch.from_numpy(a) for a in hs]
 
 
+# k_fbp_latency5 timestamp slots per wave (RTG_LATENCY_WAVES=5): 0 start, 1 own stage done, 2 next stage
+# (w0: fixed links; w1/2: gripper; w3/4: R10 received), 3 (w1/2: arm chain received; w3/4: arm done), 4 (w1/2:
+# Euler done; w3/4: arm exp-maps done), 5 pre-barrier, 6 post-barrier, 7 stored; 8/9 A formed / SVD done (fits)
+LAT5 = {0: {1: "torso_fit", 2: "fixed_links"},
+        1: {1: "wrist_fit", 2: "gripper", 3: "wait_arm", 4: "euler", 5: "euler_expmaps"},
+        3: {1: "arm_loads", 2: "wait_R10", 3: "arm", 4: "arm_expmaps"}}
+LAT5[2] = LAT5[1]
+LAT5[4] = LAT5[3]
+
+
 def phases():
     S = solver()
     out = {}
@@ -55,25 +66,38 @@ def phases():
             check(lib().rtg_retarget_f32(S.handle, ptr(ins[0]), ptr(ins[1]), ptr(ins[2]), None, B, 0, ptr(dof), None,
                                          ptr(ts), stream_handle()))
             torch.cuda.synchronize()
-            t = ts[:96].cpu().numpy().view(np.uint32).astype(np.uint64)
-            t = (t[0::2] | (t[1::2] << np.uint64(32))).reshape(3, 16).astype(np.int64)
+            t = ts[:160].cpu().numpy().view(np.uint32).astype(np.uint64)
+            t = (t[0::2] | (t[1::2] << np.uint64(32))).reshape(5, 16).astype(np.int64)
             if rep >= 10:
-                rows.append(t - t[:, 0].min())
-        r = np.median(np.stack(rows), axis=0) * 0.01   # 100 MHz ticks -> us
+                rows.append(t)
+        T = np.stack(rows)
+        nw = 5 if (T[:, 3:, 0] != 0).any() else 3
+        T = T[:, :nw]
+        T = T - T[:, :, 0].min(axis=1)[:, None, None]
+        r = np.median(T, axis=0) * 0.01   # 100 MHz ticks -> us
         res = {}
-        for w in range(3):
-            d = {"start": float(r[w, 0]), **{p: float(r[w, k + 1] - r[w, k]) for k, p in enumerate(PHASES)},
-                 "end": float(r[w, 7])}
-            # sub-phases: loads + einsum (start -> A formed), SVD + U Vt, quaternion; arm, Euler, gripper + rest
-            d["fit_loads_einsum"] = float(r[w, 8] - r[w, 0])
-            d["fit_svd"] = float(r[w, 9] - r[w, 8])
-            d["fit_quat_store"] = float(r[w, 1] - r[w, 9])
-            if w > 0:
-                d["side_arm"] = float(r[w, 10] - r[w, 2])
-                d["side_euler"] = float(r[w, 11] - r[w, 10])
-                d["side_gripper_rest"] = float(r[w, 3] - r[w, 11])
+        for w in range(nw):
+            if nw == 3:
+                d = {"start": float(r[w, 0]), **{p: float(r[w, k + 1] - r[w, k]) for k, p in enumerate(PHASES)},
+                     "end": float(r[w, 7])}
+                # sub-phases: loads + einsum (start -> A formed), SVD + U Vt, quaternion; arm, Euler, gripper + rest
+                d["fit_loads_einsum"] = float(r[w, 8] - r[w, 0])
+                d["fit_svd"] = float(r[w, 9] - r[w, 8])
+                d["fit_quat_store"] = float(r[w, 1] - r[w, 9])
+                if w > 0:
+                    d["side_arm"] = float(r[w, 10] - r[w, 2])
+                    d["side_euler"] = float(r[w, 11] - r[w, 10])
+                    d["side_gripper_rest"] = float(r[w, 3] - r[w, 11])
+            else:   # k_fbp_latency5: each stage's end time (us from the block's first timestamp)
+                d = {"start": float(r[w, 0])}
+                d.update({name: float(r[w, k]) for k, name in LAT5[w].items()})
+                if w < 3:
+                    d["svd_done"] = float(r[w, 9])
+                d["barrier_in"] = float(r[w, 5])
+                d["barrier_out"] = float(r[w, 6])
+                d["end"] = float(r[w, 7])
             res[f"wave{w}"] = d
-        out[str(B)] = res
+        out[str(B)] = {"kernel_waves": nw, **res}
     return out
 
 
