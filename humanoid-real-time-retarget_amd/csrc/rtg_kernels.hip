@@ -314,6 +314,9 @@ RTG_DEV void solve_body_rot(const SolverConsts &C, const float *__restrict__ g, 
 // solver kernel: per-frame body + coalesced DOF tile store
 // ----------------------------------------------------------------------------
 constexpr int kSolverBlock = 256;
+#ifndef RTG_SIDES_REBALANCE
+#define RTG_SIDES_REBALANCE 1   // FULL_BODY_POS side kernel: the right wave also runs the LEFT arm chain (it needs only
+#endif                          // R10) while the left wave runs the left wrist fit -- 1.5 SVD-equivalents per wave
 #ifndef RTG_SIDES_WAVES
 #define RTG_SIDES_WAVES 1   // min waves per SIMD for the side kernel (1: the compiler picks; measured best)
 #endif
@@ -444,14 +447,30 @@ RTG_DEV TipPts load_tips(const View &H)
 #define RTG_PRELOAD_TIPS 0   // 1: the gripper's hand points load with the wrist-fit points
 #endif
 
+// one arm's chain from its points and R10 (full_body_pos_retargeter.py:75-93)
+template <int SIDE>
+RTG_DEV Q fbp_arm(const SolverConsts &C, const ArmPts &ap, Q R10, const Emit &E)
+{
+    return solve_arm<SIDE ? 21 : 12>(E, vsub(ap.el, ap.sh), vsub(ap.wr, ap.el), SIDE ? C.rsh : C.lsh,
+                                     SIDE ? C.rel : C.lel, R10);
+}
+template <bool PRECISE, int SIDE, typename Hook = NoHook>
+RTG_DEV void fbp_side_after_arm(const SolverConsts &C, const TipPts &tp, Q R10, Q chain, Q W, const Emit &E,
+                                float *__restrict__ brow, const Hook &hook = Hook{});
 template <bool PRECISE, int SIDE, typename Hook = NoHook>
 RTG_DEV void solve_fbp_side(const SolverConsts &C, const ArmPts &ap, const TipPts &tp, Q R10, Q W, const Emit &E,
                             float *__restrict__ brow, const Hook &hook = Hook{})
 {
-    constexpr int L0 = SIDE ? 21 : 12, E0 = SIDE ? 25 : 16, D0 = SIDE ? 27 : 18, WROW = SIDE ? 39 : 14;
-    const Q chain = solve_arm<L0>(E, vsub(ap.el, ap.sh), vsub(ap.wr, ap.el), SIDE ? C.rsh : C.lsh,
-                                  SIDE ? C.rel : C.lel, R10);
+    const Q chain = fbp_arm<SIDE>(C, ap, R10, E);
     hook(2);
+    fbp_side_after_arm<PRECISE, SIDE>(C, tp, R10, chain, W, E, brow, hook);
+}
+// the Euler split of the wrist (:128-136), the gripper (:142-158 / :165-175) and the body_rot rows (:116, :172-173)
+template <bool PRECISE, int SIDE, typename Hook>
+RTG_DEV void fbp_side_after_arm(const SolverConsts &C, const TipPts &tp, Q R10, Q chain, Q W, const Emit &E,
+                                float *__restrict__ brow, const Hook &hook)
+{
+    constexpr int E0 = SIDE ? 25 : 16, D0 = SIDE ? 27 : 18, WROW = SIDE ? 39 : 14;
     emit_euler_xyz<E0>(E, qmul_norm(qconj(qmul_norm(R10, chain)), W));
     hook(3);
     const float a = hand_x_mean(qconj(W), tp.h0, tp.t);
@@ -560,7 +579,49 @@ __global__ __launch_bounds__(256, RTG_SIDES_WAVES) void k_solve_sides(SolverCons
         }
     }
 #endif
-    if (KIND == RTG_SOLVER_FULL_BODY_POS || KIND == RTG_SOLVER_UPPER_BODY) {
+    __shared__ float4 sarm[RTG_SIDES_REBALANCE ? kSideFrames : 1];   // the left arm chain, right wave -> left wave
+    if (KIND == RTG_SOLVER_FULL_BODY_POS && RTG_SIDES_REBALANCE) {
+        // Balanced FULL_BODY_POS: left wave = torso fit, then the left wrist fit, then the left Euler split /
+        // gripper; right wave = the right wrist fit, then BOTH arm chains (each needs only R10), then the right
+        // Euler split / gripper.  Two barriers hand R10 (left -> right) and the left chain (right -> left) over LDS.
+        const auto b = view(in0, 63);
+        Q R10 = qident(), W = qident();
+        ArmPts apL{}, apR{};
+        if (live) {
+            if (!side) {
+                R10 = fbp_torso(C, b);
+                storso[r] = make_float4(R10.x, R10.y, R10.z, R10.w);
+            } else {
+                apL = load_arm<0>(b);
+                apR = load_arm<1>(b);
+                W = fbp_wrist_fit<1>(C, view(in2, 60));
+            }
+        }
+        __syncthreads();
+        Q chain = qident();
+        if (live) {
+            if (side) {
+                const float4 t = storso[r];
+                R10 = Q{t.x, t.y, t.z, t.w};
+                const Q cl = fbp_arm<0>(C, apL, R10, E);
+                sarm[r] = make_float4(cl.x, cl.y, cl.z, cl.w);
+                chain = fbp_arm<1>(C, apR, R10, E);
+            } else {
+                emit_fixed_links(E);
+                W = fbp_wrist_fit<0>(C, view(in1, 60));
+            }
+        }
+        __syncthreads();
+        if (live) {
+            float *brow = body_rot ? body_rot + f * 236 : nullptr;
+            if (side) {
+                fbp_side_after_arm<PRECISE, 1>(C, load_tips(view(in2, 60)), R10, chain, W, E, brow);
+            } else {
+                const float4 c = sarm[r];
+                fbp_side_after_arm<PRECISE, 0>(C, load_tips(view(in1, 60)), R10, Q{c.x, c.y, c.z, c.w}, W, E, brow);
+            }
+        }
+    } else if (KIND == RTG_SOLVER_FULL_BODY_POS || KIND == RTG_SOLVER_UPPER_BODY) {
         // The torso fit is shared by both sides: the left wave fits it while the right wave fits its own hand
         // (FULL_BODY_POS; nothing to overlap for UPPER_BODY), then one block barrier hands R10 over LDS.
         const auto b = view(in0, 63);   // body (FULL_BODY_POS) / mocap points (UPPER_BODY), both (B, 21, 3)
