@@ -317,6 +317,9 @@ constexpr int kSolverBlock = 256;
 #ifndef RTG_SIDES_REBALANCE
 #define RTG_SIDES_REBALANCE 1   // FULL_BODY_POS side kernel: the right wave also runs the LEFT arm chain (it needs only
 #endif                          // R10) while the left wave runs the left wrist fit -- 1.5 SVD-equivalents per wave
+#ifndef RTG_SIDES_FIN_LEFT
+#define RTG_SIDES_FIN_LEFT 7    // exp-map slots (of 14) the left wave reads out in the balanced kernel (7, 8, 9: within noise)
+#endif
 #ifndef RTG_SIDES_WAVES
 #define RTG_SIDES_WAVES 1   // min waves per SIMD for the side kernel (1: the compiler picks; measured best)
 #endif
@@ -675,7 +678,13 @@ __global__ __launch_bounds__(256, RTG_SIDES_WAVES) void k_solve_sides(SolverCons
             else solve_body_rot_side<0>(C, view(in0, 84), E);
         }
     }
-    if (live) E.finalize(side * 7, 7);
+    if (live) {
+        // exp-map read-out split: slots [0, NL) on the left wave, [NL, 14) on the right.  Balanced FULL_BODY_POS
+        // leaves the right wave the heavier side program (two arm chains), so the left wave takes more slots; every
+        // slot was written before the last barrier, whichever wave wrote it.
+        constexpr int NL = (KIND == RTG_SOLVER_FULL_BODY_POS && RTG_SIDES_REBALANCE) ? RTG_SIDES_FIN_LEFT : 7;
+        E.finalize(side ? NL : 0, side ? 14 - NL : NL);
+    }
     __syncthreads();
     const int64_t nrows = (B - f0) < kSideFrames ? (B - f0) : kSideFrames;
     const int nvals = (int)nrows * 30;
