@@ -1120,8 +1120,11 @@ constexpr int kPosWin = RTG_FK_POS_REGS ? 0 : kFkTile * kPosPitch;   // floats o
 #else
 #define RTG_FK_WAVES
 #endif
+#ifndef RTG_FK_ALIGNED_STORE
+#define RTG_FK_ALIGNED_STORE 0   // 1: FK output rows leave as whole 64-byte sectors (chunk_store_aligned; measured 11-15 % slower); 0: per-window rows
+#endif
 #ifndef RTG_FK_REG_SLOTS
-#define RTG_FK_REG_SLOTS 0
+#define RTG_FK_REG_SLOTS (RTG_FK_ALIGNED_STORE ? 2 : 0)   // aligned stores need 8 KiB of carry LDS: slots move to VGPRs
 #endif
 #ifndef RTG_FK_NT_STORE
 #define RTG_FK_NT_STORE 0   // 1: FK output rows leave with non-temporal stores (written once, never re-read here)
@@ -1129,18 +1132,19 @@ constexpr int kPosWin = RTG_FK_POS_REGS ? 0 : kFkTile * kPosPitch;   // floats o
 #ifndef RTG_DOF_FK_POS_REGS
 #define RTG_DOF_FK_POS_REGS 1   // k_dof_fk positions staged through the rotation window (as RTG_FK_POS_REGS; measured +7-9 %)
 #endif
+constexpr int kCarryFloats = RTG_FK_ALIGNED_STORE ? 2 * kFkTile * 16 : 0;   // rotation + position carries
 static inline size_t lds_slot_floats(int nslots)
 {
     return nslots > RTG_FK_REG_SLOTS ? (size_t)(nslots - RTG_FK_REG_SLOTS) * 7 * kFkTile : 0;
 }
 static inline size_t fk_stream_lds_bytes(int nslots)
 {
-    return sizeof(float) * ((size_t)kFkTile * kRotPitch + (size_t)kPosWin + lds_slot_floats(nslots));
+    return sizeof(float) * ((size_t)kFkTile * kRotPitch + (size_t)kPosWin + kCarryFloats + lds_slot_floats(nslots));
 }
 constexpr int kDofPosWin = RTG_DOF_FK_POS_REGS ? 0 : kFkTile * kPosPitch;
 static inline size_t dof_fk_lds_bytes(int nslots)
 {
-    return sizeof(float) * ((size_t)kFkTile * kRotPitch + (size_t)kDofPosWin + lds_slot_floats(nslots));
+    return sizeof(float) * ((size_t)kFkTile * kRotPitch + (size_t)kDofPosWin + kCarryFloats + lds_slot_floats(nslots));
 }
 
 // A streaming tile is one wave, so ordering its LDS traffic needs no block
@@ -1225,6 +1229,57 @@ RTG_DEV void chunk_store(float *__restrict__ g, const float *lds, int pitch, int
     }
 }
 
+// Sector-aligned streaming store of one window (RTG_FK_ALIGNED_STORE).  A window's piece of a frame's output row is
+// 96 or 128 bytes at a 16-byte-aligned, not 64-byte-aligned, offset (the row stride is J x 12 / 16 bytes), so the
+// per-window store left two partly written 64-byte sectors per frame and window -- measured as 1.43x the
+// algorithmic WRITE_SIZE on Hu FK.  Here only whole sectors are written (4 lanes x float4); the floats of a
+// frame's last, incomplete sector wait in LDS (`carry`, 16 floats per frame) and go out with the next window.  Only
+// the frame's first and last sector (shared with the neighbouring frames' rows) are written per dword.
+// Tile-relative float x of frame fr lies in [fr S, fr S + S), S = W J; this window holds [a, b) = [fr S + W c0,
+// fr S + W (c0 + nC)) at win[fr * pitch + (x - a)]; the carry holds [a - 16, a) at carry[fr * 16 + (x - a + 16)].
+// Every store stays inside rows fr < nfr of this tile.
+RTG_DEV int floor16(int x) { return x & ~15; }
+RTG_DEV int ceil16(int x) { return (x + 15) & ~15; }
+template <int W>
+RTG_DEV void chunk_store_aligned(float *__restrict__ g, const float *win, int pitch, float *carry, int64_t f0, int nfr,
+                                 int J, int c0, int nC)
+{
+    const int S = W * J;
+    float *__restrict__ gt = g + f0 * S;   // 64 frames from a 64-frame boundary: 64-byte aligned
+    const bool first = c0 == 0, last = c0 + nC == J;
+    auto at = [&](int fr, int a, int x) { return x < a ? carry[fr * 16 + (x - a + 16)] : win[fr * pitch + (x - a)]; };
+    // whole sectors: at most two per frame and window (W nC <= 32 floats plus a carry of <= 15)
+#pragma unroll
+    for (int it = 0; it < 8; ++it) {
+        const int v = it * kFkTile + (int)threadIdx.x;
+        const int fr = v >> 3, q = (v >> 2) & 1, part = v & 3;
+        if (fr < nfr) {
+            const int A = fr * S, a = A + W * c0, b = a + W * nC;
+            const int s0 = first ? ceil16(A) : floor16(a), s1 = last ? floor16(A + S) : floor16(b);
+            const int x = s0 + 16 * q + 4 * part;
+            if (s0 + 16 * q + 16 <= s1)
+                *reinterpret_cast<float4 *>(gt + x) = make_float4(at(fr, a, x), at(fr, a, x + 1), at(fr, a, x + 2),
+                                                                  at(fr, a, x + 3));
+        }
+    }
+    const int fr = threadIdx.x;
+    const int A = fr * S, a = A + W * c0, b = a + W * nC, E = A + S;
+    if (fr < nfr && (first || last)) {   // the row's first and last sector, shared with the neighbouring rows
+        const int h1 = ceil16(A) < E ? ceil16(A) : E;
+        if (first)
+            for (int x = A; x < h1; ++x) gt[x] = at(fr, a, x);
+        if (last) {
+            int t0 = floor16(E);
+            const int lo = first ? h1 : floor16(a);
+            t0 = t0 > lo ? t0 : lo;
+            for (int x = t0; x < E; ++x) gt[x] = at(fr, a, x);
+        }
+    }
+    wave_sync();   // every lane has read the old carry
+    if (fr < nfr && !last)
+        for (int x = floor16(b); x < b; ++x) carry[fr * 16 + (x - b + 16)] = win[fr * pitch + (x - a)];
+}
+
 // slot s < RTG_FK_REG_SLOTS: registers (named members: an indexed array would be left in scratch); else LDS
 // [s - RTG_FK_REG_SLOTS][7][64].  s is launch-uniform (SGPR), so the selection is a scalar branch.
 struct Slots {
@@ -1258,7 +1313,8 @@ RTG_DEV void fk_stream_tile(const TopoView &T, const float *__restrict__ local_r
     const int nfr = (int)((B - f0) < kFkTile ? (B - f0) : kFkTile);
     float *rot = lds;                                   // [64][kRotPitch]
     float *pos = lds + kFkTile * kRotPitch;             // [64][kPosPitch] (RTG_FK_POS_REGS: none)
-    Slots slots{pos + kPosWin, qident(), qident(), V{0.0f, 0.0f, 0.0f}, V{0.0f, 0.0f, 0.0f}};
+    float *carry = pos + kPosWin;                       // [2][64][16] (RTG_FK_ALIGNED_STORE)
+    Slots slots{carry + kCarryFloats, qident(), qident(), V{0.0f, 0.0f, 0.0f}, V{0.0f, 0.0f, 0.0f}};
     const int lane = threadIdx.x;
     const bool active = lane < nfr;
     Q g = qident();
@@ -1306,7 +1362,8 @@ RTG_DEV void fk_stream_tile(const TopoView &T, const float *__restrict__ local_r
             }
         }
         wave_sync();
-        chunk_store<4>(g_rot, rot, kRotPitch, f0, nfr, J, c0, nC);
+        if (RTG_FK_ALIGNED_STORE) chunk_store_aligned<4>(g_rot, rot, kRotPitch, carry, f0, nfr, J, c0, nC);
+        else chunk_store<4>(g_rot, rot, kRotPitch, f0, nfr, J, c0, nC);
         if (RTG_FK_POS_REGS) {   // the rotation rows are out: reuse the window for the positions
             wave_sync();
             if (active) {
@@ -1316,7 +1373,9 @@ RTG_DEV void fk_stream_tile(const TopoView &T, const float *__restrict__ local_r
                     if (k < nC) { P[3 * k] = pk[k].x; P[3 * k + 1] = pk[k].y; P[3 * k + 2] = pk[k].z; }
             }
             wave_sync();
-            chunk_store<3>(g_pos, rot, kRotPitch, f0, nfr, J, c0, nC);
+            if (RTG_FK_ALIGNED_STORE)
+                chunk_store_aligned<3>(g_pos, rot, kRotPitch, carry + kFkTile * 16, f0, nfr, J, c0, nC);
+            else chunk_store<3>(g_pos, rot, kRotPitch, f0, nfr, J, c0, nC);
         } else {
             chunk_store<3>(g_pos, pos, kPosPitch, f0, nfr, J, c0, nC);
         }
@@ -1342,7 +1401,8 @@ RTG_DEV void local_rotation_tile(const TopoView &T, const float *__restrict__ g_
     const int J = T.J;
     const int nfr = (int)((B - f0) < kFkTile ? (B - f0) : kFkTile);
     float *win = fk_lds;                                 // [64][kRotPitch]
-    Slots slots{fk_lds + kFkTile * kRotPitch + kPosWin, qident(), qident(), V{0.0f, 0.0f, 0.0f},
+    float *carry = fk_lds + kFkTile * kRotPitch + kPosWin;
+    Slots slots{carry + kCarryFloats, qident(), qident(), V{0.0f, 0.0f, 0.0f},
                 V{0.0f, 0.0f, 0.0f}};   // the same LDS slot offset as fk_stream_tile
     const int lane = threadIdx.x;
     Q prev = qident();
@@ -1377,7 +1437,8 @@ RTG_DEV void local_rotation_tile(const TopoView &T, const float *__restrict__ g_
             }
         }
         wave_sync();
-        chunk_store<4>(local_rot, win, kRotPitch, f0, nfr, J, c0, nC);
+        if (RTG_FK_ALIGNED_STORE) chunk_store_aligned<4>(local_rot, win, kRotPitch, carry, f0, nfr, J, c0, nC);
+        else chunk_store<4>(local_rot, win, kRotPitch, f0, nfr, J, c0, nC);
         wave_sync();
     }
 }
@@ -1440,7 +1501,8 @@ __global__ __launch_bounds__(kFkTile) RTG_FK_WAVES void k_dof_fk(TopoView T, Dof
     const int nfr = (int)((B - f0) < kFkTile ? (B - f0) : kFkTile);
     float *rot = fk_lds;
     float *pos = fk_lds + kFkTile * kRotPitch;   // [64][kPosPitch] (RTG_DOF_FK_POS_REGS: none)
-    Slots slots{pos + kDofPosWin, qident(), qident(), V{0.0f, 0.0f, 0.0f}, V{0.0f, 0.0f, 0.0f}};
+    float *carry = pos + kDofPosWin;
+    Slots slots{carry + kCarryFloats, qident(), qident(), V{0.0f, 0.0f, 0.0f}, V{0.0f, 0.0f, 0.0f}};
     V pk[kFkChunk];   // RTG_DOF_FK_POS_REGS: the window's positions
     const int lane = threadIdx.x;
     const bool active = lane < nfr;
@@ -1494,7 +1556,8 @@ __global__ __launch_bounds__(kFkTile) RTG_FK_WAVES void k_dof_fk(TopoView T, Dof
             }
         }
         wave_sync();
-        chunk_store<4>(g_rot, rot, kRotPitch, f0, nfr, J, c0, nC);
+        if (RTG_FK_ALIGNED_STORE) chunk_store_aligned<4>(g_rot, rot, kRotPitch, carry, f0, nfr, J, c0, nC);
+        else chunk_store<4>(g_rot, rot, kRotPitch, f0, nfr, J, c0, nC);
         if (RTG_DOF_FK_POS_REGS) {   // the rotation rows are out: reuse the window for the positions
             wave_sync();
             if (active) {
@@ -1504,7 +1567,9 @@ __global__ __launch_bounds__(kFkTile) RTG_FK_WAVES void k_dof_fk(TopoView T, Dof
                     if (k < nC) { P[3 * k] = pk[k].x; P[3 * k + 1] = pk[k].y; P[3 * k + 2] = pk[k].z; }
             }
             wave_sync();
-            chunk_store<3>(g_pos, rot, kRotPitch, f0, nfr, J, c0, nC);
+            if (RTG_FK_ALIGNED_STORE)
+                chunk_store_aligned<3>(g_pos, rot, kRotPitch, carry + kFkTile * 16, f0, nfr, J, c0, nC);
+            else chunk_store<3>(g_pos, rot, kRotPitch, f0, nfr, J, c0, nC);
         } else {
             chunk_store<3>(g_pos, pos, kPosPitch, f0, nfr, J, c0, nC);
         }
