@@ -162,6 +162,22 @@ def solvers():
     return res
 
 
+def sweep():
+    """FULL_BODY_POS kernel time across batch sizes (RTG_LATENCY_MAX_B picks the latency kernel below it): run with
+    the default library and with an RTG_LATENCY_MAX_B=0 build (RTG_LIB=...) to find the crossover."""
+    zp = np.load(os.path.join(G, "zero_pose.npz"))
+    S = Solver(_lib.SOLVER_FULL_BODY_POS, zp["vtrdyn_full_local_t"], zp["vtrdyn_full_global_t"],
+               assets.parents("vtrdyn_full"), True)
+    Tf = topo("vtrdyn_full")
+    res = {}
+    for B in (4096, 8192, 16384, 24576, 32768, 49152, 65536, 98304, 131072):
+        body, lh, rh = ops.synth_full_body(Tf, B, seed=7)[:3]
+        dof = torch.empty((B, 30), device="cuda")
+        ms = time_events(lambda: S.retarget([body, lh, rh], out_dof=dof))
+        res[str(B)] = {"kernel_us": ms * 1e3, "frames_per_s": B / (ms * 1e-3)}
+    return res
+
+
 if __name__ == "__main__":
     modes = sys.argv[1:] or ["latency", "fk", "solvers"]
     out = {m: globals()[m]() for m in modes}
