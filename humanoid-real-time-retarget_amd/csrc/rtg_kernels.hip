@@ -711,7 +711,7 @@ __global__ __launch_bounds__(256, RTG_SIDES_WAVES) void k_solve_sides(SolverCons
 // Large batches keep k_solve_sides: there the third wave idles after its fit and costs throughput.
 // ----------------------------------------------------------------------------
 #ifndef RTG_LATENCY_MAX_B
-#define RTG_LATENCY_MAX_B 32768   // batches up to this size use k_fbp_latency (the GPU is not full anyway)
+#define RTG_LATENCY_MAX_B 49152   // batches up to this size use the latency kernel (swept: faster up to 49152, slower at 65536)
 #endif
 constexpr int kLatFrames = 64;
 #ifndef RTG_EXP_TIMESTAMPS
