@@ -13,6 +13,7 @@ constants happens at setup and the DOF gather after the timed region.
 from __future__ import annotations
 
 import argparse
+import hashlib
 import json
 import os
 import subprocess
@@ -47,17 +48,65 @@ def parse():
     return ap.parse_args()
 
 
-def dist_setup(args):
-    import torch
+def _free_port() -> int:
+    import socket
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launch_ranks(n: int) -> int:
+    """``--gpus N`` without a launcher: start N fresh rank processes of this script (one per GPU, RANK / LOCAL_RANK
+    / WORLD_SIZE / MASTER_* in their environment) and return the first non-zero exit code.  The parent never touches
+    the GPU, so each child initialises HIP itself; rank 0 prints the JSON line."""
+    port = _free_port()
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env))
+    rc = 0
+    try:
+        pending = list(procs)
+        while pending:
+            for p in list(pending):
+                code = p.poll()
+                if code is None:
+                    continue
+                pending.remove(p)
+                if code != 0 and rc == 0:
+                    rc = code
+                    for q in pending:      # one rank failed: the others would wait in a collective forever
+                        q.terminate()
+            time.sleep(0.05)
+    finally:
+        for p in procs:
+            if p.poll() is None:
+                p.kill()
+                p.wait()
+    return rc
+
+
+def load_backend():
+    """The rank backend: DeviceBackend (librtg_hip.so + RCCL) unless RTG_BENCH_BACKEND=module:Class names a stand-in
+    (the gloo tests drive this script's own launch path with a host backend)."""
+    spec = os.environ.get("RTG_BENCH_BACKEND")
+    if not spec:
+        return DeviceBackend
+    import importlib
+    mod, cls = spec.split(":")
+    return getattr(importlib.import_module(mod), cls)
+
+
+def dist_setup(backend_cls):
+    """Rank / world from the launcher's environment; the process group over RCCL ("nccl") for the device backend."""
     import torch.distributed as dist
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    backend_cls.bind_device(local)
     if world > 1:
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-    else:
-        torch.cuda.set_device(0)
+        dist.init_process_group(backend_cls.DIST_BACKEND, **backend_cls.pg_kwargs(local))
     return world, rank, local
 
 
@@ -129,7 +178,13 @@ def cpu_baseline(body, lh, rh, zl, zg, seconds):
     out = {"value": done / dt, "unit": "frames/s", "cores": threads, "kind": "port",
            "sample": f"{done} synthetic frames ({n}-frame slices of the bench workload), oracle/rtg_oracle.c "
                      f"OpenMP x{threads}, {dt:.1f} s", "cpu": model, "host_cpus": os.cpu_count(), "cpu_share": share,
-           "per_core_frames_per_s": done / dt / threads}
+           "per_core_frames_per_s": done / dt / threads,
+           "reference_python_cross_ref": {
+               "frames_per_s": 216.0, "ms_per_frame": 4.63, "cores": 1,
+               "cpu": "8-vCPU Intel Xeon (AVX-512) build container, torch 2.10.0 CPU, MKL 2024.2",
+               "code": "VtrdynFullBodyPosRetargeter.retarget (full_body_pos_retargeter.py:25-59), 1 process x 1 thread",
+               "source": "BASELINE.md:25 / SURVEY.md section 6 (measured there, not in this run: the reference's "
+                         "Python cannot travel to the GPU box)"}}
     # per-frame leg: `share` independent single-thread processes (children never touch the GPU)
     try:
         with tempfile.TemporaryDirectory() as td:
@@ -300,16 +355,43 @@ def source_setup():
     return (assets.parents("vtrdyn_full"), assets.local_translation("vtrdyn_full"), assets.tree_quat("vtrdyn_full"))
 
 
+GOLDEN = os.path.join(REPO, "tests", "golden", "full_body_pos_precise.npz")
+
+
+def golden_errors(dof, gold_dof):
+    """max |dof - golden| over the reference's 512 golden frames and the share of frames within 1e-5."""
+    e = np.abs(np.asarray(dof, np.float64) - gold_dof).max(1)
+    return {"frames": int(len(e)), "max_abs_err": float(e.max()), "frac_frames_le_1e-5": float(np.mean(e <= 1e-5))}
+
+
 class DeviceBackend:
     """The product path of one rank: librtg_hip.so on this rank's GPU (RCCL for the collectives)."""
+    DIST_BACKEND = "nccl"
 
-    def __init__(self, dev, layout="soa"):
+    @staticmethod
+    def bind_device(local):
+        import torch
+        torch.cuda.set_device(local)
+
+    @staticmethod
+    def pg_kwargs(local):
+        import torch
+        return {"device_id": torch.device("cuda", local)}
+
+    def __init__(self, local, layout="soa"):
         import torch
         self.torch = torch
-        self.dev = dev
+        self.dev = torch.device("cuda", local)
         self.layout = layout
-        self.comm_device = dev
+        self.comm_device = self.dev
         self.stream = torch.cuda.current_stream()
+
+    def golden_check(self, solver):
+        """This rank's own solver on the reference's golden frames (AoS rows, as the teleop callers hand them)."""
+        g = np.load(GOLDEN)
+        dof, _, _ = solver.retarget([self.torch.from_numpy(np.ascontiguousarray(g[k])).to(self.dev)
+                                     for k in ("body", "lh", "rh")])
+        return golden_errors(dof.cpu().numpy(), g["dof"])
 
     def zero_global(self, parents, lt, tq):
         """The source zero pose's global translations (SkeletonState FK of the identity pose, on the device)."""
@@ -384,10 +466,20 @@ def rank_flow(world, rank, backend, B, steps, warmup, ring):
     barrier(world, backend)
     wall = time.perf_counter() - t0
     kern_ms = backend.elapsed_ms() / max(1, steps)
-    if world > 1:
+    kern_ms_rank = kern_ms
+    if world > 1:   # the bench clock and the kernel clock are both the slowest rank's
         wall = shard.max_over_ranks(wall, backend.comm_device)
+        kern_ms = shard.max_over_ranks(kern_ms, backend.comm_device)
+    # every rank checks its own device solver against the reference goldens (after the timed region)
+    gold = backend.golden_check(solver)
+    per_rank = [gold]
+    if world > 1:
+        vals = shard.all_gather_floats([gold["max_abs_err"], gold["frac_frames_le_1e-5"], kern_ms_rank],
+                                       backend.comm_device)
+        per_rank = [{"rank": r, "frames": gold["frames"], "max_abs_err": v[0], "frac_frames_le_1e-5": v[1],
+                     "kern_ms": v[2]} for r, v in enumerate(vals)]
     out = {"wall": wall, "kern_ms": kern_ms, "frames": world * B * steps, "sets": sets, "topo": topo,
-           "solver": solver, "zl": lt, "zg": zg, "parents": parents}
+           "solver": solver, "zl": lt, "zg": zg, "parents": parents, "golden_per_rank": per_rank}
     if world > 1:   # final DOF gather to rank 0 (untimed region, reported separately)
         d = sets[(steps - 1) % ring][3]
         backend.sync()
@@ -400,11 +492,18 @@ def rank_flow(world, rank, backend, B, steps, warmup, ring):
 
 def main():
     args = parse()
-    import torch
-    world, rank, local = dist_setup(args)
+    world_env = os.environ.get("WORLD_SIZE")
+    if world_env is None and args.gpus > 1:
+        sys.exit(launch_ranks(args.gpus))
+    if world_env is not None and int(world_env) != args.gpus:
+        print(f"bench.py: --gpus {args.gpus} disagrees with WORLD_SIZE={world_env}", file=sys.stderr)
+        sys.exit(2)
+    backend_cls = load_backend()
+    world, rank, local = dist_setup(backend_cls)
+    if backend_cls is not DeviceBackend:
+        return host_main(args, backend_cls(local), world, rank)
     B = args.batch
-    dev = torch.device("cuda", local)
-    backend = DeviceBackend(dev, args.layout)
+    backend = DeviceBackend(local, args.layout)
     bytes_per_set = B * (63 + 60 + 60 + 30) * 4
     ring = args.ring or max(2, int(np.ceil(2 * 256 * 2**20 / bytes_per_set)))
     res = rank_flow(world, rank, backend, B, args.steps, args.warmup, ring)
@@ -432,6 +531,7 @@ def main():
                          if rec else None,
                          "compute": compute_roofline(rec, kern_ms)},
         }
+        line["golden_per_rank"] = res["golden_per_rank"]
         if "gather_ms" in res:
             line["gather_ms"] = res["gather_ms"]
         from rtg import ops
@@ -458,6 +558,21 @@ def main():
             line["cpu_baseline"] = cpu_baseline(b.cpu().numpy(), l.cpu().numpy(), r_.cpu().numpy(),
                                                 np.asarray(res["zl"], np.float32), np.asarray(res["zg"], np.float32),
                                                 args.cpu_seconds)
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        import torch.distributed as dist
+        dist.destroy_process_group()
+
+
+def host_main(args, backend, world, rank):
+    """The launch/collective flow with a stand-in backend (tests): same rank_flow, a reduced line."""
+    res = rank_flow(world, rank, backend, args.batch, args.steps, args.warmup, max(2, args.ring))
+    if rank == 0:
+        line = {"metric": METRIC, "value": res["frames"] / res["wall"], "unit": "frames/s", "n_gpus": world,
+                "steps": args.steps, "warmup": args.warmup, "backend": type(backend).__name__,
+                "kern_ms": res["kern_ms"], "golden_per_rank": res["golden_per_rank"]}
+        if "gathered" in res:
+            line["gathered_sha1"] = hashlib.sha1(res["gathered"].numpy().tobytes()).hexdigest()
         print(json.dumps(line), flush=True)
     if world > 1:
         import torch.distributed as dist

@@ -22,14 +22,30 @@ class BaseHumanoidRetargeter(ABC):
     #: rtg_solver_kind of the subclass
     SOLVER_KIND: Optional[int] = None
 
-    def __init__(self, source_zero_pose: RobotZeroPose, target_zero_pose: RobotZeroPose, precise_gripper=False):
+    def __init__(self, source_zero_pose: RobotZeroPose, target_zero_pose: RobotZeroPose, precise_gripper=False, *,
+                 frame_server: Optional[bool] = None, idle_ms: int = 200):
         self.source_zero_pose = source_zero_pose
         self.target_zero_pose = target_zero_pose
         self._motion_local_rotation = []
         self._motion_dof_pos = []
         self._solver = None
         self._precise = bool(precise_gripper)
-        self._frame_graphs = {}
+        self._frame_runner = None
+        self.configure_per_frame(frame_server, idle_ms)
+
+    def configure_per_frame(self, frame_server: Optional[bool] = None, idle_ms: int = 200):
+        """How single host frames are served (an addition to the reference API).
+
+        frame_server=False (the default; RTG_FRAME_SERVER=1 flips it): one launch per frame over pinned memory, on a
+        private stream -- nothing stays resident, so a caller's device-wide synchronize never waits on it.
+        frame_server=True (FULL_BODY_POS): a resident workgroup serves frames with no launch per frame; it occupies
+        its stream until ``idle_ms`` pass without a frame or :meth:`close` runs, and a device-wide synchronize in
+        between waits for it."""
+        if frame_server is None:
+            import os
+            frame_server = os.environ.get("RTG_FRAME_SERVER", "0") == "1"
+        self.close()
+        self.frame_server, self.idle_ms = bool(frame_server), int(idle_ms)
 
     # -- device solver (built lazily so construction works before a GPU is touched)
     @property
@@ -49,11 +65,12 @@ class BaseHumanoidRetargeter(ABC):
         one-launch frame call over pinned memory (rtg.realtime.per_frame_runner)."""
         dev = home_device(*inputs)
         if not batched and dev.type == "cpu":
-            g = self._frame_graphs.get(bool(want_body_rot))
-            if g is None:
+            if self._frame_runner is None:   # one runner per solver; FULL_BODY_POS always carries body_rot
                 from rtg.realtime import per_frame_runner
-                g = self._frame_graphs[bool(want_body_rot)] = per_frame_runner(self.solver, want_body_rot)
-            return g(*inputs)
+                self._frame_runner = per_frame_runner(self.solver, self.SOLVER_KIND == _lib.SOLVER_FULL_BODY_POS,
+                                                      server=self.frame_server, idle_ms=self.idle_ms)
+            lr, dof, br = self._frame_runner(*inputs)
+            return lr, dof, (br if want_body_rot else None)
         tails = [tuple(as_tensor(x).shape[-2:]) for x in inputs]
         xs = [dev_f32(as_tensor(x).reshape(-1, *t)) for x, t in zip(inputs, tails)]
         dof, lr, br = self.solver.retarget(xs, want_local_rot=True, want_body_rot=want_body_rot)
@@ -63,11 +80,10 @@ class BaseHumanoidRetargeter(ABC):
         return back(lr, dev), back(dof, dev), (back(br, dev) if br is not None else None)
 
     def close(self):
-        """End the per-frame runners (a resident frame server occupies its stream until it ends or idles out)."""
-        for g in self._frame_graphs.values():
-            if hasattr(g, "close"):
-                g.close()
-        self._frame_graphs = {}
+        """End the per-frame runner (a resident frame server occupies its stream until it ends or idles out)."""
+        g, self._frame_runner = getattr(self, "_frame_runner", None), None
+        if g is not None and hasattr(g, "close"):
+            g.close()
 
     def _record(self, local_rot, dof):
         self._motion_local_rotation.append(local_rot)

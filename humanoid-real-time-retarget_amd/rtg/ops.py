@@ -304,6 +304,14 @@ def forward_kinematics_multi(segments: Sequence[tuple]):
     require_gpu()
     if len(segments) > _lib.MAX_SEGMENTS:
         raise ValueError(f"at most {_lib.MAX_SEGMENTS} segments per launch")
+    segs, keep, outs = _fk_segments(segments)
+    check(lib().rtg_fk_multi_f32(segs, len(segments), stream_handle()))
+    return outs
+
+
+def _fk_segments(segments):
+    """ctypes FK segment table with per-segment shape checks: local_rot (B, J, 4) and a root translation that
+    broadcasts to (B, 3) -- a 2-D local_rot would otherwise make the kernel read B*J*4 floats of a J*4 buffer."""
     segs = (_lib.FkSegment * max(1, len(segments)))()
     keep, outs = [], []
     for i, (topo, lr, rt) in enumerate(segments):
@@ -321,8 +329,7 @@ def forward_kinematics_multi(segments: Sequence[tuple]):
         segs[i] = _lib.FkSegment(topo.handle.value, lr.data_ptr(), rt.data_ptr(), g_rot.data_ptr(), g_pos.data_ptr(), B)
         keep += [lr, rt]
         outs.append((g_rot, g_pos))
-    check(lib().rtg_fk_multi_f32(segs, len(segments), stream_handle()))
-    return outs
+    return segs, keep, outs
 
 
 def _inv_segments(segments):
@@ -356,18 +363,7 @@ def kinematics_multi(fk_segments: Sequence[tuple], inv_segments: Sequence[tuple]
     require_gpu()
     if len(fk_segments) + len(inv_segments) > _lib.MAX_SEGMENTS:
         raise ValueError(f"at most {_lib.MAX_SEGMENTS} segments per launch")
-    fsegs = (_lib.FkSegment * max(1, len(fk_segments)))()
-    keep, fouts = [], []
-    for i, (topo, lr, rt) in enumerate(fk_segments):
-        J = topo.num_joints
-        lr = dev_f32(lr, (J, 4), "local_rot")
-        B = int(lr.shape[0])
-        rt = dev_f32(rt, (3,), "root_t").expand(B, 3).contiguous()
-        g_rot = torch.empty((B, J, 4), device=lr.device, dtype=torch.float32)
-        g_pos = torch.empty((B, J, 3), device=lr.device, dtype=torch.float32)
-        fsegs[i] = _lib.FkSegment(topo.handle.value, lr.data_ptr(), rt.data_ptr(), g_rot.data_ptr(), g_pos.data_ptr(), B)
-        keep += [lr, rt]
-        fouts.append((g_rot, g_pos))
+    fsegs, keep, fouts = _fk_segments(fk_segments)
     isegs, ikeep, iouts = _inv_segments(inv_segments)
     check(lib().rtg_kinematics_multi_f32(fsegs, len(fk_segments), isegs, len(inv_segments), stream_handle()))
     return fouts, iouts

@@ -24,7 +24,6 @@ nodes, bit-identical outputs.
 """
 from __future__ import annotations
 
-import os
 import time
 from typing import Sequence
 
@@ -62,7 +61,9 @@ class FrameGraph:
         ins = [base + 4 * int(a) for a in self._in_offsets[:-1]] + [None] * (4 - len(sizes))
         out = self.h_out.data_ptr()
         self._args = [solver.handle] + ins + [1, 0, out + 4 * 124, out, out + 4 * 154 if want_body_rot else None]
-        self.stream = torch.cuda.current_stream(dev)
+        # a private stream: the frame never queues behind the caller's batched work, so the time limit measures
+        # this launch alone (inputs and outputs are host memory; the solver's constants were made synchronously)
+        self.stream = torch.cuda.Stream(dev)
         self.timeout_s = float(timeout_s)
 
     def _launch(self):
@@ -193,10 +194,10 @@ class FrameServer:
             pass
 
 
-def per_frame_runner(solver: Solver, want_body_rot: bool = False):
-    """The per-frame call the drop-in retargeters use for host inputs: the resident :class:`FrameServer` for
-    FULL_BODY_POS (the teleop solver; RTG_FRAME_SERVER=0 turns it off), :class:`FrameGraph` otherwise."""
+def per_frame_runner(solver: Solver, want_body_rot: bool = False, server: bool = False, idle_ms: int = 200):
+    """The per-frame call the drop-in retargeters use for host inputs: :class:`FrameGraph` (one launch per frame,
+    nothing resident), or with ``server`` the resident :class:`FrameServer` (FULL_BODY_POS only)."""
     from ._lib import SOLVER_FULL_BODY_POS
-    if solver.kind == SOLVER_FULL_BODY_POS and os.environ.get("RTG_FRAME_SERVER", "1") != "0":
-        return FrameServer(solver, want_body_rot)
+    if server and solver.kind == SOLVER_FULL_BODY_POS:
+        return FrameServer(solver, want_body_rot, idle_ms=idle_ms)
     return FrameGraph(solver, want_body_rot)

@@ -57,10 +57,13 @@ def broadcast_solver_consts(zero_local_t: Optional[torch.Tensor], zero_global_t:
     if dist.get_rank() == 0:
         blob = pack_solver_consts(zero_local_t.to(device), zero_global_t.to(device))
         if blob.numel() > cap:
-            raise ValueError(f"zero pose has more than {max_joints} joints")
-        buf[:blob.numel()] = blob
+            buf[0] = -1.0          # error marker: every rank raises after the broadcast instead of hanging in it
+        else:
+            buf[:blob.numel()] = blob
     dist.broadcast(buf, src=0)
     js = int(buf[0].item())
+    if js < 0:
+        raise ValueError(f"zero pose has more than {max_joints} joints")
     return unpack_solver_consts(buf[:1 + 6 * js])
 
 
@@ -98,13 +101,22 @@ def broadcast_setup(setup: Optional[tuple], max_joints: int, device: torch.devic
     import torch.distributed as dist
     cap = 1 + 11 * max_joints
     buf = torch.zeros(cap, dtype=torch.float32, device=device)
+    err = None
     if dist.get_rank() == 0:
-        blob = pack_setup(*setup).to(device)
-        if blob.numel() > cap:
-            raise ValueError(f"skeleton has more than {max_joints} joints")
-        buf[:blob.numel()] = blob
+        try:
+            blob = pack_setup(*setup).to(device)
+            if blob.numel() > cap:
+                raise ValueError(f"skeleton has more than {max_joints} joints")
+            buf[:blob.numel()] = blob
+        except ValueError as e:   # still broadcast: the other ranks are already waiting in it
+            err = e
+            buf[0] = -1.0
     dist.broadcast(buf, src=0)
     J = int(buf[0].item())
+    if err is not None:
+        raise err
+    if J < 0:
+        raise ValueError("rank 0 could not pack the setup blob")
     return unpack_setup(buf[:1 + 11 * J])
 
 
@@ -114,6 +126,15 @@ def max_over_ranks(x: float, device: torch.device) -> float:
     t = torch.tensor([x], dtype=torch.float64, device=device)
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
     return float(t.item())
+
+
+def all_gather_floats(values: Sequence[float], device: torch.device) -> List[List[float]]:
+    """Every rank's list of floats (same length on every rank), in rank order, on every rank."""
+    import torch.distributed as dist
+    t = torch.tensor(list(values), dtype=torch.float64, device=device)
+    outs = [torch.empty_like(t) for _ in range(dist.get_world_size())]
+    dist.all_gather(outs, t)
+    return [o.cpu().tolist() for o in outs]
 
 
 def gather_shards(shard: torch.Tensor, counts: Sequence[int], dst: int = 0) -> Optional[torch.Tensor]:

@@ -265,6 +265,33 @@ def test_frame_server_matches_batched(gpu):
         FrameServer(hu.solver, want_body_rot=True)(g["body"][0], g["lh"][0])
 
 
+def test_per_frame_calls_do_not_stall_device_synchronize(gpu):
+    """the drop-in's default per-frame path leaves nothing resident, so a torch.cuda.synchronize()
+    between teleop frames returns at once; the opt-in frame server honours the retargeter's idle_ms and close();
+    one runner serves both retarget() (body_rot) and a caller that drops it."""
+    import time
+
+    from retarget.retarget_solver import VtrdynFullBodyPosRetargeter
+    from robot_kinematics_model import RobotZeroPose
+    g = golden("full_body_pos_precise")
+    zf, zh = RobotZeroPose.from_asset("vtrdyn_full"), RobotZeroPose.from_asset("hu_v5")
+    for server, idle_ms, bound_s in ((False, 200, 0.05), (True, 10, 0.15)):
+        hu = VtrdynFullBodyPosRetargeter(zf, zh, precise_gripper=True, frame_server=server, idle_ms=idle_ms)
+        worst = 0.0
+        for i in range(6):
+            _, dof, br = hu.retarget(g["body"][i], g["lh"][i], g["rh"][i])
+            assert br.shape == (59, 4)
+            t0 = time.perf_counter()
+            torch.cuda.synchronize()
+            worst = max(worst, time.perf_counter() - t0)
+        assert worst < bound_s, (server, worst)
+        hu.close()
+        t0 = time.perf_counter()
+        torch.cuda.synchronize()
+        assert time.perf_counter() - t0 < 0.05
+        assert hu._frame_runner is None
+
+
 def test_main_retarget_from_global_translation(gpu):
     """retarget/main.py RetargetHuV5fromMocap.retarget_from_global_translation (:169-279), unchanged call, against
     the reference run end to end (tests/golden/main_retarget.npz, plot_skeleton_H captured) and against the oracle

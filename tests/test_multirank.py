@@ -131,45 +131,7 @@ def test_sharded_solve_matches_single_rank():
     np.testing.assert_array_equal(res[0], ref)
 
 
-class HostBackend:
-    """bench.DeviceBackend's interface with the oracle standing in for the device launch (gloo, CPU tensors):
-    exercises bench.rank_flow -- the bench's own N>1 flow -- without a GPU."""
-
-    def __init__(self):
-        self.comm_device = torch.device("cpu")
-
-    def zero_global(self, parents, lt, tq):
-        import oracle as orc
-        J = len(parents)
-        _, gp = orc.state_fk(parents, tq, lt, np.tile(np.float32([0, 0, 0, 1]), (1, J, 1)), np.zeros((1, 3), np.float32))
-        return gp[0]
-
-    def build(self, parents, lt, tq, zg):
-        return ("topo", np.asarray(parents)), ("solver", np.asarray(lt, np.float32), np.asarray(zg, np.float32))
-
-    def synth(self, topo, B, seed, offset):
-        from rtg import synth
-        return tuple(torch.from_numpy(a) for a in synth.synth_full_body_inputs(B, seed=seed * 1000 + offset))
-
-    def new_dof(self, B):
-        return torch.empty((B, 30), dtype=torch.float32)
-
-    def solve(self, solver, b, l, r, d):
-        import oracle as orc
-        dof, _, _ = orc.full_body_pos(solver[1], solver[2], b.numpy(), l.numpy(), r.numpy(), True, want_rot=False)
-        d.copy_(torch.from_numpy(dof))
-
-    def sync(self):
-        pass
-
-    def start(self):
-        self._t = 0.0
-
-    def stop(self):
-        pass
-
-    def elapsed_ms(self):
-        return 1.0
+from bench_host_backend import HostBackend  # noqa: E402  (bench.DeviceBackend's interface, oracle inside)
 
 
 def _bench_flow(rank, world):
@@ -219,3 +181,66 @@ def test_setup_blob_roundtrip():
     np.testing.assert_array_equal(d, zg)
     with pytest.raises(ValueError):
         shard.pack_setup(np.int32([-1, 0, 5]), lt[:3], tq[:3], zg[:3])
+
+
+def _bench_cmd(*extra, env_extra=None):
+    import subprocess
+    import sys
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_PORT")}
+    env.update(RTG_BENCH_BACKEND="bench_host_backend:HostBackend",
+               PYTHONPATH=os.pathsep.join([os.path.dirname(os.path.abspath(__file__)), repo, env.get("PYTHONPATH", "")]))
+    env.update(env_extra or {})
+    return subprocess.run([sys.executable, os.path.join(repo, "bench.py"), *extra], env=env, capture_output=True,
+                          text=True, timeout=300)
+
+
+def test_bench_gpus_flag_spawns_ranks_world2():
+    """`python bench.py --gpus 2` with no launcher environment starts two rank processes itself (the driver's
+    N-GPU invocation): rank 0 prints n_gpus 2, both ranks report their own golden check, the clock is the max over
+    ranks, and the gathered DOFs equal solving both seeded shards on one rank."""
+    import hashlib
+    import json
+    import oracle as orc
+    from rtg import assets, synth
+    r = _bench_cmd("--gpus", "2", "--steps", "3", "--warmup", "1", "--batch", "23", "--ring", "2")
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, r.stdout
+    line = json.loads(lines[0])
+    assert line["n_gpus"] == 2 and line["backend"] == "HostBackend"
+    ranks = line["golden_per_rank"]
+    assert [g["rank"] for g in ranks] == [0, 1]
+    for g in ranks:
+        assert g["frames"] == 512 and g["max_abs_err"] <= 2.2e-5
+    zp = np.load(os.path.join(os.path.dirname(__file__), "golden", "zero_pose.npz"))
+    want = []
+    for rank in (0, 1):   # the last timed step used ring set (3 - 1) % 2 = 0: frame offset 0
+        b, l, rr = synth.synth_full_body_inputs(23, seed=(1234 + rank) * 1000)
+        want.append(orc.full_body_pos(assets.local_translation("vtrdyn_full"), zp["vtrdyn_full_global_t"], b, l, rr,
+                                      True, want_rot=False)[0])
+    assert line["gathered_sha1"] == hashlib.sha1(np.ascontiguousarray(np.concatenate(want)).tobytes()).hexdigest()
+
+
+def test_bench_gpus_flag_must_match_launcher_world():
+    r = _bench_cmd("--gpus", "1", "--steps", "1", env_extra={"WORLD_SIZE": "2", "RANK": "0", "LOCAL_RANK": "0"})
+    assert r.returncode == 2 and "disagrees with WORLD_SIZE" in r.stderr
+
+
+def _bcast_too_big(rank, world):
+    J = 9
+    setup = (np.arange(-1, J - 1, dtype=np.int32), np.zeros((J, 3), np.float32), np.tile(np.float32([0, 0, 0, 1]), (J, 1)),
+             np.zeros((J, 3), np.float32)) if rank == 0 else None
+    try:
+        shard.broadcast_setup(setup, max_joints=4, device=torch.device("cpu"))
+    except ValueError as e:
+        return str(e)
+    return "no error"
+
+
+def test_broadcast_setup_error_reaches_every_rank():
+    """A skeleton larger than the broadcast buffer raises on EVERY rank (rank 0 still joins the broadcast with an
+    error marker) instead of leaving the other ranks blocked in it."""
+    res = _run(_bcast_too_big)
+    assert "more than 4 joints" in res[0]
+    assert "could not pack" in res[1]
