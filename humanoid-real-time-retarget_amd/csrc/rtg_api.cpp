@@ -506,14 +506,15 @@ int rtg_frame_server_launch(rtg_solver_t s, const float *in, float *dof, float *
 int rtg_quat_op_f32(int op, const float *a, const float *b, const float *c, int64_t n, float *out,
                     rtg_stream_t stream)
 {
-    if (op < RTG_OP_QUAT_MUL || op > RTG_OP_QUAT_ANGLE_AXIS) return fail(RTG_ERR_INVALID_ARGUMENT, "rtg_quat_op_f32: bad op %d", op);
+    if (op < RTG_OP_QUAT_MUL || op > RTG_OP_PROJECT_QUAT_XZ) return fail(RTG_ERR_INVALID_ARGUMENT, "rtg_quat_op_f32: bad op %d", op);
     if (n < 0) return fail(RTG_ERR_INVALID_ARGUMENT, "rtg_quat_op_f32: negative n");
     if (n == 0) return RTG_OK;
-    const bool needs_b = !(op == RTG_OP_QUAT_NORMALIZE || op == RTG_OP_QUAT_INVERSE || op == RTG_OP_QUAT_FROM_ROTMAT ||
-                           op == RTG_OP_QUAT_TO_EXP_MAP || op == RTG_OP_QUAT_TO_DOF_POS ||
-                           op == RTG_OP_QUAT_TO_ANGLE_AXIS || op == RTG_OP_NORMALIZE_ANGLE ||
-                           op == RTG_OP_QUAT_ABS || op == RTG_OP_QUAT_UNIT || op == RTG_OP_QUAT_ANGLE_AXIS);
-    const bool needs_c = op == RTG_OP_RADIANS_BETWEEN || op == RTG_OP_SHOULDER_PR || op == RTG_OP_ELBOW_PY;
+    const bool needs_b = op == RTG_OP_QUAT_MUL || op == RTG_OP_QUAT_MUL_NORM || op == RTG_OP_QUAT_ROTATE ||
+                         op == RTG_OP_QUAT_FROM_ANGLE_AXIS || op == RTG_OP_RADIANS_BETWEEN ||
+                         op == RTG_OP_PROJ_IN_PLANE || op == RTG_OP_SHOULDER_PR || op == RTG_OP_ELBOW_PY ||
+                         op == RTG_OP_QUAT_SLERP;
+    const bool needs_c = op == RTG_OP_RADIANS_BETWEEN || op == RTG_OP_SHOULDER_PR || op == RTG_OP_ELBOW_PY ||
+                         op == RTG_OP_QUAT_SLERP;
     if (!a || !out || (needs_b && !b) || (needs_c && !c))
         return fail(RTG_ERR_INVALID_ARGUMENT, "rtg_quat_op_f32: NULL operand for op %d", op);
     RTG_TRY(launch_quat_op(op, a, b, c, n, out, as_stream(stream)), "k_quat_op");
@@ -545,6 +546,25 @@ int rtg_quat_in_xyz_axis_f32(const float *q, const char *seq, int64_t n, float *
     if (n == 0) return RTG_OK;
     if (!q || !out) return fail(RTG_ERR_INVALID_ARGUMENT, "rtg_quat_in_xyz_axis_f32: NULL buffer");
     RTG_TRY(launch_quat_in_xyz_axis(q, ax[0], ax[1], ax[2], lower[0], n, out, as_stream(stream)), "k_quat_in_xyz_axis");
+    return RTG_OK;
+}
+
+int rtg_quat_as_euler_f64(const float *q, const char *seq, int degrees, int64_t n, double *out, rtg_stream_t stream)
+{
+    if (!seq || std::strlen(seq) != 3) return fail(RTG_ERR_INVALID_ARGUMENT, "rtg_quat_as_euler_f64: seq must have 3 axes");
+    int ax[3], lower[3];
+    for (int i = 0; i < 3; ++i)
+        if (!axis_of(seq[i], &ax[i], &lower[i]))
+            return fail(RTG_ERR_INVALID_ARGUMENT, "rtg_quat_as_euler_f64: bad axis '%c'", seq[i]);
+    if (lower[0] != lower[1] || lower[1] != lower[2])
+        return fail(RTG_ERR_INVALID_ARGUMENT, "rtg_quat_as_euler_f64: mixed intrinsic/extrinsic seq '%s'", seq);
+    if (ax[0] == ax[1] || ax[1] == ax[2])
+        return fail(RTG_ERR_INVALID_ARGUMENT, "rtg_quat_as_euler_f64: consecutive axes must differ ('%s')", seq);
+    if (n < 0) return fail(RTG_ERR_INVALID_ARGUMENT, "rtg_quat_as_euler_f64: negative n");
+    if (n == 0) return RTG_OK;
+    if (!q || !out) return fail(RTG_ERR_INVALID_ARGUMENT, "rtg_quat_as_euler_f64: NULL buffer");
+    RTG_TRY(launch_quat_as_euler(q, ax[0], ax[1], ax[2], lower[0], degrees != 0, n, out, as_stream(stream)),
+            "k_quat_as_euler");
     return RTG_OK;
 }
 

@@ -84,6 +84,8 @@ hipError_t launch_ingest_vtrdyn(const float *bp, const float *lhp, const float *
 hipError_t launch_quat_op(int op, const float *a, const float *b, const float *c, int64_t n, float *out,
                           hipStream_t s);
 hipError_t launch_cal_joint_quat(const float *Z, const float *M, int npts, int64_t n, float *out, hipStream_t s);
+hipError_t launch_quat_as_euler(const float *q, int s0, int s1, int s2, int extrinsic, int degrees, int64_t n,
+                               double *out, hipStream_t s);
 hipError_t launch_quat_in_xyz_axis(const float *q, int s0, int s1, int s2, int extrinsic, int64_t n, float *out,
                                    hipStream_t s);
 struct GaussTaps {

@@ -1,0 +1,81 @@
+// rtg_knobs.h -- every compile-time knob of librtg_hip.so with its product default, in one place: each kernel
+// TU sees the same values, and rtg_build_info() (rtg_ops.hip) reports them.  RTG_EXP_* are measurement-only;
+// STUB_SVD / NO_TABLE / HOT_INPUTS change results and the Python binding refuses a library built with them.
+#pragma once
+
+// ---- used by rtg_solver.cuh
+#ifndef RTG_SIDES_REBALANCE
+#define RTG_SIDES_REBALANCE 1   // FULL_BODY_POS side kernel: the right wave also runs the LEFT arm chain (it needs only
+#endif                          // R10) while the left wave runs the left wrist fit -- 1.5 SVD-equivalents per wave
+#ifndef RTG_SIDES_FIN_LEFT
+#define RTG_SIDES_FIN_LEFT 7    // exp-map slots (of 14) the left wave reads out in the balanced kernel (7, 8, 9: within noise)
+#endif
+#ifndef RTG_SIDES_WAVES
+#define RTG_SIDES_WAVES 1   // min waves per SIMD for the side kernel (1: the compiler picks; measured best)
+#endif
+#ifndef RTG_EXP_HOT_INPUTS
+#define RTG_EXP_HOT_INPUTS 0
+#endif
+#ifndef RTG_SOLVER_SIDES
+#define RTG_SOLVER_SIDES 1   // 0: always the fused one-lane-per-frame kernels (k_retarget), for comparison
+#endif
+#ifndef RTG_L2_PREFETCH
+#define RTG_L2_PREFETCH 0    // 1: each side wave pulls the input rows it reads late into L2 at kernel start
+#endif
+#ifndef RTG_PRELOAD_ARM
+#define RTG_PRELOAD_ARM 1    // (measured -4 %) 1: a side's arm points load at kernel start, with the torso / wrist-fit loads
+#endif
+#ifndef RTG_PRELOAD_TIPS
+#define RTG_PRELOAD_TIPS 0   // 1: the gripper's hand points load with the wrist-fit points
+#endif
+#ifndef RTG_LATENCY_MAX_B
+#define RTG_LATENCY_MAX_B 49152   // batches up to this size use the latency kernel (swept: faster up to 49152, slower at 65536)
+#endif
+#ifndef RTG_EXP_TIMESTAMPS
+#define RTG_EXP_TIMESTAMPS 0   // measurement knob: block 0's lane 0 of each wave records the 100 MHz wall clock at
+#endif                         // each phase into body_rot (as u32 pairs) -- wrong body_rot, tools/latency_phases.py
+#ifndef RTG_LATENCY_WAVES
+#define RTG_LATENCY_WAVES 5   // 5: k_fbp_latency5 (arm chain concurrent with the wrist fits); 3: k_fbp_latency
+#endif
+// ---- used by rtg_fk.hip
+#ifndef RTG_FK_CHUNK
+#define RTG_FK_CHUNK 8
+#endif
+#ifndef RTG_FK_POS_REGS
+#define RTG_FK_POS_REGS 1   // 1 (measured +3-4 %, bit-exact): positions held in registers and staged through the rotation window after it is
+                            //    stored (no separate position window: 12.8 instead of 19.2 KiB per wave)
+#endif
+#ifndef RTG_FK_MIN_WAVES
+#define RTG_FK_MIN_WAVES 0   // >0: min waves per SIMD asked of the streaming FK kernels (4: <= 128 VGPRs, 16 waves/CU)
+#endif
+#ifndef RTG_FK_ALIGNED_STORE
+#define RTG_FK_ALIGNED_STORE 0   // 1: FK output rows leave as whole 64-byte sectors (chunk_store_aligned; measured 11-15 % slower); 0: per-window rows
+#endif
+#ifndef RTG_FK_REG_SLOTS
+#define RTG_FK_REG_SLOTS (RTG_FK_ALIGNED_STORE ? 2 : 0)   // aligned stores need 8 KiB of carry LDS: slots move to VGPRs
+#endif
+#ifndef RTG_FK_NT_STORE
+#define RTG_FK_NT_STORE 0   // 1: FK output rows leave with non-temporal stores (written once, never re-read here)
+#endif
+#ifndef RTG_DOF_FK_POS_REGS
+#define RTG_DOF_FK_POS_REGS 1   // k_dof_fk positions staged through the rotation window (as RTG_FK_POS_REGS; measured +7-9 %)
+#endif
+// ---- used by rtg_math.cuh
+#ifndef RTG_FAST_EXACT
+#define RTG_FAST_EXACT 1
+#endif
+#ifndef RTG_EXP_NO_TABLE
+#define RTG_EXP_NO_TABLE 0
+#endif
+#ifndef RTG_ANG_TAB_BITS
+#define RTG_ANG_TAB_BITS 3
+#endif
+#ifndef RTG_SVD_DIV
+#define RTG_SVD_DIV 1   // 1: the compiler's IEEE f32 division sequence (measured +6 %); 0: rcp64 + mulr
+#endif
+#ifndef RTG_SVD_SQRT
+#define RTG_SVD_SQRT 0  // 0: cr_sqrt (v_sqrt_f64 + Newton); 1: the compiler's IEEE f32 sqrt sequence
+#endif
+#ifndef RTG_EXP_STUB_SVD
+#define RTG_EXP_STUB_SVD 0   // measurement knob (tools/build_variants.sh): R = identity-ish, wrong answers
+#endif

@@ -17,6 +17,7 @@
 #include <stdint.h>
 
 #include "rtg_crmath.h"
+#include "rtg_knobs.h"
 
 #pragma clang fp contract(off)
 
@@ -29,9 +30,6 @@ struct V { float x, y, z; };
 
 // ---------------------------------------------------------------- helpers
 RTG_DEV float ieee_sqrtf(float x) { return __builtin_sqrtf(x); }   // IEEE sqrt (correctly rounded build)
-#ifndef RTG_FAST_EXACT
-#define RTG_FAST_EXACT 1
-#endif
 // Correctly rounded f32 sqrt in 6 instructions: v_sqrt_f64 (not accurate enough alone: it misses on 4 % of
 // inputs) plus one Newton correction gives ~2^-100, and sqrt of an f32 is never within 2^-51 of an f32
 // midpoint, so the single rounding is exact.  0 / inf / NaN / negative: the residual is 0 or NaN and the raw
@@ -238,7 +236,8 @@ RTG_DEV V qrotate(Q q, V v)  // :205-211, two Hamilton products
 RTG_DEV Q qfrom_angle_axis(float angle, V axis)  // :122-143
 {
     const float theta = angle / 2.0f;
-    float n = cr_sqrt((axis.x * axis.x + axis.y * axis.y) + axis.z * axis.z);
+    // axis.norm(p=2, dim=-1) of a 3-vector: torch's fma chain (measured: 100 % vs 90 % for the plain left fold)
+    float n = cr_sqrt(__builtin_fmaf(axis.z, axis.z, __builtin_fmaf(axis.y, axis.y, axis.x * axis.x)));
     n = clamp_lo(n, 1e-9f);
     const Rcp r = rcp64(n);
     const float ax = mulr(axis.x, r), ay = mulr(axis.y, r), az = mulr(axis.z, r);
@@ -325,14 +324,8 @@ RTG_DEV float qexp_component(Q q, int k)
 // itself (ang_tab_code, k_build_ang_tab) with the same P.  qexp_component_tab thus skips acos, sincos and
 // atan2f (290 of the 330 instructions of an exp-map); w outside the table or a code-0 entry takes the exact
 // path.  tools/check_fastmath.hip checks qexp_component_tab == qexp_component for every f32 w.
-#ifndef RTG_EXP_NO_TABLE
-#define RTG_EXP_NO_TABLE 0
-#endif
 constexpr uint32_t kAngTabLo = 0x3e800000u;                     // bits of 0.25f
 constexpr uint32_t kAngTabEntries = 0x3f800000u - kAngTabLo;    // up to 1.0f (exclusive): 2^24
-#ifndef RTG_ANG_TAB_BITS
-#define RTG_ANG_TAB_BITS 3
-#endif
 constexpr uint32_t kAngTabBits = RTG_ANG_TAB_BITS;              // 3: moves -3..3, 10 codes per word; 4: -7..7, 8
 constexpr uint32_t kAngTabPer = kAngTabBits == 3 ? 10u : 8u;
 constexpr uint32_t kAngTabWords = (kAngTabEntries + kAngTabPer - 1) / kAngTabPer;
@@ -437,6 +430,72 @@ RTG_DEV float radians_between_axes(V v1, V v2, V n)
     return cr_acos(c) * tsign(dot3(n, cross3(v1, v2)));
 }
 
+// ------------------------------------------------ the rest of the rotation3d / transform3d surface
+// (not on the solver path; the elementwise ops 18-31 of rtg_quat_op_f32).  torch's norm(dim=-1) of a 3-vector is
+// the fma chain of lnorm3, torch.sum over 4 a left fold, x**2 = x*x, atan2 on small tensors glibc's atan2f.
+
+// exp_map_to_angle_axis (rotation3d.py:629-646) as [angle, axis]
+RTG_DEV Q exp_map_angle_axis(V e)
+{
+    const float n = lnorm3(e);
+    const Rcp r = rcp64(n);
+    const float a = normalize_angle(n);
+    const bool mask = fabsf(a) > 1e-5f;
+    return Q{mask ? a : 0.0f, mask ? mulr(e.x, r) : 0.0f, mask ? mulr(e.y, r) : 0.0f, mask ? mulr(e.z, r) : 1.0f};
+}
+// quat_slerp (transform3d.py:152-174), t per row
+RTG_DEV Q qslerp(Q q0, Q q1, float t)
+{
+    float ch = ((q0.x * q1.x + q0.y * q1.y) + q0.z * q1.z) + q0.w * q1.w;
+    if (ch < 0.0f) q1 = Q{-q1.x, -q1.y, -q1.z, -q1.w};
+    ch = fabsf(ch);
+    const float half = cr_acos(ch);
+    const float sh = cr_sqrt(1.0f - ch * ch);
+    const float ra = cr_sin((1.0f - t) * half) / sh;
+    const float rb = cr_sin(t * half) / sh;
+    if (fabsf(ch) >= 1.0f) return q0;
+    if (fabsf(sh) < 0.001f)
+        return Q{0.5f * q0.x + 0.5f * q1.x, 0.5f * q0.y + 0.5f * q1.y, 0.5f * q0.z + 0.5f * q1.z, 0.5f * q0.w + 0.5f * q1.w};
+    return Q{ra * q0.x + rb * q1.x, ra * q0.y + rb * q1.y, ra * q0.z + rb * q1.z, ra * q0.w + rb * q1.w};
+}
+// rot_matrix_det (rotation3d.py:338-350), m row-major
+RTG_DEV float rotmat_det(const float m[9])
+{
+    const float t1 = m[0] * (m[4] * m[8] - m[5] * m[7]);
+    const float t2 = m[1] * (m[3] * m[8] - m[5] * m[6]);
+    const float t3 = m[2] * (m[3] * m[7] - m[4] * m[6]);
+    return (t1 - t2) + t3;
+}
+// rot_matrix_from_quaternion (rotation3d.py:398-427): [i, j, k, r] = [x, y, z, w], row-major out
+RTG_DEV void rotmat_from_quat(Q q, float o[9])
+{
+    const float i = q.x, j = q.y, k = q.z, r = q.w;
+    const float two_s = 2.0f / (((i * i + j * j) + k * k) + r * r);
+    o[0] = 1.0f - two_s * (j * j + k * k);
+    o[1] = two_s * (i * j - k * r);
+    o[2] = two_s * (i * k + j * r);
+    o[3] = two_s * (i * j + k * r);
+    o[4] = 1.0f - two_s * (i * i + k * k);
+    o[5] = two_s * (j * k - i * r);
+    o[6] = two_s * (i * k - j * r);
+    o[7] = two_s * (j * k + i * r);
+    o[8] = 1.0f - two_s * (i * i + j * j);
+}
+// extract_rotation_along_axis (rotation3d.py:534-556) / the angles of project_quat_to_axis_* (:479-530)
+RTG_DEV float axis_angle_of(Q q, int axis)
+{
+    if (axis == 0) return g_atan2f(2.0f * (q.w * q.x + q.y * q.z), 1.0f - 2.0f * (q.x * q.x + q.z * q.z));
+    if (axis == 1) return g_atan2f(2.0f * (q.w * q.y + q.x * q.z), 1.0f - 2.0f * (q.y * q.y + q.z * q.z));
+    return g_atan2f(2.0f * (q.w * q.z + q.x * q.y), 1.0f - 2.0f * (q.z * q.z + q.y * q.y));
+}
+// [sin(a/2) e_axis, cos(a/2)], unnormalised (the new_q of project_quat_to_axis_*)
+RTG_DEV Q axis_half_quat(int axis, float a)
+{
+    const float h = a / 2.0f;
+    const float s = cr_sin(h), c = cr_cos(h);
+    return Q{axis == 0 ? s : 0.0f, axis == 1 ? s : 0.0f, axis == 2 ? s : 0.0f, c};
+}
+
 // ------------------------------------------------ Kabsch: torch.linalg.svd as MKL sgesdd computes it
 // transform3d.py:40-45 runs torch.linalg.svd on one (1,3,3) float32 matrix, i.e. oneMKL 2024.2 SGESDD(JOBZ='A').
 // For 3x3 that is SGEBD2 -> SBDSDC('U','I') -> SLASDQ -> SBDSQR -> SORMBR('Q') on U / SORMBR('P') on VT.  Each
@@ -444,12 +503,6 @@ RTG_DEV float radians_between_axes(V v1, V v2, V n)
 // by stage against MKL's own entry points (tools/mkl_sgesdd_probe.py) and matches bit for bit.  The
 // oracle (oracle/rtg_oracle.c, la_gesdd3) restates the same routines independently.  All divisions / square
 // roots are IEEE-exact (fdiv = one rcp64 + mulr, cr_sqrt).  Matrices are column-major: a[r + 3 c].
-#ifndef RTG_SVD_DIV
-#define RTG_SVD_DIV 1   // 1: the compiler's IEEE f32 division sequence (measured +6 %); 0: rcp64 + mulr
-#endif
-#ifndef RTG_SVD_SQRT
-#define RTG_SVD_SQRT 0  // 0: cr_sqrt (v_sqrt_f64 + Newton); 1: the compiler's IEEE f32 sqrt sequence
-#endif
 RTG_DEV float fdiv(float a, float b)
 {
 #if RTG_SVD_DIV
@@ -878,9 +931,6 @@ RTG_DEV void la_gesdd3(float a[9], Svd3 &z)
 }
 // transform3d.py:40-45: R = U Vt ((p0 + p1) + p2, torch's bmm order); det(R) < 0 -> Vt[-1,:] *= -1; R = U Vt.
 // A and R row-major.  det only decides a sign (|det| = 1 up to rounding), taken in float64.
-#ifndef RTG_EXP_STUB_SVD
-#define RTG_EXP_STUB_SVD 0   // measurement knob (tools/build_variants.sh): R = identity-ish, wrong answers
-#endif
 RTG_DEV void kabsch_rot(const float A[9], float R[9])
 {
 #if RTG_EXP_STUB_SVD

@@ -1,0 +1,649 @@
+// rtg_ops.hip -- motion prep, ingest, elementwise primitives, Kabsch / Euler ops, velocities, synthetic
+// frames, and the build-configuration record.
+#include "rtg_device.cuh"
+
+namespace rtg {
+
+// ----------------------------------------------------------------------------
+// retarget/main.py motion-level prep, one frame per lane.
+// ----------------------------------------------------------------------------
+struct Dir3 {
+    float x, y, z;
+    int32_t on;
+};
+
+// Retarget.rescale_motion_to_standard_size (main.py:37-47) after coord_transform(dir) (:170).  A bone's parent
+// end is the parent's RESCALED position: re-read from this lane's own output row (program order).
+__global__ __launch_bounds__(256) void k_rescale_motion(TopoView T, const float *__restrict__ motion, int64_t B,
+                                                        Dir3 dir, float *__restrict__ out)
+{
+    const int64_t f = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (f >= B) return;
+    const int J = T.J;
+    const float *m = motion + f * J * 3;
+    float *o = out + f * J * 3;
+    auto mp = [&](int j) {
+        const V v = ld3(m + 3 * j);
+        return dir.on ? V{v.x * dir.x, v.y * dir.y, v.z * dir.z} : v;
+    };
+    for (int j = 0; j < J; ++j) {
+        const int p = ld_const(T.parents + j);
+        const V mj = mp(j);
+        if (p < 0) {
+            st3(o + 3 * j, mj);
+            continue;
+        }
+        const V d = vsub(mj, mp(p));
+        const float scale = lnorm3(d) / lnorm3(ld_const(T.local_t + j));
+        const V q = vdiv(d, scale);
+        const V op = ld3(o + 3 * p);
+        st3(o + 3 * j, V{op.x + q.x, op.y + q.y, op.z + q.z});
+    }
+}
+
+// torch.max over a batch of norms: every norm is >= 0 or NaN, so the float bits order as ints once NaN is
+// pinned to the largest pattern.  Wave-reduced, then one atomic per wave.
+RTG_DEV int32_t max_key(float v) { return v != v ? 0x7fffffff : __float_as_int(v); }
+RTG_DEV int32_t wave_max(int32_t v)
+{
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+        const int32_t w = __shfl_xor(v, o, 64);
+        v = w > v ? w : v;
+    }
+    return v;
+}
+RTG_DEV bool batch_small(const float *ws, int i)   // (max norm) <= 1e-6, false for NaN
+{
+    const int32_t k = reinterpret_cast<const int32_t *>(ws)[i];
+    return k != 0x7fffffff && __int_as_float(k) <= 1e-6f;
+}
+
+// quat_between_two_vecs (transform3d.py:8-21) for one pair; `ident`: the batch-level branch of :11-12
+RTG_DEV Q quat_between(V v1, V v2, bool ident)
+{
+    if (ident) return qident();
+    v1 = vdiv(v1, lnorm3(v1));
+    v2 = vdiv(v2, lnorm3(v2));
+    const V c = cross3(v1, v2);
+    return qnormalize(Q{c.x, c.y, c.z, 1.0f + dot3(v1, v2)});   // torch.sum(v1*v2): left fold (measured)
+}
+
+__global__ __launch_bounds__(256) void k_qbtv_norm_max(const float *__restrict__ v1, const float *__restrict__ v2,
+                                                       int64_t n, float *ws)
+{
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    int32_t a = 0, b = 0;
+    if (i < n) {
+        a = max_key(lnorm3(ld3(v1 + 3 * i)));   // torch.norm(dim=-1): the fma form (measured)
+        b = max_key(lnorm3(ld3(v2 + 3 * i)));
+    }
+    a = wave_max(a);
+    b = wave_max(b);
+    if ((threadIdx.x & 63) == 0) {
+        atomicMax(reinterpret_cast<int32_t *>(ws), a);
+        atomicMax(reinterpret_cast<int32_t *>(ws) + 1, b);
+    }
+}
+
+__global__ __launch_bounds__(256) void k_quat_between(const float *__restrict__ v1, const float *__restrict__ v2,
+                                                      int64_t n, const float *ws, float *__restrict__ out)
+{
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const bool ident = batch_small(ws, 0) || batch_small(ws, 1);
+    st4(out + 4 * i, quat_between(ld3(v1 + 3 * i), ld3(v2 + 3 * i), ident));
+}
+
+// _rebuild_with_vtrdyn_zero_pose (main.py:116-165): pass 1, per child joint j the batch max of |m_j - m_p|
+__global__ __launch_bounds__(256) void k_rebuild_norm_max(TopoView T, const float *__restrict__ motion, int64_t B,
+                                                          float *ws)
+{
+    const int64_t f = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const int J = T.J;
+    const float *m = motion + (f < B ? f : 0) * J * 3;
+    for (int j = 1; j < J; ++j) {
+        const int p = ld_const(T.parents + j);
+        if (p == 0 || p == 10) continue;
+        int32_t k = f < B ? max_key(lnorm3(vsub(ld3(m + 3 * j), ld3(m + 3 * p)))) : 0;
+        k = wave_max(k);
+        if ((threadIdx.x & 63) == 0) atomicMax(reinterpret_cast<int32_t *>(ws) + j, k);
+    }
+}
+
+// pass 2: rows 0 and 10 from the Kabsch fits (:126-136); every other row r takes quat_between_two_vecs of its
+// LAST child c (the loop :144-152 overwrites row r once per child, in index order), or stays identity; then
+// SkeletonState.from_rotation_and_root_translation normalises every row (skeleton3d.py:610).
+__global__ __launch_bounds__(256) void k_rebuild_vtrdyn(TopoView T, const float *__restrict__ motion, int64_t B,
+                                                        const float *ws, float *__restrict__ g_rot,
+                                                        float *__restrict__ root_t)
+{
+    const int64_t f = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (f >= B) return;
+    const int J = T.J;
+    const float *m = motion + f * J * 3;
+    float *gr = g_rot + f * J * 4;
+    auto zl = [&](int j) { return ld_const(T.local_t + j); };
+    const V m0 = ld3(m), m10 = ld3(m + 30);
+    {
+        const V Z[3] = {zl(4), zl(1), zl(7)};
+        const V M[3] = {vsub(ld3(m + 12), m0), vsub(ld3(m + 3), m0), vsub(ld3(m + 21), m0)};
+        st4(gr, qnormalize(cal_joint_quat<3>(Z, M)));
+    }
+    {
+        const V Z[3] = {zl(17), zl(13), zl(11)};
+        const V M[3] = {vsub(ld3(m + 51), m10), vsub(ld3(m + 39), m10), vsub(ld3(m + 33), m10)};
+        st4(gr + 40, qnormalize(cal_joint_quat<3>(Z, M)));
+    }
+    for (int r = 1; r < J; ++r) {
+        if (r == 10) continue;
+        int c = -1;   // uniform scalar search: last child of r
+        for (int k = r + 1; k < J; ++k)
+            if (ld_const(T.parents + k) == r) c = k;
+        Q q = qident();
+        if (c > 0)   // batch condition: max |vec1| = |zl_c| (one vector repeated), max |vec2| from pass 1
+            q = quat_between(zl(c), vsub(ld3(m + 3 * c), ld3(m + 3 * r)), lnorm3(zl(c)) <= 1e-6f || batch_small(ws, c));
+        st4(gr + 4 * r, qnormalize(q));
+    }
+    st3(root_t + f * 3, m0);
+}
+
+// ----------------------------------------------------------------------------
+// VTRDyn ingest: sim_full_body_teleop.py:109 (body 23 -> 21), :111-112 (hand order), :92 (skip all-zero frames)
+// ----------------------------------------------------------------------------
+__constant__ int8_t c_body23_to_21[21] = {0, 1, 2, 3, 5, 6, 7, 9, 10, 11, 12, 13, 14, 15, 16, 17, 18, 19, 20, 21, 22};
+__constant__ int8_t c_hand_order[20] = {0, 4, 5, 6, 7, 8, 9, 10, 11, 16, 17, 18, 19, 12, 13, 14, 15, 1, 2, 3};
+
+// element (frame f, point j, component c) of a (B, P, C) batch in the given layout (rtg.h rtg_layout)
+RTG_DEV int64_t lay_idx(bool soa, int64_t f, int j, int c, int P, int C, int64_t B)
+{
+    return soa ? ((int64_t)(j * C + c)) * B + f : f * (P * C) + C * j + c;
+}
+
+__global__ __launch_bounds__(256) void k_ingest_vtrdyn(const float *__restrict__ bp, const float *__restrict__ lhp,
+                                                       const float *__restrict__ rhp, int64_t B,
+                                                       float *__restrict__ body, float *__restrict__ lh,
+                                                       float *__restrict__ rh, uint8_t *__restrict__ valid, bool soa)
+{
+    const int64_t f = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (f >= B) return;
+    const float *b = bp + f * 69;
+    bool close = true;   // np.allclose(body_pos, 0): |x| <= 1e-8 everywhere (a NaN is never close)
+    for (int i = 0; i < 69; ++i) close = close && (fabsf(b[i]) <= 1e-8f);
+    valid[f] = close ? 0 : 1;
+    if (!soa) {
+        for (int j = 0; j < 21; ++j) st3(body + f * 63 + 3 * j, ld3(b + 3 * c_body23_to_21[j]));
+        for (int j = 0; j < 20; ++j) {
+            st3(lh + f * 60 + 3 * j, ld3(lhp + f * 60 + 3 * c_hand_order[j]));
+            st3(rh + f * 60 + 3 * j, ld3(rhp + f * 60 + 3 * c_hand_order[j]));
+        }
+        return;
+    }
+    for (int j = 0; j < 21; ++j)   // SoA planes: each store instruction writes 256 contiguous bytes per wave
+        for (int c = 0; c < 3; ++c) body[lay_idx(true, f, j, c, 21, 3, B)] = b[3 * c_body23_to_21[j] + c];
+    for (int j = 0; j < 20; ++j)
+        for (int c = 0; c < 3; ++c) {
+            lh[lay_idx(true, f, j, c, 20, 3, B)] = lhp[f * 60 + 3 * c_hand_order[j] + c];
+            rh[lay_idx(true, f, j, c, 20, 3, B)] = rhp[f * 60 + 3 * c_hand_order[j] + c];
+        }
+}
+
+int32_t fk_schedule(const int32_t *parents, int32_t J, int32_t *sched)
+{
+    // last non-consecutive child of every branch parent
+    int32_t *last = new int32_t[J];
+    int32_t *slot_of = new int32_t[J];
+    for (int j = 0; j < J; ++j) last[j] = slot_of[j] = -1;
+    for (int k = 1; k < J; ++k)
+        if (parents[k] != k - 1) last[parents[k]] = k;
+    uint32_t used = 0;   // bitmask of live slots (the schedule is only used when nslots <= kMaxFkSlots)
+    int32_t nslots = 0, overflow = 0;
+    for (int j = 0; j < J; ++j) {
+        int32_t ld = kNoSlot, sv = kNoSlot;
+        const int p = j > 0 ? parents[j] : -1;
+        if (j > 0 && p != j - 1) {
+            ld = slot_of[p];
+            if (last[p] == j && ld >= 0 && ld < 32) used &= ~(1u << ld);   // free after this read
+        }
+        if (last[j] >= 0) {
+            int s = 0;
+            while (s < 32 && (used >> s) & 1u) ++s;
+            if (s >= 32) { overflow = 1; s = 31; }
+            used |= 1u << s;
+            slot_of[j] = s;
+            sv = s;
+            nslots = s + 1 > nslots ? s + 1 : nslots;
+        }
+        sched[j] = (ld & 0xFF) | ((sv & 0xFF) << 8);
+    }
+    delete[] last;
+    delete[] slot_of;
+    return overflow ? 1 << 30 : nslots;
+}
+
+
+// ----------------------------------------------------------------------------
+// elementwise primitives
+// ----------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void k_quat_op(int op, const float *__restrict__ a, const float *__restrict__ b,
+                                                 const float *__restrict__ c, int64_t n, float *__restrict__ out)
+{
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    switch (op) {
+    case RTG_OP_QUAT_MUL: st4(out + 4 * i, qmul(ld4(a + 4 * i), ld4(b + 4 * i))); break;
+    case RTG_OP_QUAT_MUL_NORM: st4(out + 4 * i, qmul_norm(ld4(a + 4 * i), ld4(b + 4 * i))); break;
+    case RTG_OP_QUAT_NORMALIZE: st4(out + 4 * i, qnormalize(ld4(a + 4 * i))); break;
+    case RTG_OP_QUAT_ROTATE: st3(out + 3 * i, qrotate(ld4(a + 4 * i), ld3(b + 3 * i))); break;
+    case RTG_OP_QUAT_INVERSE: st4(out + 4 * i, qconj(ld4(a + 4 * i))); break;
+    case RTG_OP_QUAT_FROM_ANGLE_AXIS: st4(out + 4 * i, qfrom_angle_axis(a[i], ld3(b + 3 * i))); break;
+    case RTG_OP_QUAT_FROM_ROTMAT: {
+        float m[9];
+#pragma unroll
+        for (int k = 0; k < 9; ++k) m[k] = a[9 * i + k];
+        st4(out + 4 * i, qfrom_rotmat(m));
+        break;
+    }
+    case RTG_OP_QUAT_TO_EXP_MAP: st3(out + 3 * i, qexp_map(ld4(a + 4 * i))); break;
+    case RTG_OP_RADIANS_BETWEEN: out[i] = radians_between(ld3(a + 3 * i), ld3(b + 3 * i), ld3(c + 3 * i)); break;
+    case RTG_OP_PROJ_IN_PLANE: st3(out + 3 * i, proj_in_plane(ld3(a + 3 * i), ld3(b + 3 * i))); break;
+    case RTG_OP_QUAT_TO_DOF_POS: {
+        const float *q = a + i * 124 + 4;   // local_rot[1:]
+#pragma unroll
+        for (int k = 0; k < 30; ++k) out[i * 30 + k] = qexp_component(ld4(q + 4 * k), hu_dof_axis(k));
+        break;
+    }
+    case RTG_OP_SHOULDER_PR: {
+        Q p, r;
+        const V v0 = ld3(b + 3 * i);
+        shoulder_pr(ld3(a + 3 * i), shoulder_zero(v0), ld4(c + 4 * i), p, r);
+        st4(out + 8 * i, p);
+        st4(out + 8 * i + 4, r);
+        break;
+    }
+    case RTG_OP_ELBOW_PY: {
+        Q y, e;
+        const V v0 = ld3(b + 3 * i);
+        elbow_py(ld3(a + 3 * i), elbow_zero(v0), ld4(c + 4 * i), y, e);
+        st4(out + 8 * i, y);
+        st4(out + 8 * i + 4, e);
+        break;
+    }
+    case RTG_OP_QUAT_TO_ANGLE_AXIS: st4(out + 4 * i, qangle_axis(ld4(a + 4 * i))); break;
+    case RTG_OP_NORMALIZE_ANGLE: out[i] = normalize_angle(a[i]); break;
+    case RTG_OP_QUAT_ABS: out[i] = qabs(ld4(a + 4 * i)); break;
+    case RTG_OP_QUAT_UNIT: st4(out + 4 * i, qunit(ld4(a + 4 * i))); break;
+    case RTG_OP_QUAT_ANGLE_AXIS: st4(out + 4 * i, qangle_axis_abs(ld4(a + 4 * i))); break;
+    case RTG_OP_EXP_MAP_TO_ANGLE_AXIS: st4(out + 4 * i, exp_map_angle_axis(ld3(a + 3 * i))); break;
+    case RTG_OP_EXP_MAP_TO_QUAT: {
+        const Q aa = exp_map_angle_axis(ld3(a + 3 * i));
+        st4(out + 4 * i, qfrom_angle_axis(aa.x, V{aa.y, aa.z, aa.w}));
+        break;
+    }
+    case RTG_OP_QUAT_SLERP: st4(out + 4 * i, qslerp(ld4(a + 4 * i), ld4(b + 4 * i), c[i])); break;
+    case RTG_OP_QUAT_FROM_XYZ: {
+        const V v = ld3(a + 3 * i);
+        st4(out + 4 * i, Q{v.x, v.y, v.z, 1.0f - lnorm3(v)});
+        break;
+    }
+    case RTG_OP_ROT_MATRIX_DET: {
+        float m[9];
+#pragma unroll
+        for (int k = 0; k < 9; ++k) m[k] = a[9 * i + k];
+        out[i] = rotmat_det(m);
+        break;
+    }
+    case RTG_OP_ROT_MATRIX_FROM_QUAT: {
+        float m[9];
+        rotmat_from_quat(ld4(a + 4 * i), m);
+#pragma unroll
+        for (int k = 0; k < 9; ++k) out[9 * i + k] = m[k];
+        break;
+    }
+    case RTG_OP_ROTATION_ALONG_X:
+    case RTG_OP_ROTATION_ALONG_Y:
+    case RTG_OP_ROTATION_ALONG_Z: out[i] = axis_angle_of(ld4(a + 4 * i), op - RTG_OP_ROTATION_ALONG_X); break;
+    case RTG_OP_PROJECT_QUAT_X:
+    case RTG_OP_PROJECT_QUAT_Y:
+    case RTG_OP_PROJECT_QUAT_Z: {
+        const int ax = op - RTG_OP_PROJECT_QUAT_X;
+        st4(out + 4 * i, axis_half_quat(ax, axis_angle_of(ld4(a + 4 * i), ax)));
+        break;
+    }
+    case RTG_OP_PROJECT_QUAT_XY:
+    case RTG_OP_PROJECT_QUAT_XZ: {
+        const Q q = ld4(a + 4 * i);
+        const int ax2 = op == RTG_OP_PROJECT_QUAT_XY ? 1 : 2;
+        st4(out + 4 * i, qmul(axis_half_quat(0, axis_angle_of(q, 0)), axis_half_quat(ax2, axis_angle_of(q, ax2))));
+        break;
+    }
+    default: break;
+    }
+}
+
+// scipy Rotation.from_quat(q).as_euler(seq[, degrees]) in float64 (rotation3d.py:658-661 quat_to_eular)
+__global__ __launch_bounds__(256) void k_quat_as_euler(const float *__restrict__ q, int s0, int s1, int s2,
+                                                       int extrinsic, int degrees, int64_t n, double *__restrict__ out)
+{
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    double ang[3];
+    scipy_as_euler(ld4(q + 4 * i), s0, s1, s2, extrinsic != 0, ang);
+#pragma unroll
+    for (int t = 0; t < 3; ++t) out[3 * i + t] = degrees ? ang[t] * (180.0 / M_PI) : ang[t];   // np.rad2deg
+}
+
+template <int N>
+__global__ __launch_bounds__(256) void k_cal_joint_quat(const float *__restrict__ Z, const float *__restrict__ M,
+                                                        int64_t n, float *__restrict__ out)
+{
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    V z[N], m[N];
+#pragma unroll
+    for (int j = 0; j < N; ++j) {
+        z[j] = ld3(Z + (i * N + j) * 3);
+        m[j] = ld3(M + (i * N + j) * 3);
+    }
+    st4(out + 4 * i, cal_joint_quat<N>(z, m));
+}
+
+__global__ __launch_bounds__(256) void k_quat_in_xyz_axis(const float *__restrict__ q, int s0, int s1, int s2,
+                                                          int extrinsic, int64_t n, float *__restrict__ out)
+{
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    Q e[3];
+    quat_in_xyz_axis(ld4(q + 4 * i), s0, s1, s2, extrinsic != 0, e);
+#pragma unroll
+    for (int t = 0; t < 3; ++t) st4(out + (i * 3 + t) * 4, e[t]);
+}
+
+// ----------------------------------------------------------------------------
+// motion velocities: thread per (sequence, frame, channel), channel fastest
+// (coalesced over the J*C channels of a frame).
+// ----------------------------------------------------------------------------
+// np.gradient along frames (edge_order 1, unit spacing) then / dt, all float32
+__global__ __launch_bounds__(256) void k_gradient_dt(const float *__restrict__ p, int64_t nseq, int64_t L, int64_t S,
+                                                     float dt, float *__restrict__ v)
+{
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= nseq * L * S) return;
+    const int64_t s = i % S, t = (i / S) % L, base = i - s - t * S;
+    float g;
+    if (L == 1) g = 0.0f;   // numpy raises for < 2 frames; rtg_* rejects L < 2 before launch
+    else if (t == 0) g = (p[base + S + s] - p[base + s]) / 1.0f;
+    else if (t == L - 1) g = (p[base + t * S + s] - p[base + (t - 1) * S + s]) / 1.0f;
+    else g = (p[base + (t + 1) * S + s] - p[base + (t - 1) * S + s]) / 2.0f;
+    v[i] = g / dt;
+}
+
+// quat_mul_norm(r[t+1], quat_inverse(r[t])) -> quat_angle_axis -> axis * angle / dt (last frame: identity -> 0)
+__global__ __launch_bounds__(256) void k_angular_raw(const float *__restrict__ r, int64_t nseq, int64_t L, int64_t J,
+                                                     float dt, float *__restrict__ v)
+{
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= nseq * L * J) return;
+    const int64_t t = (i / J) % L;
+    Q d = qident();
+    if (t < L - 1) d = qmul_norm(ld4(r + 4 * (i + J)), qconj(ld4(r + 4 * i)));
+    const Q aa = qangle_axis_abs(d);
+    v[3 * i + 0] = (aa.y * aa.x) / dt;
+    v[3 * i + 1] = (aa.z * aa.x) / dt;
+    v[3 * i + 2] = (aa.w * aa.x) / dt;
+}
+
+// scipy.ndimage.gaussian_filter1d(mode='nearest') along frames: symmetric correlate1d,
+// float64 accumulation from the outermost tap pair inwards, rounded to float32 once
+__global__ __launch_bounds__(256) void k_gauss_nearest(const float *__restrict__ v, int64_t nseq, int64_t L, int64_t S,
+                                                       GaussTaps taps, float *__restrict__ out)
+{
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= nseq * L * S) return;
+    const int64_t s = i % S, t = (i / S) % L, base = i - s - t * S;
+    const int R = taps.radius;
+    auto at = [&](int64_t tt) { tt = tt < 0 ? 0 : (tt > L - 1 ? L - 1 : tt); return (double)v[base + tt * S + s]; };
+    double acc = at(t) * taps.w[R];
+    for (int jj = -R; jj < 0; ++jj) acc += (at(t + jj) + at(t - jj)) * taps.w[R + jj];
+    out[i] = (float)acc;
+}
+
+hipError_t launch_linear_velocity(const float *p, int64_t nseq, int64_t L, int64_t S, float dt, const GaussTaps *taps,
+                                  float *tmp, float *out, hipStream_t s)
+{
+    const int64_t n = nseq * L * S;
+    const unsigned g = (unsigned)((n + 255) / 256);
+    hipLaunchKernelGGL(k_gradient_dt, dim3(g), dim3(256), 0, s, p, nseq, L, S, dt, taps ? tmp : out);
+    if (taps) hipLaunchKernelGGL(k_gauss_nearest, dim3(g), dim3(256), 0, s, tmp, nseq, L, S, *taps, out);
+    return hipGetLastError();
+}
+
+hipError_t launch_angular_velocity(const float *r, int64_t nseq, int64_t L, int64_t J, float dt,
+                                   const GaussTaps *taps, float *tmp, float *out, hipStream_t s)
+{
+    const int64_t n = nseq * L * J;
+    hipLaunchKernelGGL(k_angular_raw, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, r, nseq, L, J, dt,
+                       taps ? tmp : out);
+    if (taps)
+        hipLaunchKernelGGL(k_gauss_nearest, dim3((unsigned)((3 * n + 255) / 256)), dim3(256), 0, s, tmp, nseq, L,
+                           3 * J, *taps, out);
+    return hipGetLastError();
+}
+
+// ----------------------------------------------------------------------------
+// synthetic mocap on the device (bench / large-size tests)
+// counter-based hash RNG: frame f, draw k -> uniform in (0,1)
+// ----------------------------------------------------------------------------
+RTG_DEV uint64_t mix64(uint64_t z)
+{
+    z = (z ^ (z >> 30)) * 0xbf58476d1ce4e5b9ull;
+    z = (z ^ (z >> 27)) * 0x94d049bb133111ebull;
+    return z ^ (z >> 31);
+}
+RTG_DEV float urand(uint64_t seed, uint64_t f, uint32_t k)
+{
+    const uint64_t h = mix64(seed * 0x9e3779b97f4a7c15ull ^ mix64(f * 0x100000001b3ull + k));
+    return ((float)(h >> 40) + 0.5f) * (1.0f / 16777216.0f);
+}
+RTG_DEV float nrand(uint64_t seed, uint64_t f, uint32_t k)   // Box-Muller
+{
+    const float u1 = urand(seed, f, k), u2 = urand(seed, f, k + 0x8000u);
+    return sqrtf(-2.0f * logf(u1)) * cosf(6.28318530718f * u2);
+}
+RTG_DEV Q axis_angle_f(V ax, float ang)
+{
+    const float n = sqrtf(ax.x * ax.x + ax.y * ax.y + ax.z * ax.z);
+    const float s = sinf(0.5f * ang) / n, c = cosf(0.5f * ang);
+    return Q{ax.x * s, ax.y * s, ax.z * s, c};
+}
+RTG_DEV Q fast_qmul(Q a, Q b)
+{
+    return Q{a.w * b.x + a.x * b.w + a.y * b.z - a.z * b.y, a.w * b.y + a.y * b.w + a.z * b.x - a.x * b.z,
+             a.w * b.z + a.z * b.w + a.x * b.y - a.y * b.x, a.w * b.w - a.x * b.x - a.y * b.y - a.z * b.z};
+}
+RTG_DEV V fast_rot(Q q, V v)
+{
+    const V u{q.x, q.y, q.z};
+    const V t{2.0f * (u.y * v.z - u.z * v.y), 2.0f * (u.z * v.x - u.x * v.z), 2.0f * (u.x * v.y - u.y * v.x)};
+    return V{v.x + q.w * t.x + (u.y * t.z - u.z * t.y), v.y + q.w * t.y + (u.z * t.x - u.x * t.z),
+             v.z + q.w * t.z + (u.x * t.y - u.y * t.x)};
+}
+
+// joint group of VTRDYN_FULL (retarget/robot_config/VTRDYN_FULL.py:9-69): 0 root, 1 spine/arm, 2 leg, 3 finger
+RTG_DEV int full_group(int j)
+{
+    if (j == 0) return 0;
+    if (j <= 6) return 2;
+    if ((j >= 15 && j <= 33) || j >= 40) return 3;
+    return 1;
+}
+
+__constant__ int kFullToBody[21] = {0, 4, 5, 6, 1, 2, 3, 7, 8, 9, 10, 34, 35, 36, 37, 38, 39, 11, 12, 13, 14};
+
+__global__ __launch_bounds__(64) void k_synth_full_body(TopoView T, uint64_t seed, int64_t off, int64_t B,
+                                                        float *__restrict__ body, float *__restrict__ lh,
+                                                        float *__restrict__ rh, float *__restrict__ body_rot, bool soa)
+{
+    __shared__ float sp[64][59 * 3 + 1];
+    __shared__ float sq[64][59 * 4];
+    const int64_t f = (int64_t)blockIdx.x * 64 + threadIdx.x;
+    if (f >= B) return;
+    const uint64_t fr = (uint64_t)(off + f);
+    float *P = sp[threadIdx.x];
+    float *G = sq[threadIdx.x];
+    for (int j = 0; j < T.J; ++j) {
+        const int grp = full_group(j);
+        const uint32_t k = 16u * (uint32_t)j;
+        Q lq;
+        if (grp == 0) {
+            lq = axis_angle_f(V{0.f, 0.f, 1.f}, (urand(seed, fr, k) * 2.0f - 1.0f) * 3.14159265f);
+        } else if (grp == 3) {
+            const bool yax = urand(seed, fr, k + 1) < 0.5f;
+            lq = axis_angle_f(yax ? V{0.f, 1.f, 0.f} : V{0.f, 0.f, 1.f}, 1.2f * urand(seed, fr, k + 2));
+        } else {
+            const V ax{nrand(seed, fr, k + 3), nrand(seed, fr, k + 4), nrand(seed, fr, k + 5)};
+            lq = axis_angle_f(ax, (grp == 1 ? 1.0f : 0.5f) * urand(seed, fr, k + 6));
+        }
+        Q g;
+        V t;
+        const int p = T.parents[j];
+        if (p < 0) {
+            g = lq;
+            t = V{0.1f * nrand(seed, fr, 2000), 0.1f * nrand(seed, fr, 2001), 0.1f * nrand(seed, fr, 2002)};
+        } else {
+            const Q gp{G[4 * p], G[4 * p + 1], G[4 * p + 2], G[4 * p + 3]};
+            const V r = fast_rot(gp, T.local_t[j]);
+            g = fast_qmul(gp, lq);
+            t = V{r.x + P[3 * p], r.y + P[3 * p + 1], r.z + P[3 * p + 2]};
+        }
+        G[4 * j] = g.x; G[4 * j + 1] = g.y; G[4 * j + 2] = g.z; G[4 * j + 3] = g.w;
+        P[3 * j] = t.x; P[3 * j + 1] = t.y; P[3 * j + 2] = t.z;
+    }
+    auto jit = [&](int j, int c) { return P[3 * j + c] + 0.002f * nrand(seed, fr, 3000u + 3u * j + c); };
+    for (int i = 0; i < 21; ++i) {
+        const int j = kFullToBody[i];
+#pragma unroll
+        for (int c = 0; c < 3; ++c) body[lay_idx(soa, f, i, c, 21, 3, B)] = jit(j, c);
+        if (body_rot) {
+            float n = sqrtf(G[4 * j] * G[4 * j] + G[4 * j + 1] * G[4 * j + 1] + G[4 * j + 2] * G[4 * j + 2] +
+                            G[4 * j + 3] * G[4 * j + 3]);
+            if (G[4 * j + 3] < 0.0f) n = -n;
+#pragma unroll
+            for (int c = 0; c < 4; ++c) body_rot[lay_idx(soa, f, i, c, 21, 4, B)] = G[4 * j + c] / n;
+        }
+    }
+    for (int i = 0; i < 20; ++i) {
+#pragma unroll
+        for (int c = 0; c < 3; ++c) {
+            lh[lay_idx(soa, f, i, c, 20, 3, B)] = jit(14 + i, c);
+            rh[lay_idx(soa, f, i, c, 20, 3, B)] = jit(39 + i, c);
+        }
+    }
+}
+
+hipError_t launch_rescale_motion(const TopoView &T, const float *motion, int64_t B, const float *dir, float *out,
+                                 hipStream_t s)
+{
+    const Dir3 d = dir ? Dir3{dir[0], dir[1], dir[2], 1} : Dir3{1.0f, 1.0f, 1.0f, 0};
+    hipLaunchKernelGGL(k_rescale_motion, dim3(grid_for(B, 256)), dim3(256), 0, s, T, motion, B, d, out);
+    return hipGetLastError();
+}
+
+hipError_t launch_quat_between(const float *v1, const float *v2, int64_t n, float *out, float *ws, hipStream_t s)
+{
+    hipError_t e = hipMemsetAsync(ws, 0, 2 * sizeof(float), s);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(k_qbtv_norm_max, dim3(grid_for(n, 256)), dim3(256), 0, s, v1, v2, n, ws);
+    hipLaunchKernelGGL(k_quat_between, dim3(grid_for(n, 256)), dim3(256), 0, s, v1, v2, n, ws, out);
+    return hipGetLastError();
+}
+
+hipError_t launch_rebuild_vtrdyn(const TopoView &T, const float *motion, int64_t B, float *g_rot, float *root_t,
+                                 float *ws, hipStream_t s)
+{
+    hipError_t e = hipMemsetAsync(ws, 0, T.J * sizeof(float), s);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(k_rebuild_norm_max, dim3(grid_for(B, 256)), dim3(256), 0, s, T, motion, B, ws);
+    hipLaunchKernelGGL(k_rebuild_vtrdyn, dim3(grid_for(B, 256)), dim3(256), 0, s, T, motion, B, ws, g_rot, root_t);
+    return hipGetLastError();
+}
+
+hipError_t launch_ingest_vtrdyn(const float *bp, const float *lhp, const float *rhp, int64_t B, int layout,
+                                float *body, float *lh, float *rh, uint8_t *valid, hipStream_t s)
+{
+    hipLaunchKernelGGL(k_ingest_vtrdyn, dim3(grid_for(B, 256)), dim3(256), 0, s, bp, lhp, rhp, B, body, lh, rh, valid,
+                       layout == RTG_LAYOUT_SOA);
+    return hipGetLastError();
+}
+
+hipError_t launch_quat_op(int op, const float *a, const float *b, const float *c, int64_t n, float *out,
+                          hipStream_t s)
+{
+    hipLaunchKernelGGL(k_quat_op, dim3(grid_for(n, 256)), dim3(256), 0, s, op, a, b, c, n, out);
+    return hipGetLastError();
+}
+
+hipError_t launch_cal_joint_quat(const float *Z, const float *M, int npts, int64_t n, float *out, hipStream_t s)
+{
+    const dim3 g(grid_for(n, 256)), b(256);
+    switch (npts) {
+    case 1: hipLaunchKernelGGL(k_cal_joint_quat<1>, g, b, 0, s, Z, M, n, out); break;
+    case 2: hipLaunchKernelGGL(k_cal_joint_quat<2>, g, b, 0, s, Z, M, n, out); break;
+    case 3: hipLaunchKernelGGL(k_cal_joint_quat<3>, g, b, 0, s, Z, M, n, out); break;
+    case 4: hipLaunchKernelGGL(k_cal_joint_quat<4>, g, b, 0, s, Z, M, n, out); break;
+    case 5: hipLaunchKernelGGL(k_cal_joint_quat<5>, g, b, 0, s, Z, M, n, out); break;
+    case 6: hipLaunchKernelGGL(k_cal_joint_quat<6>, g, b, 0, s, Z, M, n, out); break;
+    case 7: hipLaunchKernelGGL(k_cal_joint_quat<7>, g, b, 0, s, Z, M, n, out); break;
+    default: hipLaunchKernelGGL(k_cal_joint_quat<8>, g, b, 0, s, Z, M, n, out); break;
+    }
+    return hipGetLastError();
+}
+
+hipError_t launch_quat_as_euler(const float *q, int s0, int s1, int s2, int extrinsic, int degrees, int64_t n,
+                               double *out, hipStream_t s)
+{
+    hipLaunchKernelGGL(k_quat_as_euler, dim3(grid_for(n, 256)), dim3(256), 0, s, q, s0, s1, s2, extrinsic, degrees, n,
+                       out);
+    return hipGetLastError();
+}
+hipError_t launch_quat_in_xyz_axis(const float *q, int s0, int s1, int s2, int extrinsic, int64_t n, float *out,
+                                   hipStream_t s)
+{
+    hipLaunchKernelGGL(k_quat_in_xyz_axis, dim3(grid_for(n, 256)), dim3(256), 0, s, q, s0, s1, s2, extrinsic, n, out);
+    return hipGetLastError();
+}
+
+hipError_t launch_synth_full_body(const TopoView &T, uint64_t seed, int64_t off, int64_t B, float *body, float *lh,
+                                  float *rh, float *body_rot, int layout, hipStream_t s)
+{
+    hipLaunchKernelGGL(k_synth_full_body, dim3(grid_for(B, 64)), dim3(64), 0, s, T, seed, off, B, body, lh, rh,
+                       body_rot,
+                       layout == RTG_LAYOUT_SOA);
+    return hipGetLastError();
+}
+
+}  // namespace rtg
+
+// ----------------------------------------------------------------------------
+// build configuration (rtg.h rtg_build_info): every RTG_* knob as compiled into this library
+// ----------------------------------------------------------------------------
+#if RTG_EXP_STUB_SVD + RTG_EXP_NO_TABLE + RTG_EXP_HOT_INPUTS == 0
+#define RTG_WRONG_ANSWER_KNOBS 0
+#else
+#define RTG_WRONG_ANSWER_KNOBS 1
+#endif
+#define RTG_STR2(x) #x
+#define RTG_STR(x) RTG_STR2(x)
+#define RTG_KNOB(k) "\"" #k "\":\"" RTG_STR(k) "\","   // values as written (some are expressions)
+extern "C" const char *rtg_build_info(void)
+{
+    return "{\"abi\":" RTG_STR(RTG_ABI_VERSION) ",\"arch\":\"gfx950\",\"knobs\":{"
+        RTG_KNOB(RTG_FAST_EXACT) RTG_KNOB(RTG_SVD_DIV) RTG_KNOB(RTG_SVD_SQRT) RTG_KNOB(RTG_ANG_TAB_BITS)
+        RTG_KNOB(RTG_SOLVER_SIDES) RTG_KNOB(RTG_SIDES_REBALANCE) RTG_KNOB(RTG_SIDES_FIN_LEFT) RTG_KNOB(RTG_SIDES_WAVES)
+        RTG_KNOB(RTG_PRELOAD_ARM) RTG_KNOB(RTG_PRELOAD_TIPS) RTG_KNOB(RTG_L2_PREFETCH) RTG_KNOB(RTG_LATENCY_MAX_B)
+        RTG_KNOB(RTG_LATENCY_WAVES) RTG_KNOB(RTG_FK_CHUNK) RTG_KNOB(RTG_FK_POS_REGS) RTG_KNOB(RTG_FK_MIN_WAVES)
+        RTG_KNOB(RTG_FK_ALIGNED_STORE) RTG_KNOB(RTG_FK_REG_SLOTS) RTG_KNOB(RTG_FK_NT_STORE) RTG_KNOB(RTG_DOF_FK_POS_REGS)
+        RTG_KNOB(RTG_EXP_TIMESTAMPS) RTG_KNOB(RTG_EXP_STUB_SVD) RTG_KNOB(RTG_EXP_NO_TABLE)
+        "\"RTG_EXP_HOT_INPUTS\":\"" RTG_STR(RTG_EXP_HOT_INPUTS) "\"},\"wrong_answer_knobs\":"
+        RTG_STR(RTG_WRONG_ANSWER_KNOBS) "}";
+}

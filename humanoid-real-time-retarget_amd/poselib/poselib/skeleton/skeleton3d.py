@@ -23,12 +23,13 @@ from rtg import ops
 from rtg.bridge import as_tensor, back, topology
 from rtg.safe_pickle import load_skeleton_state_arrays
 
+from ..core.backend import Serializable
 from ..core.rotation3d import quat_identity, quat_normalize
 
-__all__ = ["SkeletonTree", "SkeletonState", "SkeletonMotion", "load_skeleton_state"]
+__all__ = ["SkeletonTree", "SkeletonState", "SkeletonMotion", "MotionDICT", "load_skeleton_state"]
 
 
-class SkeletonTree:
+class SkeletonTree(Serializable):
     """Parent-indexed rigid skeleton (skeleton3d.py:22-263)."""
 
     def __init__(self, node_names, parent_indices, local_translation, quat=None):
@@ -98,7 +99,7 @@ class SkeletonTree:
                             ("local_translation", d(self.local_translation))])
 
 
-class SkeletonState:
+class SkeletonState(Serializable):
     """A static pose: rotations (local or global) + root translation (skeleton3d.py:266-934)."""
 
     def __init__(self, tensor_backend, skeleton_tree, is_local):
@@ -306,16 +307,52 @@ class SkeletonMotion(SkeletonState):
         return cls.from_state_vector_and_velocity(skeleton_state.skeleton_tree, skeleton_state.tensor,
                                                   back(gv, dev), back(gav, dev), skeleton_state.is_local, fps)
 
-    def to_dict(self):
-        d = super().to_dict()
+    @staticmethod
+    def _to_state_vector(rot, rt, vel, avel):
+        """[J*4 rotations, 3 root, J*3 velocities, J*3 angular velocities] (skeleton3d.py:1051-1058)."""
+        shape = rot.shape[:-2]
+        parts = [rot, rt.to(rot.device).broadcast_to(*shape + rt.shape[-1:]), vel.to(rot.device), avel.to(rot.device)]
+        return torch.cat([x.reshape(*(shape + (-1,))) for x in parts], dim=-1)
 
+    def to_dict(self):
         def arr(x):
             x = x.detach().cpu().numpy()
             return {"arr": x, "context": {"dtype": x.dtype.name}}
-        d["global_velocity"] = arr(self.global_velocity)
-        d["global_angular_velocity"] = arr(self.global_angular_velocity)
-        d["fps"] = self.fps
-        return d
+        return OrderedDict([("rotation", arr(self.rotation)), ("root_translation", arr(self.root_translation)),
+                            ("global_velocity", arr(self.global_velocity)),
+                            ("global_angular_velocity", arr(self.global_angular_velocity)),
+                            ("skeleton_tree", self.skeleton_tree.to_dict()), ("is_local", self.is_local),
+                            ("fps", self.fps)])
+
+    @classmethod
+    def from_dict(cls, dict_repr, *args, **kwargs):
+        """skeleton3d.py:1061-1071"""
+        def arr(d):
+            return torch.from_numpy(np.asarray(d["arr"]).astype(d["context"]["dtype"]))
+        return cls(SkeletonMotion._to_state_vector(arr(dict_repr["rotation"]), arr(dict_repr["root_translation"]),
+                                                   arr(dict_repr["global_velocity"]),
+                                                   arr(dict_repr["global_angular_velocity"])),
+                   skeleton_tree=SkeletonTree.from_dict(dict_repr["skeleton_tree"]), is_local=dict_repr["is_local"],
+                   fps=dict_repr["fps"])
+
+
+class MotionDICT:
+    """Global translations + skeleton tree, indexable by frame (skeleton3d.py:1295-1315; the viewers' input)."""
+
+    def __init__(self, gt, sk_tree, get_state=False) -> None:
+        self.global_translation = as_tensor(gt).clone()
+        self.skeleton_tree = sk_tree
+        if not get_state and self.global_translation.dim() == 2:
+            self.global_translation = self.global_translation[None, ...]
+
+    def clone(self):
+        return MotionDICT(self.global_translation.clone(), self.skeleton_tree)
+
+    def __getitem__(self, t):
+        return MotionDICT(self.global_translation[t].clone(), self.skeleton_tree, get_state=True)
+
+    def __len__(self):
+        return self.global_translation.shape[0]
 
 
 def load_skeleton_state(path: str) -> SkeletonState:

@@ -28,3 +28,7 @@ Hu_DOF_UPPER = torch.Tensor([
     1.0472, 1.5708, 1.5708, 1.5708, 1.5708, 0.785, 0.7854, 0.044, 0.,
     1.0472, 0., 1.5708, 1.5708, 1.5708, 0.785, 0.7854, 0.044, 0.,
     1., ])
+
+from retarget.robot_config import fill_from_checkout  # noqa: E402
+
+fill_from_checkout(globals())   # the reference's viewer graphs / joint mappings, when a checkout is overlaid

@@ -6,11 +6,23 @@ Results return on the device of the first tensor argument.
 """
 from __future__ import annotations
 
+import copy  # noqa: F401  (re-exported: the reference's module namespace is its star-export surface)
+from typing import Dict  # noqa: F401
+
+import numpy as np  # noqa: F401  (sim_full_body_teleop.py uses ``np`` from ``transform3d import *``)
 import torch
+from scipy.spatial.transform import Rotation as sRot  # noqa: F401
 
 from poselib.poselib.core.rotation3d import *  # noqa: F401,F403  (the reference re-exports rotation3d)
 from rtg import ops
 from rtg.bridge import as_tensor, back, home_device
+
+
+def quat_between_two_vecs(vec1, vec2):
+    """(:8-21) the rotation taking vec1 to vec2 per row: normalise([v1 x v2, 1 + v1.v2]); identity rows when the
+    largest |vec1| or |vec2| in the batch is <= 1e-6 (the reference decides that over the whole batch)."""
+    dev = home_device(vec1, vec2)
+    return back(ops.quat_between_two_vecs(as_tensor(vec1), as_tensor(vec2)), dev)
 
 
 def coord_transform(p, order: list = None, dir=None):
@@ -46,6 +58,19 @@ def radians_between_vecs(v1, v2, n):
     """Signed angle v1 -> v2 about n (:77-100)."""
     dev = home_device(v1, v2, n)
     return back(ops.radians_between_vecs(as_tensor(v1), as_tensor(v2), as_tensor(n)), dev)
+
+
+def exp_map_to_quat(exp_map):
+    """(:146-150) = rotation3d.exp_map_to_quat"""
+    dev = home_device(exp_map)
+    return back(ops.exp_map_to_quat(as_tensor(exp_map)), dev)
+
+
+def quat_slerp(q0, q1, t):
+    """(:152-174) spherical interpolation with the reference's shortest-arc flip and its two fallbacks
+    (|sin half| < 0.001 -> midpoint, |cos half| >= 1 -> q0); t broadcasts to (..., 1)."""
+    dev = home_device(q0, q1, t)
+    return back(ops.quat_slerp(as_tensor(q0), as_tensor(q1), as_tensor(t)), dev)
 
 
 def quat_to_dof_pos(quat, dof_axis):

@@ -67,10 +67,24 @@ class RobotZeroPose:
 
     @classmethod
     def from_urdf(cls, urdf_path):
-        """URDF parsing needs urdfpy (absent, setup-time only).  Build the
-        zero pose from the shipped SkeletonState instead (``from_skeleton_state``)."""
-        raise NotImplementedError("RobotZeroPose.from_urdf needs urdfpy; use from_skeleton_state with "
-                                  "asset/hu_pose/hu_v5_zero_pose.pkl (or rtg.assets 'hu_v5')")
+        """base_robot.py:71-81: the zero pose of a URDF through the reference's own parser,
+        ``retarget.utils.parse_urdf.parse_urdf`` (urdfpy ``link_fk`` -> SkeletonTree.from_dict -> SkeletonState
+        .zero_pose, both drop-in classes here).  That module is not replaced: it comes from the reference checkout
+        the drop-in overlays, imported on first use so that a deployment without urdfpy can still
+        import this module.  Raises ImportError only when the parser (or urdfpy) cannot be imported."""
+        try:
+            from retarget.utils.parse_urdf import parse_urdf
+        except ImportError as e:
+            raise ImportError("RobotZeroPose.from_urdf needs the reference's retarget.utils.parse_urdf (and urdfpy): "
+                              "overlay the drop-in onto a reference checkout, or build the zero pose with "
+                              f"from_skeleton_state / from_asset ({e})") from e
+        robot_zero_pose, _link_mesh_file_names = parse_urdf(urdf_path)
+        return cls(local_translation=robot_zero_pose.local_translation,
+                   global_translation=robot_zero_pose.global_translation,
+                   parent_indices=robot_zero_pose.skeleton_tree.parent_indices,
+                   num_joints=robot_zero_pose.skeleton_tree.num_joints,
+                   node_names=robot_zero_pose.skeleton_tree.node_names,
+                   skeleton_tree=robot_zero_pose.skeleton_tree)
 
     @classmethod
     def from_skeleton_state(cls, skeleton_state: SkeletonState):

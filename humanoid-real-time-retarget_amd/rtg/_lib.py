@@ -46,6 +46,14 @@ OP_NORMALIZE_ANGLE = 14
 OP_QUAT_ABS = 15
 OP_QUAT_UNIT = 16
 OP_QUAT_ANGLE_AXIS = 17
+OP_EXP_MAP_TO_ANGLE_AXIS = 18
+OP_EXP_MAP_TO_QUAT = 19
+OP_QUAT_SLERP = 20
+OP_QUAT_FROM_XYZ = 21
+OP_ROT_MATRIX_DET = 22
+OP_ROT_MATRIX_FROM_QUAT = 23
+OP_ROTATION_ALONG_X = 24      # + axis (0, 1, 2)
+OP_PROJECT_QUAT = {"x": 27, "y": 28, "z": 29, "xy": 30, "xz": 31}
 
 MAX_SEGMENTS = 8
 
@@ -72,6 +80,7 @@ SIGNATURES = {
     "rtg_abi_version": (c_int, []),
     "rtg_last_error": (c_char_p, []),
     "rtg_device_count": (c_int, []),
+    "rtg_build_info": (c_char_p, []),
     "rtg_topology_create": (c_int, [POINTER(c_int32), POINTER(c_float), POINTER(c_float), c_int32, POINTER(c_void_p)]),
     "rtg_topology_destroy": (c_int, [c_void_p]),
     "rtg_topology_num_joints": (c_int, [c_void_p]),
@@ -102,6 +111,7 @@ SIGNATURES = {
     "rtg_quat_op_f32": (c_int, [c_int, c_void_p, c_void_p, c_void_p, c_int64, c_void_p, c_void_p]),
     "rtg_cal_joint_quat_f32": (c_int, [c_void_p, c_void_p, c_int32, c_int64, c_void_p, c_void_p]),
     "rtg_quat_in_xyz_axis_f32": (c_int, [c_void_p, c_char_p, c_int64, c_void_p, c_void_p]),
+    "rtg_quat_as_euler_f64": (c_int, [c_void_p, c_char_p, c_int, c_int64, c_void_p, c_void_p]),
     "rtg_linear_velocity_f32": (c_int, [c_void_p, c_int64, c_int64, c_int64, c_float, c_void_p, c_int32, c_void_p,
                                         c_void_p, c_void_p]),
     "rtg_angular_velocity_f32": (c_int, [c_void_p, c_int64, c_int64, c_int64, c_float, c_void_p, c_int32, c_void_p,
@@ -128,8 +138,29 @@ def lib() -> ctypes.CDLL:
             fn.argtypes = args
         if handle.rtg_abi_version() != ABI_VERSION:
             raise ImportError(f"librtg_hip ABI {handle.rtg_abi_version()} != expected {ABI_VERSION}")
+        info = build_info(handle)
+        if info["wrong_answer_knobs"] and os.environ.get("RTG_ALLOW_MEASUREMENT_BUILD") != "1":
+            on = {k: v for k, v in info["knobs"].items() if k in WRONG_ANSWER_KNOBS and v}
+            raise ImportError(f"{LIB_PATH} was built with measurement-only knobs that change results ({on}); "
+                              "only tools/variant_bench.sh may load it (RTG_ALLOW_MEASUREMENT_BUILD=1)")
         _lib = handle
     return _lib
+
+
+WRONG_ANSWER_KNOBS = ("RTG_EXP_STUB_SVD", "RTG_EXP_NO_TABLE", "RTG_EXP_HOT_INPUTS")
+
+
+def build_info(handle=None) -> dict:
+    """rtg_build_info(): the library's compile-time knobs (rtg.h)."""
+    import json
+    h = handle if handle is not None else lib()
+    info = json.loads(h.rtg_build_info().decode())
+    for k, v in info["knobs"].items():   # values as the preprocessor wrote them: integers where they are
+        try:
+            info["knobs"][k] = int(v)
+        except ValueError:
+            pass
+    return info
 
 
 def check(status: int) -> None:

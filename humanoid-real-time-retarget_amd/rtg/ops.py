@@ -438,3 +438,67 @@ def synth_full_body(topo_full: Topology, B: int, seed: int = 1234, frame_offset:
     check(lib().rtg_synth_full_body_f32(topo_full.handle, ctypes.c_uint64(seed), frame_offset, B, code, ptr(body),
                                         ptr(lh), ptr(rh), ptr(rot), stream_handle()))
     return (body, lh, rh, rot) if want_rot else (body, lh, rh)
+
+
+# ---- the rest of the rotation3d / transform3d surface (rtg_quat_op_f32 ops 18-31, rtg_quat_as_euler_f64)
+def exp_map_to_angle_axis(e):
+    """rotation3d.py:629-646 -> (angle (...), axis (...,3))"""
+    r = _quat_op(_lib.OP_EXP_MAP_TO_ANGLE_AXIS, e, a_tail=3, out_tail=4)
+    return r[..., 0], r[..., 1:]
+
+
+def exp_map_to_quat(e):
+    """rotation3d.py:648-652 / transform3d.py:146-150"""
+    return _quat_op(_lib.OP_EXP_MAP_TO_QUAT, e, a_tail=3, out_tail=4)
+
+
+def quat_slerp(q0, q1, t):
+    """transform3d.py:152-174: q0, q1 (...,4), t broadcastable to (...,1) -> (...,4)"""
+    q0, q1 = _bcast(q0, q1, 4, 4)
+    t = dev_f32(t)
+    if t.dim() >= 1 and t.shape[-1] == 1 and t.dim() == q0.dim():
+        t = t[..., 0]
+    t = t.expand(q0.shape[:-1]).contiguous()
+    return _quat_op(_lib.OP_QUAT_SLERP, q0, q1, t, c_tail=0)
+
+
+def quat_from_xyz(xyz):
+    """rotation3d.py:101-108 per row: (...,3) -> (...,4) [xyz, 1 - |xyz|]"""
+    return _quat_op(_lib.OP_QUAT_FROM_XYZ, xyz, a_tail=3, out_tail=4)
+
+
+def rot_matrix_det(m):
+    """rotation3d.py:338-350: (...,3,3) -> (...)"""
+    m = dev_f32(m, (3, 3), "m")
+    lead = m.shape[:-2]
+    out = torch.empty(tuple(lead), device=m.device, dtype=torch.float32)
+    check(lib().rtg_quat_op_f32(_lib.OP_ROT_MATRIX_DET, ptr(m), None, None, int(torch.Size(lead).numel()), ptr(out),
+                                stream_handle()))
+    return out
+
+
+def rot_matrix_from_quaternion(q):
+    """rotation3d.py:398-427: (...,4) -> (...,3,3)"""
+    return _quat_op(_lib.OP_ROT_MATRIX_FROM_QUAT, q, out_tail=(3, 3))
+
+
+def extract_rotation_along_axis(q, axis: int):
+    """rotation3d.py:534-556: (n,4) -> (n)"""
+    if axis not in (0, 1, 2):
+        raise ValueError("Invalid axis. Axis must be 0 (x), 1 (y), or 2 (z).")
+    return _quat_op(_lib.OP_ROTATION_ALONG_X + axis, q, out_tail=0)
+
+
+def project_quat_to_axis(q, which: str):
+    """project_quat_to_axis_{x,y,z,xy,xz} (rotation3d.py:479-530): (n,4) -> (n,4)"""
+    return _quat_op(_lib.OP_PROJECT_QUAT[which], q)
+
+
+def quat_as_euler(q, seq: str, degrees: bool = False):
+    """scipy Rotation.from_quat(q).as_euler(seq, degrees) in float64 on the device: (...,4) -> (...,3) f64."""
+    q = dev_f32(q, (4,), "q")
+    lead = q.shape[:-1]
+    out = torch.empty(tuple(lead) + (3,), device=q.device, dtype=torch.float64)
+    check(lib().rtg_quat_as_euler_f64(ptr(q), seq.encode(), int(bool(degrees)), int(torch.Size(lead).numel()),
+                                      ptr(out), stream_handle()))
+    return out

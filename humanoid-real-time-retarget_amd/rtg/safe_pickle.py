@@ -22,7 +22,7 @@ from typing import Any, Dict, List
 
 import numpy as np
 
-__all__ = ["Global", "Call", "Obj", "PersId", "read_pickle_tree", "load_skeleton_state_arrays"]
+__all__ = ["Global", "Call", "Obj", "PersId", "read_pickle_tree", "read_npy_object", "load_skeleton_state_arrays"]
 
 
 @dataclass(frozen=True)
@@ -150,7 +150,10 @@ def _run_vm(stream: io.BytesIO) -> Any:
         elif n == "REDUCE":
             args = stack.pop()
             func = stack.pop()
-            stack.append(Call(func, args))
+            if isinstance(func, Global) and func.qualname == "collections.OrderedDict" and args == ():
+                stack.append({})     # an empty mapping that SETITEM(S) fill: plain data, nothing called
+            else:
+                stack.append(Call(func, args))
         elif n == "NEWOBJ":
             args = stack.pop()
             cls = stack.pop()
@@ -227,6 +230,13 @@ def _resolve(node: Any) -> Any:
                 return _legacy_storage_from_bytes(node.args[0])
             if f.qualname == "collections.OrderedDict":
                 return {}
+            if f.qualname in _NP_RECONSTRUCT:          # np.ndarray.__reduce__: rebuilt from its BUILD state
+                return _ndarray_from_state(node.state)
+            if f.qualname == "numpy.dtype":
+                return _dtype_from(node)
+            if f.qualname in _NP_SCALAR:
+                dt, raw = _resolve(node.args[0]), node.args[1]
+                return np.frombuffer(raw, dtype=dt)[0] if dt != np.dtype(object) else raw
         raise ValueError(f"refusing to resolve call to {f}")
     if isinstance(node, Obj):
         cls = node.cls.qualname if isinstance(node.cls, Global) else str(node.cls)
@@ -241,6 +251,52 @@ def _resolve(node: Any) -> Any:
     if isinstance(node, tuple):
         return tuple(_resolve(v) for v in node)
     return node
+
+
+_NP_RECONSTRUCT = ("numpy.core.multiarray._reconstruct", "numpy._core.multiarray._reconstruct")
+_NP_SCALAR = ("numpy.core.multiarray.scalar", "numpy._core.multiarray.scalar")
+
+
+def _dtype_from(node: Call) -> np.dtype:
+    """numpy.dtype('<code>', align, copy) with BUILD state (version, byteorder, ...): only plain (non-structured)
+    dtypes are accepted."""
+    code = node.args[0]
+    if not isinstance(code, str) or len(code) > 4:
+        raise ValueError(f"refusing dtype {code!r}")
+    dt = np.dtype(code)
+    order = node.state[1] if isinstance(node.state, tuple) and len(node.state) > 1 else "|"
+    if order in ("<", ">"):
+        dt = dt.newbyteorder(order)
+    if dt.fields is not None:
+        raise ValueError("structured dtypes are not supported")
+    return dt
+
+
+def _ndarray_from_state(state: Any) -> np.ndarray:
+    """ndarray BUILD state (version, shape, dtype, is_fortran, data): data is raw bytes, or a list of objects for
+    dtype=object (each resolved as an inert tree)."""
+    _ver, shape, dt, fortran, data = state
+    dt = _resolve(dt)
+    order = "F" if fortran else "C"
+    if dt == np.dtype(object):
+        flat = np.empty(len(data), dtype=object)
+        for i, v in enumerate(data):
+            flat[i] = _resolve(v)
+        return flat.reshape(tuple(shape), order=order)
+    return np.frombuffer(bytes(data), dtype=dt).reshape(tuple(shape), order=order).copy()
+
+
+def read_npy_object(path: str) -> Any:
+    """``np.save`` of a python object (a 0-d object array, e.g. poselib's Serializable.to_file ``.npy``) read as an
+    inert tree -- the non-executing counterpart of ``np.load(path, allow_pickle=True).item()``."""
+    with open(path, "rb") as f:
+        version = np.lib.format.read_magic(f)
+        shape, _fortran, dtype = np.lib.format._read_array_header(f, version)
+        if dtype != np.dtype(object):
+            f.seek(0)
+            return np.lib.format.read_array(f, allow_pickle=False)
+        arr = _resolve(_run_vm(io.BytesIO(f.read())))
+    return arr.reshape(()).item() if isinstance(arr, np.ndarray) and arr.shape == () else arr
 
 
 def read_pickle_tree(path: str) -> Any:

@@ -53,6 +53,10 @@ int rtg_abi_version(void);
 const char *rtg_last_error(void);
 /* Number of visible devices (0 when no GPU / driver). */
 int rtg_device_count(void);
+/* The compile-time configuration of this library as a JSON object: every RTG_* build knob and its value, and
+ * "wrong_answer_knobs" = how many measurement-only knobs that change results (RTG_EXP_STUB_SVD, RTG_EXP_NO_TABLE,
+ * RTG_EXP_HOT_INPUTS) are on.  A product library has 0; the Python binding refuses any other. */
+const char *rtg_build_info(void);
 
 /* ------------------------------------------------------------------------
  * Topology: a parent-indexed skeleton (SkeletonTree, skeleton3d.py:83-96;
@@ -234,7 +238,22 @@ typedef enum rtg_quat_op {
     RTG_OP_NORMALIZE_ANGLE = 14,    /* x (n) -> (n) atan2(sin x, cos x)      rotation3d.py:582-584 */
     RTG_OP_QUAT_ABS = 15,           /* q (n,4) -> (n) |q|                    rotation3d.py:41-47  */
     RTG_OP_QUAT_UNIT = 16,          /* q (n,4) -> q / max(|q|, 1e-9)         rotation3d.py:50-56  */
-    RTG_OP_QUAT_ANGLE_AXIS = 17     /* q (n,4) -> [acos(2w^2-1), xyz/|xyz|]  rotation3d.py:230-240 */
+    RTG_OP_QUAT_ANGLE_AXIS = 17,    /* q (n,4) -> [acos(2w^2-1), xyz/|xyz|]  rotation3d.py:230-240 */
+    /* the rest of the rotation3d / transform3d surface (off the solver path; same op-order contract) */
+    RTG_OP_EXP_MAP_TO_ANGLE_AXIS = 18, /* e (n,3) -> (n,4) [angle, axis]      rotation3d.py:629-646 */
+    RTG_OP_EXP_MAP_TO_QUAT = 19,    /* e (n,3) -> (n,4)      rotation3d.py:648-652 = transform3d.py:146-150 */
+    RTG_OP_QUAT_SLERP = 20,         /* q0 a (n,4), q1 b (n,4), t c (n) -> (n,4)   transform3d.py:152-174 */
+    RTG_OP_QUAT_FROM_XYZ = 21,      /* xyz (n,3) -> (n,4) [xyz, 1 - |xyz|], per row  rotation3d.py:101-108 */
+    RTG_OP_ROT_MATRIX_DET = 22,     /* m (n,3,3) -> (n)                      rotation3d.py:338-350 */
+    RTG_OP_ROT_MATRIX_FROM_QUAT = 23, /* q (n,4) -> (n,3,3)                  rotation3d.py:398-427 */
+    RTG_OP_ROTATION_ALONG_X = 24,   /* q (n,4) -> (n) extract_rotation_along_axis(q, 0)  rotation3d.py:534-556 */
+    RTG_OP_ROTATION_ALONG_Y = 25,   /* ... axis 1 */
+    RTG_OP_ROTATION_ALONG_Z = 26,   /* ... axis 2 */
+    RTG_OP_PROJECT_QUAT_X = 27,     /* q (n,4) -> (n,4)  project_quat_to_axis_x   rotation3d.py:479-486 */
+    RTG_OP_PROJECT_QUAT_Y = 28,     /*                   project_quat_to_axis_y   :488-495 */
+    RTG_OP_PROJECT_QUAT_Z = 29,     /*                   project_quat_to_axis_z   :497-504 */
+    RTG_OP_PROJECT_QUAT_XY = 30,    /*                   project_quat_to_axis_xy  :506-517 */
+    RTG_OP_PROJECT_QUAT_XZ = 31     /*                   project_quat_to_axis_xz  :519-530 */
 } rtg_quat_op;
 int rtg_quat_op_f32(int op, const float *a, const float *b, const float *c, int64_t n, float *out,
                     rtg_stream_t stream);
@@ -247,6 +266,9 @@ int rtg_cal_joint_quat_f32(const float *Z, const float *M, int32_t npts, int64_t
 /* quat_in_xyz_axis (transform3d.py:52-59): scipy Euler split (float64) into three
  * single-axis quaternions.  seq: 3 chars of xyz/XYZ (upper = intrinsic). q (n,4) -> (n,3,4). */
 int rtg_quat_in_xyz_axis_f32(const float *q, const char *seq, int64_t n, float *out, rtg_stream_t stream);
+/* scipy Rotation.from_quat(q).as_euler(seq, degrees) in float64 (rotation3d.py:658-661 quat_to_eular uses
+ * 'xyz', degrees=True; degrees multiply by 180/pi like np.rad2deg).  q (n,4) f32 -> out (n,3) f64. */
+int rtg_quat_as_euler_f64(const float *q, const char *seq, int degrees, int64_t n, double *out, rtg_stream_t stream);
 
 /* ------------------------------------------------------------------------
  * Motion velocities (SkeletonMotion.from_skeleton_state, poselib skeleton3d.py:1026-1049,

@@ -354,3 +354,63 @@ def atan2f(y, x):
     out = np.empty_like(y)
     lib().oracle_atan2f_n(_fp(y), _fp(x), _i64(len(y)), _fp(out))
     return out
+
+
+# ---- the rest of the rotation3d / transform3d surface (rotation3d.py:101-108, 338-427, 479-556, 629-661;
+# transform3d.py:146-174), rows of the reference's per-element arithmetic
+def exp_map_to_angle_axis(e):
+    """rotation3d.py:629-646 -> (n,4) [angle, axis xyz]."""
+    e = _c32(e).reshape(-1, 3)
+    return _unary("oracle_exp_map_to_angle_axis", e, (len(e), 4))
+
+
+def exp_map_to_quat(e):
+    e = _c32(e).reshape(-1, 3)
+    return _unary("oracle_exp_map_to_quat", e, (len(e), 4))
+
+
+def quat_slerp(q0, q1, t):
+    q0, q1 = _c32(q0).reshape(-1, 4), _c32(q1).reshape(-1, 4)
+    t = _c32(np.broadcast_to(np.asarray(t, np.float32).reshape(-1), (len(q0),)))
+    out = np.empty((len(q0), 4), np.float32)
+    lib().oracle_quat_slerp(_fp(q0), _fp(q1), _fp(t), _i64(len(q0)), _fp(out))
+    return out
+
+
+def quat_from_xyz(xyz):
+    xyz = _c32(xyz).reshape(-1, 3)
+    return _unary("oracle_quat_from_xyz", xyz, (len(xyz), 4))
+
+
+def rot_matrix_det(m):
+    m = _c32(m).reshape(-1, 9)
+    out = np.empty(len(m), np.float32)
+    lib().oracle_rot_matrix_det(_fp(m), _i64(len(m)), _fp(out))
+    return out
+
+
+def rot_matrix_from_quaternion(q):
+    q = _c32(q).reshape(-1, 4)
+    return _unary("oracle_rot_matrix_from_quat", q, (len(q), 3, 3))
+
+
+def extract_rotation_along_axis(q, axis):
+    q = _c32(q).reshape(-1, 4)
+    out = np.empty(len(q), np.float32)
+    lib().oracle_rotation_along_axis(_fp(q), ctypes.c_int32(axis), _i64(len(q)), _fp(out))
+    return out
+
+
+PROJECT_MODES = {"x": 0, "y": 1, "z": 2, "xy": 3, "xz": 4}
+
+
+def project_quat_to_axis(q, which):
+    q = _c32(q).reshape(-1, 4)
+    out = np.empty((len(q), 4), np.float32)
+    lib().oracle_project_quat_to_axis(_fp(q), ctypes.c_int32(PROJECT_MODES[which]), _i64(len(q)), _fp(out))
+    return out
+
+
+def quat_to_eular(q):
+    """rotation3d.py:658-661: scipy as_euler('xyz', degrees=True) = radians * (180 / pi) (np.rad2deg)."""
+    return as_euler(_c32(q).reshape(-1, 4), "xyz") * (180.0 / np.pi)

@@ -160,3 +160,126 @@ def test_solver_rejects_bad_input_shapes():
     r = _fake_solver(_lib.SOLVER_FULL_BODY_ROT)
     with pytest.raises(ValueError):   # rotations need 4 components
         r.retarget([torch.zeros(B, 21, 3), torch.zeros(B, 21, 3), torch.zeros(B, 20, 3), torch.zeros(B, 20, 3)])
+
+
+def test_build_info_reports_every_knob_and_no_wrong_answer_build():
+    """rtg_build_info(): every RTG_* knob the sources define is reported, and the product library carries none of
+    the measurement-only knobs that change results (rtg._lib.lib() refuses such a build)."""
+    import json
+    import glob
+    from rtg import _lib
+    info = _lib.build_info()
+    assert info["wrong_answer_knobs"] == 0 and info["abi"] == _lib.ABI_VERSION
+    src = "".join(open(p).read() for ext in ("*.hip", "*.cuh", "*.h", "*.cpp")
+                  for p in glob.glob(os.path.join(REPO, "humanoid-real-time-retarget_amd", "csrc", ext)))
+    defined = set(re.findall(r"#ifndef (RTG_[A-Z0-9_]+)", src)) - {"RTG_H"}
+    assert defined <= set(info["knobs"]), defined - set(info["knobs"])
+    for k in _lib.WRONG_ANSWER_KNOBS:
+        assert info["knobs"][k] == 0
+    json.dumps(info)
+
+
+def _overlay():
+    import json
+    return json.load(open(os.path.join(REPO, "tests", "golden", "overlay_names.json")))
+
+
+def _star(modname):
+    import importlib
+    m = importlib.import_module(modname)
+    names = getattr(m, "__all__", None)
+    return set(names) if names is not None else {n for n in vars(m) if not n.startswith("_")}
+
+
+def test_overlay_exports_every_name_the_reference_uses():
+    """tools/overlay_names.py scanned every reference module the drop-in does NOT replace (retarget/utils, the
+    sim_*_teleop entry points, the viewers, the asset generators) for the names they take from replaced modules
+    -- explicit imports, star imports (then every free name used) and Cls.attr on imported classes.  The drop-ins
+    export every one, and each star-imported drop-in module star-exports at least the reference module's set."""
+    import importlib
+    d = _overlay()
+    assert len(d["names"]) >= 40 and "retarget.spatial_transform.transform3d" in d["star_exports"]
+    for e in d["names"]:
+        m = importlib.import_module(e["module"])
+        assert hasattr(m, e["name"]), (e["module"], e["name"], e["used_by"])
+    for mod, names in d["star_exports"].items():
+        missing = set(names) - _star(mod)
+        assert not missing, (mod, sorted(missing))
+    for e in d["class_attributes"]:
+        if "out_of_scope" in e:
+            continue
+        cls_name, attr = e["attr"].split(".", 1)
+        cls = getattr(importlib.import_module(e["module"]), cls_name)
+        assert hasattr(cls, attr), (e["module"], e["attr"], e["used_by"])
+    # the verdict's list, by name (transform3d.py:9,147,153; rotation3d.py:101,243,629-661)
+    t3 = importlib.import_module("retarget.spatial_transform.transform3d")
+    r3 = importlib.import_module("poselib.poselib.core.rotation3d")
+    for n in ("quat_between_two_vecs", "exp_map_to_quat", "quat_slerp"):
+        assert callable(getattr(t3, n))
+    for n in ("exp_map_to_angle_axis", "exp_map_to_quat", "quat_from_xyz", "quat_yaw_rotation", "quat_to_eular"):
+        assert callable(getattr(r3, n))
+
+
+def test_from_urdf_delegates_to_the_reference_parser(tmp_path):
+    """RobotZeroPose.from_urdf (base_robot.py:71-81) calls retarget.utils.parse_urdf.parse_urdf from the reference
+    checkout the drop-in overlays -- found through the drop-in packages' extended __path__ when that checkout comes
+    later on sys.path -- and raises ImportError naming the parser only when it cannot be imported."""
+    import subprocess
+    import sys
+    ref = tmp_path / "checkout"
+    (ref / "retarget" / "utils").mkdir(parents=True)
+    (ref / "retarget" / "utils" / "__init__.py").write_text("")
+    (ref / "retarget" / "utils" / "parse_urdf.py").write_text(
+        "import torch\n"
+        "from types import SimpleNamespace as NS\n"
+        "CALLS = []\n"
+        "def parse_urdf(urdf_path):\n"
+        "    CALLS.append(urdf_path)\n"
+        "    tree = NS(parent_indices=torch.tensor([-1, 0]), num_joints=2, node_names=['base', 'link'])\n"
+        "    zp = NS(local_translation=torch.tensor([[0., 0, 0], [0, 0, 1]]),\n"
+        "            global_translation=torch.tensor([[0., 0, 0], [0, 0, 1]]), skeleton_tree=tree)\n"
+        "    return zp, ['base.stl', 'link.stl']\n")
+    code = ("import sys\n"
+            "from robot_kinematics_model.base_robot import RobotZeroPose\n"
+            "z = RobotZeroPose.from_urdf('asset/hu/hu_v5.urdf')\n"
+            "import retarget.utils.parse_urdf as P\n"
+            "mod = sys.modules['retarget.utils.parse_urdf']\n"
+            "assert mod.CALLS == ['asset/hu/hu_v5.urdf'], mod.CALLS\n"
+            "assert z.num_joints == 2 and z.node_names == ['base', 'link'] and z.num_dofs == 1\n"
+            "assert z.global_translation[1, 2].item() == 1.0\n"
+            "print('ok')\n")
+    pkg = os.path.join(REPO, "humanoid-real-time-retarget_amd")
+    env = dict(os.environ, PYTHONPATH=os.pathsep.join([pkg, str(ref)]))
+    r = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0 and "ok" in r.stdout, r.stderr[-2000:]
+    # without a checkout: ImportError that names the parser
+    env = dict(os.environ, PYTHONPATH=pkg)
+    r = subprocess.run([sys.executable, "-c", "from robot_kinematics_model.base_robot import RobotZeroPose\n"
+                        "RobotZeroPose.from_urdf('x.urdf')"], env=env, capture_output=True, text=True, timeout=120)
+    assert r.returncode != 0 and "ImportError" in r.stderr and "parse_urdf" in r.stderr
+
+
+def test_serializable_json_and_npy_roundtrip(tmp_path):
+    """Serializable.to_file / from_file (poselib core/backend/abstract.py:94-128) for SkeletonTree / SkeletonState /
+    SkeletonMotion; the .npy path is read by the non-executing pickle walker, not np.load(allow_pickle=True)."""
+    import torch
+    from poselib.poselib.skeleton.skeleton3d import SkeletonMotion, SkeletonState, SkeletonTree
+    tree = SkeletonTree(["a", "b", "c"], torch.tensor([-1, 0, 1]), torch.arange(9, dtype=torch.float32).reshape(3, 3))
+    rot = torch.rand(4, 3, 4)
+    st = SkeletonState(SkeletonState._to_state_vector(rot, torch.rand(4, 3)), tree, True)
+    mo = SkeletonMotion(SkeletonMotion._to_state_vector(rot, torch.rand(4, 3), torch.rand(4, 3, 3), torch.rand(4, 3, 3)),
+                        tree, True, 30)
+    for obj in (tree, st, mo):
+        for ext in ("json", "npy"):
+            p = str(tmp_path / f"{type(obj).__name__}.{ext}")
+            obj.to_file(p)
+            back = type(obj).from_file(p)
+            if isinstance(obj, SkeletonTree):
+                assert back.node_names == tree.node_names and torch.equal(back.parent_indices, tree.parent_indices)
+                assert torch.equal(back.local_translation, tree.local_translation)
+            else:
+                assert torch.equal(back.tensor, obj.tensor) and back.is_local == obj.is_local
+            if isinstance(obj, SkeletonMotion):
+                assert back.fps == 30 and torch.equal(back.global_angular_velocity, obj.global_angular_velocity)
+    with pytest.raises(AssertionError):
+        SkeletonState.from_file(str(tmp_path / "SkeletonTree.json"))

@@ -145,6 +145,57 @@ def local_bindings(tree):
     return out
 
 
+# names the scan finds that the drop-in deliberately leaves out, with the reason (SURVEY.md §2 scope)
+OUT_OF_SCOPE = {
+    "SkeletonTree.from_mjcf": "offline MJCF import (SURVEY §2 row 3); only poselib's own broken test_skeleton.py uses it",
+}
+
+
+def provides(ref, mod, name):
+    """Does the REFERENCE module itself bind ``name`` (a top-level name, star export, or submodule)?"""
+    if mod not in ref.mods:
+        return False
+    if name in ref.star_exports(mod) or f"{mod}.{name}" in ref.mods:
+        return True
+    return any(name in Ref._binds(st) for st in ref._toplevel(ref.tree(mod).body))
+
+
+def class_has(ref, mod, dotted):
+    """Does the reference class (defined in ``mod`` or imported there) have the attribute, through its bases?"""
+    cls, attr = dotted.split(".", 1)
+    seen = set()
+
+    def find(m, c):
+        if (m, c) in seen or m not in ref.mods:
+            return None
+        seen.add((m, c))
+        for node in ast.walk(ref.tree(m)):
+            if isinstance(node, ast.ClassDef) and node.name == c:
+                return m, node
+        for node in ast.walk(ref.tree(m)):     # re-exported: follow the import
+            if isinstance(node, ast.ImportFrom):
+                src = resolve(m, ref.is_pkg(m), node)
+                for a in node.names:
+                    if a.name == "*" or (a.asname or a.name) == c:
+                        hit = find(src, c if a.name == "*" else a.name)
+                        if hit:
+                            return hit
+        return None
+
+    def has(m, c):
+        hit = find(m, c)
+        if not hit:
+            return False
+        m2, node = hit
+        for st in node.body:
+            if isinstance(st, (ast.FunctionDef, ast.AsyncFunctionDef)) and st.name == attr:
+                return True
+            if attr in Ref._binds(st):
+                return True
+        return any(has(m2, b.id) for b in node.bases if isinstance(b, ast.Name))
+    return has(mod, cls)
+
+
 def scan(ref_root):
     ref = Ref(ref_root)
     drop = modules(DROP, MIRRORED_TOPS)
@@ -201,12 +252,23 @@ def scan(ref_root):
             if isinstance(n, ast.Attribute) and isinstance(n.value, ast.Name) and n.value.id in imported_cls \
                     and n.value.id[:1].isupper():
                 need(class_attrs, (imported_cls[n.value.id], f"{n.value.id}.{n.attr}"), f"{rel}:{n.lineno}")
+    star_sources = sorted({src for (src, _name) in req if any("import *" in u for u in req[(src, _name)])})
+    broken = {k: v for k, v in req.items() if not provides(ref, k[0], k[1])}
+    names = {k: v for k, v in req.items() if k not in broken}
+    attrs_ok = {k: v for k, v in class_attrs.items() if class_has(ref, k[0], k[1])}
     return {
         "about": "names that non-replaced reference modules take from replaced ones (tools/overlay_names.py)",
         "replaced_modules": replaced,
-        "names": [{"module": k[0], "name": k[1], "used_by": sorted(v)} for k, v in sorted(req.items())],
-        "class_attributes": [{"module": k[0], "attr": k[1], "used_by": sorted(v)} for k, v in sorted(class_attrs.items())],
+        "names": [{"module": k[0], "name": k[1], "used_by": sorted(v)} for k, v in sorted(names.items())],
+        "class_attributes": [{"module": k[0], "attr": k[1], "used_by": sorted(v),
+                              **({"out_of_scope": OUT_OF_SCOPE[k[1]]} if k[1] in OUT_OF_SCOPE else {})}
+                             for k, v in sorted(attrs_ok.items())],
+        # a replaced module that some caller star-imports must star-export everything the reference's does
+        "star_exports": {m: sorted(ref.star_exports(m)) for m in star_sources},
         "reference_submodules_not_replaced": [{"module": k, "used_by": sorted(v)} for k, v in sorted(submods.items())],
+        "broken_in_reference": [{"module": k[0], "name": k[1], "used_by": sorted(v)} for k, v in sorted(broken.items())]
+        + [{"module": k[0], "attr": k[1], "used_by": sorted(v)} for k, v in sorted(class_attrs.items())
+           if k not in attrs_ok],
     }
 
 

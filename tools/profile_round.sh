@@ -15,7 +15,7 @@ B="python bench.py --steps 10 --warmup 2 --no-cpu-baseline"
 pmc() {   # pmc <name> <lib or -> <counters...>
   name=$1; lib=$2; shift 2
   if [ "$lib" = "-" ]; then env_lib=""; else env_lib="$lib"; fi
-  RTG_LIB=${env_lib:-$PWD/humanoid-real-time-retarget_amd/librtg_hip.so} timeout -s KILL 120 \
+  RTG_ALLOW_MEASUREMENT_BUILD=1 RTG_LIB=${env_lib:-$PWD/humanoid-real-time-retarget_amd/librtg_hip.so} timeout -s KILL 120 \
     rocprofv3 --pmc "$@" -d $out/$name -o $name --output-format csv -- $B > $out/$name.log 2>&1
 }
 timeout -k 10 300 python bench.py > $out/bench.log 2>&1
