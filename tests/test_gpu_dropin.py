@@ -342,3 +342,56 @@ def test_main_retarget_from_global_translation(gpu):
     s = frame_stats(robot.local_rotation.numpy(), g["robot_local_rot"])
     assert s["max"] <= 2e-5 and s["exact_elems"] >= 0.9, s
     assert frame_stats(robot.global_translation.numpy(), g["robot_g_pos"])["max"] <= 2e-5
+
+
+def test_rotation3d_transform3d_full_surface_vs_oracle_and_reference(gpu):
+    """Everything rotation3d / transform3d export beyond the solver path, through the drop-in functions (rtg_quat_op_f32
+    ops 18-31, rtg_quat_as_euler_f64, rtg_quat_between_f32): bit-exact vs the oracle, and vs the reference's own
+    outputs (tests/golden/overlay_extras.npz) exact where no transcendental is involved, within VML's ulps where
+    one is.  CPU tensors in, CPU tensors out, like the reference."""
+    import oracle as orc
+    import poselib.poselib.core.rotation3d as r3
+    import retarget.spatial_transform.transform3d as t3
+    g = golden("overlay_extras")
+    T = torch.from_numpy
+
+    def both(got, o, ref, exact_ref):
+        got = got.numpy() if isinstance(got, torch.Tensor) else np.asarray(got)
+        np.testing.assert_array_equal(got, o)
+        if exact_ref:
+            np.testing.assert_array_equal(got, ref)
+        else:
+            e = np.abs(got.astype(np.float64) - ref)
+            assert np.nanmax(e) <= 2.5e-7, np.nanmax(e)
+
+    a, ax = r3.exp_map_to_angle_axis(T(g["em_e"]))
+    assert a.device.type == "cpu"
+    both(torch.cat([a[:, None], ax], 1), orc.exp_map_to_angle_axis(g["em_e"]), g["exp_map_to_angle_axis"], False)
+    both(r3.exp_map_to_quat(T(g["em_e"])), orc.exp_map_to_quat(g["em_e"]), g["exp_map_to_quat"], False)
+    both(t3.exp_map_to_quat(T(g["em_e"])), orc.exp_map_to_quat(g["em_e"]), g["t3_exp_map_to_quat"], False)
+    both(t3.quat_slerp(T(g["sl_q0"]), T(g["sl_q1"]), T(g["sl_t"])), orc.quat_slerp(g["sl_q0"], g["sl_q1"], g["sl_t"]),
+         g["quat_slerp"], False)
+    qb = np.concatenate([t3.quat_between_two_vecs(T(g["qb_v1"][i:i + 16]), T(g["qb_v2"][i:i + 16])).numpy()
+                         for i in range(0, len(g["qb_v1"]), 16)])   # batch-level identity branch: same chunks
+    np.testing.assert_array_equal(qb, g["quat_between_two_vecs"])
+    both(torch.stack([r3.quat_from_xyz(T(x.copy())) for x in g["qx_xyz"]]), orc.quat_from_xyz(g["qx_xyz"]),
+         g["quat_from_xyz"], True)
+    with pytest.raises(AssertionError):
+        r3.quat_from_xyz(torch.tensor([1.0, 1.0, 1.0]))                        # rotation3d.py:107
+    both(r3.rot_matrix_from_quaternion(T(g["pq_q"])), orc.rot_matrix_from_quaternion(g["pq_q"]),
+         g["rot_matrix_from_quaternion"], True)
+    both(r3.rot_matrix_det(T(g["det_m"])), orc.rot_matrix_det(g["det_m"]), g["rot_matrix_det"], True)
+    for k in ("x", "y", "z", "xy", "xz"):
+        both(getattr(r3, f"project_quat_to_axis_{k}")(T(g["pq_q"])), orc.project_quat_to_axis(g["pq_q"], k),
+             g[f"project_quat_to_axis_{k}"], False)
+    for axis in range(3):
+        both(r3.extract_rotation_along_axis(T(g["pq_q"]), axis), orc.extract_rotation_along_axis(g["pq_q"], axis),
+             g[f"extract_rotation_along_axis_{axis}"], True)
+    for z_up in (True, False):
+        np.testing.assert_array_equal(r3.quat_yaw_rotation(T(g["pq_q"]), z_up).numpy(), g[f"quat_yaw_rotation_{int(z_up)}"])
+    eu = r3.quat_to_eular(T(g["pq_q"][:256]))
+    assert eu.dtype == np.float64
+    np.testing.assert_array_equal(eu, g["quat_to_eular"])
+    np.testing.assert_array_equal(r3.euclidean_to_transform(T(g["eu_m"])).numpy(), g["euclidean_to_transform"])
+    with pytest.raises(RuntimeError):
+        r3.euclidean_inverse(T(g["eu_m"]))                                     # broken in the reference too

@@ -353,3 +353,25 @@ def test_motion_prep_vs_reference():
     np.testing.assert_array_equal(gr[:, other], d["g_rot"][:, other])
     e = np.abs(gr[:, [0, 10]] - d["g_rot"][:, [0, 10]]).reshape(len(gr), -1).max(1)   # per-frame max
     assert e.max() <= 6e-8 and (gr[:, [0, 10]] == d["g_rot"][:, [0, 10]]).mean() >= 0.99, e.max()
+
+
+def test_overlay_extras_oracle_vs_reference():
+    """The rest of the rotation3d / transform3d surface (tests/golden/overlay_extras.npz, the reference run on
+    chunks of 16): exact where the arithmetic has no transcendental, within VML's ulps where it does."""
+    g = golden("overlay_extras")
+    exact = [(orc.quat_between(g["qb_v1"], g["qb_v2"]), g["quat_between_two_vecs"]),
+             (orc.quat_from_xyz(g["qx_xyz"]), g["quat_from_xyz"]),
+             (orc.rot_matrix_from_quaternion(g["pq_q"]), g["rot_matrix_from_quaternion"]),
+             (orc.rot_matrix_det(g["det_m"]), g["rot_matrix_det"]),
+             (orc.quat_to_eular(g["pq_q"][:256]), g["quat_to_eular"])]
+    exact += [(orc.extract_rotation_along_axis(g["pq_q"], a), g[f"extract_rotation_along_axis_{a}"]) for a in range(3)]
+    for got, ref in exact:
+        np.testing.assert_array_equal(got, ref)
+    ulps = [(orc.exp_map_to_angle_axis(g["em_e"]), g["exp_map_to_angle_axis"]),
+            (orc.exp_map_to_quat(g["em_e"]), g["exp_map_to_quat"]),
+            (orc.exp_map_to_quat(g["em_e"]), g["t3_exp_map_to_quat"]),
+            (orc.quat_slerp(g["sl_q0"], g["sl_q1"], g["sl_t"]), g["quat_slerp"])]
+    ulps += [(orc.project_quat_to_axis(g["pq_q"], k), g[f"project_quat_to_axis_{k}"]) for k in ("x", "y", "z", "xy", "xz")]
+    for got, ref in ulps:
+        s = frame_stats(got, ref)
+        assert s["max"] <= 2.5e-7 and s["exact_elems"] >= 0.88, s

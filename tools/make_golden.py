@@ -405,6 +405,73 @@ def gen_expmap(ref, torch):
     return out
 
 
+def gen_overlay_extras(ref, torch):
+    """The rest of the rotation3d / transform3d surface the drop-in now exports (rotation3d.py:101-108, 243-261,
+    338-350, 398-427, 465-473, 479-556, 629-661; transform3d.py:8-21, 146-174), called on chunks of 16 like the
+    per-frame callers (torch takes glibc's scalar atan2f below 32 elements).  Edge cases: zero / tiny / > pi
+    exp-maps, slerp with cos < 0, t in {0, 1}, nearly equal and identical quaternions, parallel and opposite vectors."""
+    r3, t3 = ref.rotation3d, ref.transform3d
+    rng = np.random.default_rng(29)
+    out = {}
+    n = 1024
+    e = (rng.standard_normal((n, 3)) * rng.uniform(0, 4, (n, 1))).astype(np.float32)
+    e[:8] = 0.0
+    e[8:16] *= np.float32(1e-6)
+    e[16:24] = rng.standard_normal((8, 3)).astype(np.float32) * np.float32(3e-6)
+    e[24:32] *= np.float32(3.0)                                   # |e| > pi: normalize_angle wraps
+    out["em_e"] = e
+    chunks = [torch.from_numpy(e[i:i + 16]) for i in range(0, n, 16)]
+    aa = [r3.exp_map_to_angle_axis(c) for c in chunks]
+    out["exp_map_to_angle_axis"] = np.concatenate([np.concatenate([t2n(a)[:, None], t2n(x)], 1) for a, x in aa])
+    out["exp_map_to_quat"] = np.concatenate([t2n(r3.exp_map_to_quat(c)) for c in chunks])
+    out["t3_exp_map_to_quat"] = np.concatenate([t2n(t3.exp_map_to_quat(c)) for c in chunks])
+    q0, q1 = _rand_quats(rng, n), _rand_quats(rng, n)
+    q1[: n // 4] *= -1.0                                          # cos(half) < 0: the shortest-arc flip
+    q1[n // 4: n // 4 + 16] = q0[n // 4: n // 4 + 16]              # identical: |cos| >= 1
+    q1[n // 4 + 16: n // 4 + 32] = (q0[n // 4 + 16: n // 4 + 32] + np.float32(1e-4)).astype(np.float32)
+    t = rng.uniform(0, 1, (n, 1)).astype(np.float32)
+    t[:4] = 0.0
+    t[4:8] = 1.0
+    out["sl_q0"], out["sl_q1"], out["sl_t"] = q0, q1, t
+    out["quat_slerp"] = np.concatenate([t2n(t3.quat_slerp(torch.from_numpy(q0[i:i + 16]), torch.from_numpy(q1[i:i + 16]),
+                                                          torch.from_numpy(t[i:i + 16]))) for i in range(0, n, 16)])
+    v1 = rng.standard_normal((n, 3)).astype(np.float32)
+    v2 = rng.standard_normal((n, 3)).astype(np.float32)
+    v2[:8] = v1[:8] * np.float32(2.0)                            # parallel
+    v2[8:16] = -v1[8:16]                                          # opposite
+    out["qb_v1"], out["qb_v2"] = v1, v2
+    out["quat_between_two_vecs"] = np.concatenate([t2n(t3.quat_between_two_vecs(torch.from_numpy(v1[i:i + 16]),
+                                                                                torch.from_numpy(v2[i:i + 16])))
+                                                   for i in range(0, n, 16)])
+    xyz = (rng.standard_normal((64, 3)) * 0.3).astype(np.float32)
+    xyz /= np.maximum(1.0, np.linalg.norm(xyz, axis=1, keepdims=True) * 1.01).astype(np.float32)
+    out["qx_xyz"] = xyz
+    out["quat_from_xyz"] = np.stack([t2n(r3.quat_from_xyz(torch.from_numpy(x.copy()))) for x in xyz])
+    q = _rand_quats(rng, n)
+    q[: n // 2] *= rng.uniform(0.5, 2.0, (n // 2, 1)).astype(np.float32)   # not unit: rot_matrix_from_quaternion's 2/|q|^2
+    out["pq_q"] = q
+    qc = [torch.from_numpy(q[i:i + 16]) for i in range(0, n, 16)]
+    out["rot_matrix_from_quaternion"] = np.concatenate([t2n(r3.rot_matrix_from_quaternion(c)) for c in qc])
+    m = rng.standard_normal((n, 3, 3)).astype(np.float32)
+    out["det_m"] = m
+    out["rot_matrix_det"] = np.concatenate([t2n(r3.rot_matrix_det(torch.from_numpy(m[i:i + 16]))) for i in range(0, n, 16)])
+    for k in ("x", "y", "z", "xy", "xz"):
+        out[f"project_quat_to_axis_{k}"] = np.concatenate([t2n(getattr(r3, f"project_quat_to_axis_{k}")(c)) for c in qc])
+    for ax in range(3):
+        out[f"extract_rotation_along_axis_{ax}"] = np.concatenate([t2n(r3.extract_rotation_along_axis(c, ax)) for c in qc])
+    for z_up in (True, False):
+        out[f"quat_yaw_rotation_{int(z_up)}"] = np.concatenate([t2n(r3.quat_yaw_rotation(c, z_up)) for c in qc])
+    out["quat_to_eular"] = np.stack([r3.quat_to_eular(torch.from_numpy(x.copy())) for x in q[:256]]).astype(np.float64)
+    eu = np.zeros((64, 4, 4), np.float32)
+    for i in range(64):
+        eu[i, :3, :3] = rng.standard_normal((3, 3))
+        eu[i, :3, 3] = rng.standard_normal(3)
+        eu[i, 3, 3] = 1.0
+    out["eu_m"] = eu
+    out["euclidean_to_transform"] = t2n(r3.euclidean_to_transform(torch.from_numpy(eu)))
+    return out
+
+
 def gen_kat(ref, torch):
     """retarget/rotation_test.py:95-152 restated as data: arm segments from known joint angles."""
     r3 = ref.rotation3d
@@ -457,6 +524,7 @@ def main() -> None:
         "motion_prep": lambda: gen_motion_prep(ref, torch),
         "expmap": lambda: gen_expmap(ref, torch),
         "main_retarget": lambda: gen_main_retarget(ref, torch),
+        "overlay_extras": lambda: gen_overlay_extras(ref, torch),
     }
     only = set(sys.argv[1:])
     for name, fn in jobs.items():
