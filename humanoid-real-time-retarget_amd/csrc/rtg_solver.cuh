@@ -527,6 +527,25 @@ __global__ __launch_bounds__(256, RTG_SIDES_WAVES) void k_solve_sides(SolverCons
     }
 #endif
     __shared__ float4 sarm[RTG_SIDES_REBALANCE ? kSideFrames : 1];   // the left arm chain, right wave -> left wave
+#if RTG_EXP_TIMESTAMPS
+    // measurement knob: lane 0 of each wave of every 8th block records the 100 MHz wall clock at the phase
+    // boundaries into the body_rot buffer (tools/side_phases.py): 16 slots per wave, 4 waves per block
+    float *const tsb = body_rot;
+    body_rot = nullptr;
+    auto TS = [&](int k) {
+        if (tsb && (blockIdx.x & 7) == 0 && (threadIdx.x & 63) == 0) {
+            const uint64_t t = wall_clock64();
+            uint32_t *o = reinterpret_cast<uint32_t *>(tsb) + 2 * (((blockIdx.x >> 3) * 4 + w) * 16 + k);
+            o[0] = (uint32_t)t;
+            o[1] = (uint32_t)(t >> 32);
+        }
+    };
+#else
+    auto TS = [](int) {};
+#endif
+    auto hook1 = [&](int k) { TS(1 + k); };    // 1: first fit's A formed (its points loaded), 2: its SVD + R done
+    auto hook2 = [&](int k) { TS(10 + k); };   // 10 / 11: the same for the left wave's second fit
+    TS(0);
     if (KIND == RTG_SOLVER_FULL_BODY_POS && RTG_SIDES_REBALANCE) {
         // Balanced FULL_BODY_POS: left wave = torso fit, then the left wrist fit, then the left Euler split /
         // gripper; right wave = the right wrist fit, then BOTH arm chains (each needs only R10), then the right
@@ -536,15 +555,17 @@ __global__ __launch_bounds__(256, RTG_SIDES_WAVES) void k_solve_sides(SolverCons
         ArmPts apL{}, apR{};
         if (live) {
             if (!side) {
-                R10 = fbp_torso(C, b);
+                R10 = fbp_torso(C, b, hook1);
                 storso[r] = make_float4(R10.x, R10.y, R10.z, R10.w);
             } else {
                 apL = load_arm<0>(b);
                 apR = load_arm<1>(b);
-                W = fbp_wrist_fit<1>(C, view(in2, 60));
+                W = fbp_wrist_fit<1>(C, view(in2, 60), hook1);
             }
         }
+        TS(3);
         __syncthreads();
+        TS(4);
         Q chain = qident();
         if (live) {
             if (side) {
@@ -555,10 +576,12 @@ __global__ __launch_bounds__(256, RTG_SIDES_WAVES) void k_solve_sides(SolverCons
                 chain = fbp_arm<1>(C, apR, R10, E);
             } else {
                 emit_fixed_links(E);
-                W = fbp_wrist_fit<0>(C, view(in1, 60));
+                W = fbp_wrist_fit<0>(C, view(in1, 60), hook2);
             }
         }
+        TS(5);
         __syncthreads();
+        TS(6);
         if (live) {
             float *brow = body_rot ? body_rot + f * 236 : nullptr;
             if (side) {
@@ -568,6 +591,7 @@ __global__ __launch_bounds__(256, RTG_SIDES_WAVES) void k_solve_sides(SolverCons
                 fbp_side_after_arm<PRECISE, 0>(C, load_tips(view(in1, 60)), R10, Q{c.x, c.y, c.z, c.w}, W, E, brow);
             }
         }
+        TS(7);
     } else if (KIND == RTG_SOLVER_FULL_BODY_POS || KIND == RTG_SOLVER_UPPER_BODY) {
         // The torso fit is shared by both sides: the left wave fits it while the right wave fits its own hand
         // (FULL_BODY_POS; nothing to overlap for UPPER_BODY), then one block barrier hands R10 over LDS.
@@ -632,7 +656,9 @@ __global__ __launch_bounds__(256, RTG_SIDES_WAVES) void k_solve_sides(SolverCons
         static_assert(NL >= 7 && NL <= 11, "RTG_SIDES_FIN_LEFT must keep each wave's wrist slots on that wave");
         E.finalize(side ? NL : 0, side ? 14 - NL : NL);
     }
+    TS(8);
     __syncthreads();
+    TS(9);
     const int64_t nrows = (B - f0) < kSideFrames ? (B - f0) : kSideFrames;
     const int nvals = (int)nrows * 30;
     float *dst = dof + f0 * 30;
@@ -646,6 +672,7 @@ __global__ __launch_bounds__(256, RTG_SIDES_WAVES) void k_solve_sides(SolverCons
         *reinterpret_cast<float4 *>(dst + i) = make_float4(at(i), at(i + 1), at(i + 2), at(i + 3));
     }
     for (int i = (nvec << 2) + threadIdx.x; i < nvals; i += 256) dst[i] = at(i);
+    TS(12);
 }
 
 // ----------------------------------------------------------------------------

@@ -391,7 +391,10 @@ def test_rotation3d_transform3d_full_surface_vs_oracle_and_reference(gpu):
         np.testing.assert_array_equal(r3.quat_yaw_rotation(T(g["pq_q"]), z_up).numpy(), g[f"quat_yaw_rotation_{int(z_up)}"])
     eu = r3.quat_to_eular(T(g["pq_q"][:256]))
     assert eu.dtype == np.float64
-    np.testing.assert_array_equal(eu, g["quat_to_eular"])
+    # float64 out: the device's f64 atan2 / hypot (OCML) are within a few ulp of glibc's, which scipy and the
+    # oracle use -- exact agreement is not claimed here (the solver path rounds these angles to f32 first)
+    np.testing.assert_allclose(eu, g["quat_to_eular"], rtol=1e-13, atol=1e-12)
+    np.testing.assert_allclose(eu, orc.quat_to_eular(g["pq_q"][:256]), rtol=1e-13, atol=1e-12)
     np.testing.assert_array_equal(r3.euclidean_to_transform(T(g["eu_m"])).numpy(), g["euclidean_to_transform"])
     with pytest.raises(RuntimeError):
         r3.euclidean_inverse(T(g["eu_m"]))                                     # broken in the reference too
