@@ -10,6 +10,9 @@
 #ifndef RTG_SIDES_FIN_LEFT
 #define RTG_SIDES_FIN_LEFT 7    // exp-map slots (of 14) the left wave reads out in the balanced kernel (7, 8, 9: within noise)
 #endif
+#ifndef RTG_SIDES_FLAGS
+#define RTG_SIDES_FLAGS 1   // balanced FULL_BODY_POS side kernel: per-tile LDS flags instead of the two block barriers
+#endif
 #ifndef RTG_SIDES_WAVES
 #define RTG_SIDES_WAVES 1   // min waves per SIMD for the side kernel (1: the compiler picks; measured best)
 #endif

@@ -494,6 +494,24 @@ RTG_DEV void solve_body_rot_side(const SolverConsts &C, const View &g, const Emi
     E.row[D0] = 0.0f; E.row[D0 + 1] = 0.0f;
 }
 
+// A release is per lane, but the hand-over is per wave: the lanes that skipped the work (frames past B) must not
+// raise the flag on their own -- the compiler may run their path first (it did: the flag went up before the live
+// lanes' writes).  So the flag goes up after a convergent ballot, where the whole wave has rejoined and every
+// lane's LDS writes have issued, from one lane, with a release (s_waitcnt lgkmcnt(0) before the store).
+RTG_DEV void lds_signal(int *flag)
+{
+    const uint64_t joined = __builtin_amdgcn_ballot_w64(true);
+    if (joined != 0 && (threadIdx.x & 63) == (unsigned)__builtin_ctzll(joined))
+        __hip_atomic_store(flag, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+RTG_DEV void lds_wait(int *flag)
+{
+    for (int it = 0; it < (1 << 22); ++it) {   // ~0.1 s at s_sleep 1: a bound every wave reaches
+        if (__hip_atomic_load(flag, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP)) return;
+        __builtin_amdgcn_s_sleep(1);
+    }
+}
+
 template <int KIND, bool PRECISE, bool SOA>
 __global__ __launch_bounds__(256, RTG_SIDES_WAVES) void k_solve_sides(SolverConsts C, const float *__restrict__ in0,
                                                      const float *__restrict__ in1, const float *__restrict__ in2,
@@ -527,6 +545,13 @@ __global__ __launch_bounds__(256, RTG_SIDES_WAVES) void k_solve_sides(SolverCons
     }
 #endif
     __shared__ float4 sarm[RTG_SIDES_REBALANCE ? kSideFrames : 1];   // the left arm chain, right wave -> left wave
+#if RTG_SIDES_FLAGS
+    __shared__ int sflag[2][2];   // per tile: [0] R10 ready (left -> right), [1] left chain ready (right -> left)
+    if (KIND == RTG_SOLVER_FULL_BODY_POS && RTG_SIDES_REBALANCE) {
+        if (threadIdx.x < 4) (&sflag[0][0])[threadIdx.x] = 0;
+        __syncthreads();
+    }
+#endif
 #if RTG_EXP_TIMESTAMPS
     // measurement knob: lane 0 of each wave of every 8th block records the 100 MHz wall clock at the phase
     // boundaries into the body_rot buffer (tools/side_phases.py): 16 slots per wave, 4 waves per block
@@ -550,9 +575,16 @@ __global__ __launch_bounds__(256, RTG_SIDES_WAVES) void k_solve_sides(SolverCons
         // Balanced FULL_BODY_POS: left wave = torso fit, then the left wrist fit, then the left Euler split /
         // gripper; right wave = the right wrist fit, then BOTH arm chains (each needs only R10), then the right
         // Euler split / gripper.  Two barriers hand R10 (left -> right) and the left chain (right -> left) over LDS.
+        // RTG_SIDES_FLAGS: the two hand-overs are per-tile LDS flags instead of block barriers, so each wave waits
+        // only for what it reads -- the right wave for R10, the left wave for the left chain -- and the left wave
+        // starts its wrist fit as soon as its torso fit is out (it idled 8-10 us at the first barrier behind the
+        // right wave's wrist fit: tools/side_phases.py, profiles/r03/side_phases_base.json).
         const auto b = view(in0, 63);
         Q R10 = qident(), W = qident();
         ArmPts apL{}, apR{};
+#if RTG_SIDES_FLAGS
+        int *const fl = sflag[w >> 1];
+#endif
         if (live) {
             if (!side) {
                 R10 = fbp_torso(C, b, hook1);
@@ -564,23 +596,35 @@ __global__ __launch_bounds__(256, RTG_SIDES_WAVES) void k_solve_sides(SolverCons
             }
         }
         TS(3);
+#if RTG_SIDES_FLAGS
+        if (!side) lds_signal(&fl[0]);   // R10 of this tile is in storso
+        else lds_wait(&fl[0]);
+#else
         __syncthreads();
+#endif
         TS(4);
         Q chain = qident();
-        if (live) {
-            if (side) {
+        if (side) {
+            if (live) {
                 const float4 t = storso[r];
                 R10 = Q{t.x, t.y, t.z, t.w};
                 const Q cl = fbp_arm<0>(C, apL, R10, E);
                 sarm[r] = make_float4(cl.x, cl.y, cl.z, cl.w);
-                chain = fbp_arm<1>(C, apR, R10, E);
-            } else {
-                emit_fixed_links(E);
-                W = fbp_wrist_fit<0>(C, view(in1, 60), hook2);
             }
+#if RTG_SIDES_FLAGS
+            lds_signal(&fl[1]);          // the left chain and its exp-map slots 0-3 are in LDS
+#endif
+            if (live) chain = fbp_arm<1>(C, apR, R10, E);
+        } else if (live) {
+            emit_fixed_links(E);
+            W = fbp_wrist_fit<0>(C, view(in1, 60), hook2);
         }
         TS(5);
+#if RTG_SIDES_FLAGS
+        if (!side) lds_wait(&fl[1]);
+#else
         __syncthreads();
+#endif
         TS(6);
         if (live) {
             float *brow = body_rot ? body_rot + f * 236 : nullptr;
@@ -654,6 +698,10 @@ __global__ __launch_bounds__(256, RTG_SIDES_WAVES) void k_solve_sides(SolverCons
         // wrote itself or the arm slots: NL in [7, 11] (static_assert below).
         constexpr int NL = (KIND == RTG_SOLVER_FULL_BODY_POS && RTG_SIDES_REBALANCE) ? RTG_SIDES_FIN_LEFT : 7;
         static_assert(NL >= 7 && NL <= 11, "RTG_SIDES_FIN_LEFT must keep each wave's wrist slots on that wave");
+        // with flags the left wave has only the left chain's slots 0-3 from the right wave (the right arm's 7-10 are
+        // written after the flag): it reads exactly [0, 7)
+        static_assert(!(KIND == RTG_SOLVER_FULL_BODY_POS && RTG_SIDES_REBALANCE && RTG_SIDES_FLAGS) || NL == 7,
+                      "RTG_SIDES_FLAGS needs RTG_SIDES_FIN_LEFT == 7");
         E.finalize(side ? NL : 0, side ? 14 - NL : NL);
     }
     TS(8);
@@ -784,23 +832,6 @@ __global__ __launch_bounds__(192) void k_fbp_latency(SolverConsts C, const float
 // cap.  Every value is computed by the same device function from the same operands as in k_fbp_latency /
 // k_solve_sides: the same bits (test_solver_batch_invariance covers both sizes).
 // ----------------------------------------------------------------------------
-// A release is per lane, but the hand-over is per wave: the lanes that skipped the work (frames past B) must not
-// raise the flag on their own -- the compiler may run their path first (it did: the flag went up before the live
-// lanes' writes).  So the flag goes up after a convergent ballot, where the whole wave has rejoined and every
-// lane's LDS writes have issued, from one lane, with a release (s_waitcnt lgkmcnt(0) before the store).
-RTG_DEV void lds_signal(int *flag)
-{
-    const uint64_t joined = __builtin_amdgcn_ballot_w64(true);
-    if (joined != 0 && (threadIdx.x & 63) == (unsigned)__builtin_ctzll(joined))
-        __hip_atomic_store(flag, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
-}
-RTG_DEV void lds_wait(int *flag)
-{
-    for (int it = 0; it < (1 << 22); ++it) {   // ~0.1 s at s_sleep 1: a bound every wave reaches
-        if (__hip_atomic_load(flag, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP)) return;
-        __builtin_amdgcn_s_sleep(1);
-    }
-}
 
 // one 64-frame tile (frames f0..) by the 320 threads of a workgroup; shared by the batched latency kernel and the
 // per-frame server (k_frame_server)

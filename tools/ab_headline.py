@@ -1,0 +1,73 @@
+"""A/B of the headline solve (FULL_BODY_POS, precise gripper, B = 262144, SoA and AoS inputs from the device
+producer, a ring of input sets over 2 x 256 MiB) across library builds, interleaved so box drift hits every build
+alike.  Each build runs in its own process (RTG_LIB); the DOFs of every build are hashed and must match the first.
+
+  python tools/ab_headline.py base=humanoid-real-time-retarget_amd/librtg_hip.so v=.../variants/v.so [--rounds 3]
+"""
+from __future__ import annotations
+
+import hashlib
+import json
+import os
+import subprocess
+import sys
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+CHILD = r"""
+import hashlib, json, os, sys, numpy as np, torch
+sys.path.insert(0, os.path.join(sys.argv[1], "humanoid-real-time-retarget_amd"))
+from rtg import _lib, assets, ops
+from rtg.runtime import Solver, Topology
+zp = np.load(os.path.join(sys.argv[1], "tests", "golden", "zero_pose.npz"))
+S = Solver(_lib.SOLVER_FULL_BODY_POS, zp["vtrdyn_full_local_t"], zp["vtrdyn_full_global_t"], assets.parents("vtrdyn_full"), True)
+T = Topology(assets.parents("vtrdyn_full"), assets.local_translation("vtrdyn_full"), assets.tree_quat("vtrdyn_full"))
+B, out = 262144, {}
+for layout in ("soa", "aos"):
+    sets = [ops.synth_full_body(T, B, seed=1234, frame_offset=r * B, layout=layout) for r in range(3)]
+    dof = torch.empty((B, 30), device="cuda")
+    for i in range(5):
+        S.retarget(list(sets[i % 3]), out_dof=dof, layout=layout)
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for i in range(60):
+        S.retarget(list(sets[i % 3]), out_dof=dof, layout=layout)
+    e1.record(); e1.synchronize()
+    S.retarget(list(sets[0]), out_dof=dof, layout=layout)
+    h = hashlib.sha1(dof.cpu().numpy().tobytes()).hexdigest()[:16]
+    out[layout] = {"kernel_us": e0.elapsed_time(e1) / 60 * 1e3, "dof_sha": h}
+print(json.dumps(out))
+"""
+
+
+def main():
+    args = [a for a in sys.argv[1:] if not a.startswith("--")]
+    rounds = 3
+    if "--rounds" in sys.argv:
+        rounds = int(sys.argv[sys.argv.index("--rounds") + 1])
+        args = [a for a in args if a != str(rounds)]
+    builds = [a.split("=", 1) for a in args]
+    res = {n: [] for n, _ in builds}
+    for _ in range(rounds):
+        for name, lib in builds:
+            env = dict(os.environ, RTG_LIB=os.path.abspath(lib), RTG_ALLOW_MEASUREMENT_BUILD="1")
+            r = subprocess.run([sys.executable, "-c", CHILD, REPO], env=env, capture_output=True, text=True,
+                               timeout=300)
+            if r.returncode != 0:
+                print(json.dumps({"build": name, "error": r.stderr[-1500:]}), flush=True)
+                sys.exit(1)
+            res[name].append(json.loads(r.stdout.strip().splitlines()[-1]))
+            print(json.dumps({"build": name, **res[name][-1]}), flush=True)
+    ref = res[builds[0][0]][0]
+    summary = {}
+    for name, runs in res.items():
+        summary[name] = {lay: {"kernel_us_min": min(r[lay]["kernel_us"] for r in runs),
+                               "kernel_us_med": sorted(r[lay]["kernel_us"] for r in runs)[len(runs) // 2],
+                               "bits_match_first_build": all(r[lay]["dof_sha"] == ref[lay]["dof_sha"] for r in runs)}
+                         for lay in ("soa", "aos")}
+    print(json.dumps({"summary": summary}), flush=True)
+
+
+if __name__ == "__main__":
+    main()
