@@ -521,6 +521,7 @@ __global__ __launch_bounds__(256, RTG_SIDES_WAVES) void k_solve_sides(SolverCons
 {
     __shared__ float sdof[kSideFrames * kDofStride];
     __shared__ float4 storso[kSideFrames];   // the tile's torso fit, handed from the left wave to the right one
+    __shared__ float4 sarm_own[(RTG_SIDES_REBALANCE && !RTG_SIDES_FLAGS) ? kSideFrames : 1];
     __shared__ float2 sst[2 * 14 * 64];      // exp-map stash, [tile][slot][lane]
     const int w = threadIdx.x >> 6, side = w & 1;
     const int r = (w >> 1) * 64 + (threadIdx.x & 63);   // tile row
@@ -544,7 +545,10 @@ __global__ __launch_bounds__(256, RTG_SIDES_WAVES) void k_solve_sides(SolverCons
         }
     }
 #endif
-    __shared__ float4 sarm[RTG_SIDES_REBALANCE ? kSideFrames : 1];   // the left arm chain, right wave -> left wave
+    // the left arm chain, right wave -> left wave.  With flags it shares storso: the right wave reads its R10 from
+    // storso[r] before it writes its chain there (same lane, program order), and the left wave reads the chain after
+    // the flag -- 2 KiB less LDS, 32.3 KiB per block, so 5 blocks (5 waves / SIMD) fit a CU's 160 KiB
+    float4 *const sarm = RTG_SIDES_FLAGS ? storso : sarm_own;
 #if RTG_SIDES_FLAGS
     __shared__ int sflag[2][2];   // per tile: [0] R10 ready (left -> right), [1] left chain ready (right -> left)
     if (KIND == RTG_SOLVER_FULL_BODY_POS && RTG_SIDES_REBALANCE) {
