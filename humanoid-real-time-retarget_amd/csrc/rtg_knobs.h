@@ -12,6 +12,7 @@
 #endif
 #ifndef RTG_SIDES_FLAGS
 #define RTG_SIDES_FLAGS 1   // balanced FULL_BODY_POS side kernel: per-tile LDS flags instead of the two block barriers
+                            // (2: right arm before the hand-over, left wave takes more read-out -- measured 2-4% slower)
 #endif
 #ifndef RTG_SIDES_WAVES
 #define RTG_SIDES_WAVES 1   // min waves per SIMD for the side kernel (1: the compiler picks; measured best)
@@ -66,6 +67,9 @@
 // ---- used by rtg_math.cuh
 #ifndef RTG_FAST_EXACT
 #define RTG_FAST_EXACT 1
+#endif
+#ifndef RTG_FAST_NORM
+#define RTG_FAST_NORM 1   // sqrt_clamp_rcp: one v_rsq_f64 + Goldschmidt / Newton for the norm and 1/norm (else cr_sqrt + rcp64)
 #endif
 #ifndef RTG_EXP_NO_TABLE
 #define RTG_EXP_NO_TABLE 0

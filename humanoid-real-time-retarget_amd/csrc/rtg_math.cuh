@@ -95,8 +95,46 @@ RTG_DEV float mulr(float a, const Rcp &r)
     if (__builtin_expect(__builtin_fabs(p) < 0x1p-126 && p != 0.0, 0)) q = a / r.n;
     return q;
 }
-RTG_DEV float tsign(float v) { return v > 0.0f ? 1.0f : (v < 0.0f ? -1.0f : 0.0f); }
 RTG_DEV float clamp_lo(float v, float lo) { return v < lo ? lo : v; }          // NaN passes through
+// n = max(RN32(sqrt(s)), lo) and its reciprocal for mulr -- the normalisation step every quat_unit / quat_normalize /
+// axis normalisation takes (clamp(norm, 1e-9), then k divisions by it).  cr_sqrt + rcp64 issue three f64
+// transcendentals (v_sqrt_f64, v_rcp_f64 in the sqrt correction, v_rcp_f64 for 1/n) on the dependent chain; this
+// form issues ONE (v_rsq_f64): two coupled Goldschmidt steps refine sqrt(s) and 1/(2 sqrt(s)) together, the f32
+// rounding of the first gives n, and two Newton steps from 2 * the second give 1/n.  s = 0, +inf, NaN, negative
+// and a clamped n take the cr_sqrt + rcp64 path (rare, divergent).  tools/check_fastmath.hip [4] checks on the
+// device that (n, r) are bitwise those of the cr_sqrt + rcp64 path for every f32 s (both lo used here).
+struct NormRcp {
+    float n;
+    Rcp r;
+};
+RTG_DEV NormRcp sqrt_clamp_rcp(float s, float lo)
+{
+#if RTG_FAST_NORM
+    const double d = (double)s;
+    if (__builtin_expect(d > 0.0 && d < __builtin_inf(), 1)) {
+        const double y = __builtin_amdgcn_rsq(d);
+        double g = d * y, h = 0.5 * y;
+        double e = __builtin_fma(-g, h, 0.5);
+        g = __builtin_fma(g, e, g);
+        h = __builtin_fma(h, e, h);
+        e = __builtin_fma(-g, h, 0.5);
+        g = __builtin_fma(g, e, g);
+        h = __builtin_fma(h, e, h);
+        const float n = (float)g;
+        if (__builtin_expect(n >= lo, 1)) {
+            const double dn = (double)n, r0 = h + h;
+            const double e0 = __builtin_fma(-dn, r0, 1.0);
+            const double r1 = __builtin_fma(r0, e0, r0);
+            const double e1 = __builtin_fma(-dn, r1, 1.0);
+            return NormRcp{n, Rcp{__builtin_fma(r1, e1, r1), n}};
+        }
+    }
+#endif
+    const float n = clamp_lo(cr_sqrt(s), lo);
+    return NormRcp{n, rcp64(n)};
+}
+
+RTG_DEV float tsign(float v) { return v > 0.0f ? 1.0f : (v < 0.0f ? -1.0f : 0.0f); }
 RTG_DEV float clamp_lohi(float v, float lo, float hi) { return v < lo ? lo : (v > hi ? hi : v); }
 
 // glibc 2.35 float atanf (fdlibm s_atanf.c algorithm, decimal constants)
@@ -205,25 +243,21 @@ RTG_DEV Q qnormalize(Q q)  // quat_unit(quat_pos(q)) :30-56,92-98
 {
     const float f = 1.0f - 2.0f * (q.w < 0.0f ? 1.0f : 0.0f);
     q.x = f * q.x; q.y = f * q.y; q.z = f * q.z; q.w = f * q.w;
-    float n = cr_sqrt(((q.x * q.x + q.y * q.y) + q.z * q.z) + q.w * q.w);
-    n = clamp_lo(n, 1e-9f);
-    const Rcp r = rcp64(n);
+    const Rcp r = sqrt_clamp_rcp(((q.x * q.x + q.y * q.y) + q.z * q.z) + q.w * q.w, 1e-9f).r;
     return Q{mulr(q.x, r), mulr(q.y, r), mulr(q.z, r), mulr(q.w, r)};
 }
 RTG_DEV Q qmul_norm(Q a, Q b) { return qnormalize(qmul(a, b)); }
 RTG_DEV float qabs(Q q) { return cr_sqrt(((q.x * q.x + q.y * q.y) + q.z * q.z) + q.w * q.w); }   // :41-47
 RTG_DEV Q qunit(Q q)                                                                                 // :50-56
 {
-    const float n = clamp_lo(qabs(q), 1e-9f);
-    const Rcp r = rcp64(n);
+    const Rcp r = sqrt_clamp_rcp(((q.x * q.x + q.y * q.y) + q.z * q.z) + q.w * q.w, 1e-9f).r;
     return Q{mulr(q.x, r), mulr(q.y, r), mulr(q.z, r), mulr(q.w, r)};
 }
 // quat_angle_axis (:230-240): angle = acos(clamp(2 w^2 - 1)), axis = xyz / max(|xyz|, 1e-9)
 RTG_DEV Q qangle_axis_abs(Q q)
 {
     const float s = clamp_lohi(2.0f * (q.w * q.w) - 1.0f, -1.0f, 1.0f);
-    const float n = clamp_lo(cr_sqrt((q.x * q.x + q.y * q.y) + q.z * q.z), 1e-9f);
-    const Rcp r = rcp64(n);
+    const Rcp r = sqrt_clamp_rcp((q.x * q.x + q.y * q.y) + q.z * q.z, 1e-9f).r;
     return Q{cr_acos(s), mulr(q.x, r), mulr(q.y, r), mulr(q.z, r)};
 }
 
@@ -237,9 +271,8 @@ RTG_DEV Q qfrom_angle_axis(float angle, V axis)  // :122-143
 {
     const float theta = angle / 2.0f;
     // axis.norm(p=2, dim=-1) of a 3-vector: torch's fma chain (measured: 100 % vs 90 % for the plain left fold)
-    float n = cr_sqrt(__builtin_fmaf(axis.z, axis.z, __builtin_fmaf(axis.y, axis.y, axis.x * axis.x)));
-    n = clamp_lo(n, 1e-9f);
-    const Rcp r = rcp64(n);
+    const Rcp r = sqrt_clamp_rcp(__builtin_fmaf(axis.z, axis.z, __builtin_fmaf(axis.y, axis.y, axis.x * axis.x)),
+                                 1e-9f).r;
     const float ax = mulr(axis.x, r), ay = mulr(axis.y, r), az = mulr(axis.z, r);
     const SC t = cr_sincos((double)theta);
     const float s = t.s, c = t.c;
@@ -406,6 +439,12 @@ RTG_DEV V vdiv(V a, float s)
     return V{mulr(a.x, r), mulr(a.y, r), mulr(a.z, r)};
 }
 RTG_DEV V vmul(V a, float s) { return V{s * a.x, s * a.y, s * a.z}; }
+// v / torch.linalg.norm(v): vdiv(v, lnorm3(v)) through one sqrt_clamp_rcp (lo = 0 clamps nothing)
+RTG_DEV V vunit(V a)
+{
+    const Rcp r = sqrt_clamp_rcp(__builtin_fmaf(a.z, a.z, __builtin_fmaf(a.y, a.y, a.x * a.x)), 0.0f).r;
+    return V{mulr(a.x, r), mulr(a.y, r), mulr(a.z, r)};
+}
 
 RTG_DEV V proj_in_plane(V v, V n)  // :61-75
 {
@@ -415,9 +454,9 @@ RTG_DEV V proj_in_plane(V v, V n)  // :61-75
 
 RTG_DEV float radians_between(V v1, V v2, V n)  // :77-100
 {
-    v1 = vdiv(v1, lnorm3(v1));
-    v2 = vdiv(v2, lnorm3(v2));
-    const V nrm = vdiv(n, lnorm3(n));
+    v1 = vunit(v1);
+    v2 = vunit(v2);
+    const V nrm = vunit(n);
     const float c = clamp_lohi(dot3(v1, v2), -1.0f, 1.0f);
     return cr_acos(c) * tsign(dot3(nrm, cross3(v1, v2)));
 }
@@ -425,7 +464,7 @@ RTG_DEV float radians_between(V v1, V v2, V n)  // :77-100
 // identity (lnorm3 = sqrt(1) = 1, x * RN(1/1) = x), so only v2 is normalised -- the same bits, 2/3 fewer divides.
 RTG_DEV float radians_between_axes(V v1, V v2, V n)
 {
-    v2 = vdiv(v2, lnorm3(v2));
+    v2 = vunit(v2);
     const float c = clamp_lohi(dot3(v1, v2), -1.0f, 1.0f);
     return cr_acos(c) * tsign(dot3(n, cross3(v1, v2)));
 }
@@ -437,8 +476,9 @@ RTG_DEV float radians_between_axes(V v1, V v2, V n)
 // exp_map_to_angle_axis (rotation3d.py:629-646) as [angle, axis]
 RTG_DEV Q exp_map_angle_axis(V e)
 {
-    const float n = lnorm3(e);
-    const Rcp r = rcp64(n);
+    const NormRcp nr = sqrt_clamp_rcp(__builtin_fmaf(e.z, e.z, __builtin_fmaf(e.y, e.y, e.x * e.x)), 0.0f);
+    const float n = nr.n;
+    const Rcp r = nr.r;
     const float a = normalize_angle(n);
     const bool mask = fabsf(a) > 1e-5f;
     return Q{mask ? a : 0.0f, mask ? mulr(e.x, r) : 0.0f, mask ? mulr(e.y, r) : 0.0f, mask ? mulr(e.z, r) : 1.0f};

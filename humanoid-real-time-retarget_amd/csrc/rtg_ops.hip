@@ -638,7 +638,7 @@ hipError_t launch_synth_full_body(const TopoView &T, uint64_t seed, int64_t off,
 extern "C" const char *rtg_build_info(void)
 {
     return "{\"abi\":" RTG_STR(RTG_ABI_VERSION) ",\"arch\":\"gfx950\",\"knobs\":{"
-        RTG_KNOB(RTG_FAST_EXACT) RTG_KNOB(RTG_SVD_DIV) RTG_KNOB(RTG_SVD_SQRT) RTG_KNOB(RTG_ANG_TAB_BITS)
+        RTG_KNOB(RTG_FAST_EXACT) RTG_KNOB(RTG_FAST_NORM) RTG_KNOB(RTG_SVD_DIV) RTG_KNOB(RTG_SVD_SQRT) RTG_KNOB(RTG_ANG_TAB_BITS)
         RTG_KNOB(RTG_SOLVER_SIDES) RTG_KNOB(RTG_SIDES_REBALANCE) RTG_KNOB(RTG_SIDES_FIN_LEFT) RTG_KNOB(RTG_SIDES_FLAGS) RTG_KNOB(RTG_SIDES_WAVES)
         RTG_KNOB(RTG_PRELOAD_ARM) RTG_KNOB(RTG_PRELOAD_TIPS) RTG_KNOB(RTG_L2_PREFETCH) RTG_KNOB(RTG_LATENCY_MAX_B)
         RTG_KNOB(RTG_LATENCY_WAVES) RTG_KNOB(RTG_FK_CHUNK) RTG_KNOB(RTG_FK_POS_REGS) RTG_KNOB(RTG_FK_MIN_WAVES)

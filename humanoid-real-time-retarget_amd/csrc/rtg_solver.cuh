@@ -612,13 +612,16 @@ __global__ __launch_bounds__(256, RTG_SIDES_WAVES) void k_solve_sides(SolverCons
             if (live) {
                 const float4 t = storso[r];
                 R10 = Q{t.x, t.y, t.z, t.w};
+                if (RTG_SIDES_FLAGS == 2) chain = fbp_arm<1>(C, apR, R10, E);   // right arm first: see below
                 const Q cl = fbp_arm<0>(C, apL, R10, E);
                 sarm[r] = make_float4(cl.x, cl.y, cl.z, cl.w);
             }
 #if RTG_SIDES_FLAGS
-            lds_signal(&fl[1]);          // the left chain and its exp-map slots 0-3 are in LDS
+            // the left chain and its exp-map slots 0-3 are in LDS (RTG_SIDES_FLAGS == 2: the right arm's 7-10 too, so
+            // the left wave, which finishes its own program first, can take more of the read-out: RTG_SIDES_FIN_LEFT)
+            lds_signal(&fl[1]);
 #endif
-            if (live) chain = fbp_arm<1>(C, apR, R10, E);
+            if (live && RTG_SIDES_FLAGS != 2) chain = fbp_arm<1>(C, apR, R10, E);
         } else if (live) {
             emit_fixed_links(E);
             W = fbp_wrist_fit<0>(C, view(in1, 60), hook2);
@@ -704,8 +707,8 @@ __global__ __launch_bounds__(256, RTG_SIDES_WAVES) void k_solve_sides(SolverCons
         static_assert(NL >= 7 && NL <= 11, "RTG_SIDES_FIN_LEFT must keep each wave's wrist slots on that wave");
         // with flags the left wave has only the left chain's slots 0-3 from the right wave (the right arm's 7-10 are
         // written after the flag): it reads exactly [0, 7)
-        static_assert(!(KIND == RTG_SOLVER_FULL_BODY_POS && RTG_SIDES_REBALANCE && RTG_SIDES_FLAGS) || NL == 7,
-                      "RTG_SIDES_FLAGS needs RTG_SIDES_FIN_LEFT == 7");
+        static_assert(!(KIND == RTG_SOLVER_FULL_BODY_POS && RTG_SIDES_REBALANCE && RTG_SIDES_FLAGS == 1) || NL == 7,
+                      "RTG_SIDES_FLAGS == 1 needs RTG_SIDES_FIN_LEFT == 7");
         E.finalize(side ? NL : 0, side ? 14 - NL : NL);
     }
     TS(8);

@@ -2,7 +2,8 @@
 //  [1] cr_sqrt (v_sqrt_f64 + Newton) == IEEE f32 sqrt for EVERY f32 bit pattern (NaN == NaN);
 //  [2] (float)((double)a * rcp64(n)) == IEEE f32 a / n for 2^32 hashed (a, n) pairs (full bit patterns,
 //      clustered exponents, n near 1) plus every pair of 64 special values (0, denormals, inf, NaN, extremes);
-//  [3] qexp_component_tab (exp-map angle table) == qexp_component for every f32 w bit pattern.
+//  [3] qexp_component_tab (exp-map angle table) == qexp_component for every f32 w bit pattern;
+//  [4] sqrt_clamp_rcp (one v_rsq_f64) == clamp(cr_sqrt) + rcp64, bitwise, for every f32 s.
 // Built with the library's flags by __graft_entry__.build(); run by tests/test_gpu_parity.py.
 #include <hip/hip_runtime.h>
 #include <cstdio>
@@ -17,10 +18,17 @@ __device__ __forceinline__ bool same(float a, float b)
     return __float_as_uint(a) == __float_as_uint(b) || (a != a && b != b);
 }
 
+__device__ unsigned long long g_done[5];   // threads that ran each check (a failed launch must not read as a pass)
+__device__ __forceinline__ void ran(int k)
+{
+    if (threadIdx.x == 0) atomicAdd(&g_done[k], (unsigned long long)blockDim.x);
+}
+
 __global__ void k_sqrt(uint64_t base, unsigned long long *bad)
 {
     const uint32_t u = (uint32_t)(base + (uint64_t)blockIdx.x * blockDim.x + threadIdx.x);
     const float x = __uint_as_float(u);
+    ran(0);
     if (!same(cr_sqrt(x), ieee_sqrtf(x))) atomicAdd(bad, 1ull);
 }
 
@@ -46,6 +54,7 @@ __global__ void k_div(uint64_t base, unsigned long long *bad)
     }
     if ((i & 7) == 2) un = (un & 0x80FFFFFFu) | 0x3F000000u;
     const float a = __uint_as_float(ua), n = __uint_as_float(un);
+    ran(1);
     if (!same(mulr(a, rcp64(n)), a / n)) {
         const unsigned long long k = atomicAdd(bad + 1, 1ull);
         if (k < 4) {
@@ -68,6 +77,7 @@ __global__ void k_div_special(unsigned long long *bad)
     const int i = threadIdx.x, j = blockIdx.x;   // 64 x 64
     const float a = __uint_as_float(sp[i & 31] | ((i & 32) ? 0x80000000u : 0u));
     const float n = __uint_as_float(sp[j & 31] | ((j & 32) ? 0x80000000u : 0u));
+    ran(2);
     if (!same(mulr(a, rcp64(n)), a / n)) atomicAdd(bad + 2, 1ull);
 }
 
@@ -88,14 +98,33 @@ __global__ void k_exptab(uint64_t base, const uint32_t *tab, unsigned long long 
                 z = (float)(int32_t)((h >> 32) & 0xffff) * 0x1p-15f;
     const Q q{x - 1.0f, y - 1.0f, z - 1.0f, __uint_as_float((uint32_t)i)};
     const int k = (int)(i % 3);
+    ran(3);
     if (!same(qexp_component_tab(q, k, tab), qexp_component(q, k))) atomicAdd(bad + 3, 1ull);
+}
+
+// [4] sqrt_clamp_rcp (one v_rsq_f64) == (clamp(cr_sqrt(s), lo), rcp64(n)) bitwise, n and the f64 reciprocal, for
+// EVERY f32 s and both clamps the library uses (1e-9 and 0)
+__global__ void k_normrcp(uint64_t base, unsigned long long *bad)
+{
+    const uint32_t u = (uint32_t)(base + (uint64_t)blockIdx.x * blockDim.x + threadIdx.x);
+    const float s = __uint_as_float(u);
+    ran(4);
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+        const float lo = k ? 0.0f : 1e-9f;
+        const NormRcp f = sqrt_clamp_rcp(s, lo);
+        const float n = clamp_lo(cr_sqrt(s), lo);
+        const Rcp r = rcp64(n);
+        const bool same_r = __double_as_longlong(f.r.r) == __double_as_longlong(r.r) || (f.r.r != f.r.r && r.r != r.r);
+        if (!same(f.n, n) || !same(f.r.n, r.n) || !same_r) atomicAdd(bad + 4, 1ull);
+    }
 }
 
 int main()
 {
     unsigned long long *bad;
-    (void)hipMalloc(&bad, 4 * sizeof(unsigned long long));
-    (void)hipMemset(bad, 0, 4 * sizeof(unsigned long long));
+    (void)hipMalloc(&bad, 5 * sizeof(unsigned long long));
+    (void)hipMemset(bad, 0, 5 * sizeof(unsigned long long));
     uint32_t *tab;
     (void)hipMalloc(&tab, kAngTabWords * sizeof(uint32_t));
     hipLaunchKernelGGL(k_build_tab, dim3((kAngTabWords + 255u) / 256u), dim3(256), 0, 0, tab);
@@ -104,18 +133,31 @@ int main()
         hipLaunchKernelGGL(k_sqrt, dim3((unsigned)(chunk / 256)), dim3(256), 0, 0, base, bad);
         hipLaunchKernelGGL(k_div, dim3((unsigned)(chunk / 256)), dim3(256), 0, 0, base, bad);
         hipLaunchKernelGGL(k_exptab, dim3((unsigned)(chunk / 256)), dim3(256), 0, 0, base, tab, bad);
+        hipLaunchKernelGGL(k_normrcp, dim3((unsigned)(chunk / 256)), dim3(256), 0, 0, base, bad);
     }
     hipLaunchKernelGGL(k_div_special, dim3(64), dim3(64), 0, 0, bad);
-    unsigned long long h[4] = {0, 0, 0, 0};
+    if (hipDeviceSynchronize() != hipSuccess || hipGetLastError() != hipSuccess) {
+        printf("launch/run failure: %s\n", hipGetErrorString(hipGetLastError()));
+        return 2;
+    }
+    unsigned long long h[5] = {0, 0, 0, 0, 0}, d[5] = {0, 0, 0, 0, 0};
     (void)hipMemcpy(h, bad, sizeof h, hipMemcpyDeviceToHost);
+    (void)hipMemcpyFromSymbol(d, HIP_SYMBOL(g_done), sizeof d);
+    const unsigned long long want[5] = {1ull << 32, 1ull << 32, 4096ull, 1ull << 32, 1ull << 32};
+    for (int k = 0; k < 5; ++k)
+        if (d[k] != want[k]) {
+            printf("check %d covered %llu of %llu inputs\n", k, d[k], want[k]);
+            return 2;
+        }
     printf("[1] cr_sqrt: 4294967296 inputs, %llu mismatches\n", h[0]);
     printf("[2] rcp64 division: 4294967296 pairs, %llu mismatches\n", h[1]);
     printf("[2b] rcp64 division, special values: 4096 pairs, %llu mismatches\n", h[2]);
     printf("[3] exp-map angle table: 4294967296 w bit patterns, %llu mismatches\n", h[3]);
+    printf("[4] sqrt_clamp_rcp: 4294967296 inputs x 2 clamps, %llu mismatches\n", h[4]);
     uint32_t f[16];
     (void)hipMemcpyFromSymbol(f, HIP_SYMBOL(g_first), sizeof f);
     for (unsigned k = 0; k < (h[1] < 4 ? h[1] : 4); ++k)
         printf("  a=%08x n=%08x fast=%08x ieee=%08x\n", f[4 * k], f[4 * k + 1], f[4 * k + 2], f[4 * k + 3]);
     (void)hipFree(tab);
-    return (h[0] || h[1] || h[2] || h[3]) ? 1 : 0;
+    return (h[0] || h[1] || h[2] || h[3] || h[4]) ? 1 : 0;
 }
