@@ -308,7 +308,10 @@ RTG_DEV void fk_stream_tile(const TopoView &T, const float *__restrict__ local_r
                 Q lq = Q{R[4 * k], R[4 * k + 1], R[4 * k + 2], R[4 * k + 3]};
                 Q ng;
                 V nt;
-                if (j == 0) {   // root: global = local, unnormalised (kinematics.py:27-29)
+                if (RTG_EXP_FK_COPY) {   // measurement knob: the window goes straight back out (no chain)
+                    ng = lq;
+                    nt = V{lq.x, lq.y, lq.z};
+                } else if (j == 0) {   // root: global = local, unnormalised (kinematics.py:27-29)
                     ng = lq;
                     nt = root;
                 } else {
@@ -321,7 +324,7 @@ RTG_DEV void fk_stream_tile(const TopoView &T, const float *__restrict__ local_r
                 R[4 * k] = ng.x; R[4 * k + 1] = ng.y; R[4 * k + 2] = ng.z; R[4 * k + 3] = ng.w;
                 if (RTG_FK_POS_REGS) pk[k] = nt;
                 else { P[3 * k] = nt.x; P[3 * k + 1] = nt.y; P[3 * k + 2] = nt.z; }
-                if (((sc >> 8) & 0xFF) != kNoSlot) slot_put(slots, (sc >> 8) & 0xFF, ng, nt);
+                if (!RTG_EXP_FK_COPY && ((sc >> 8) & 0xFF) != kNoSlot) slot_put(slots, (sc >> 8) & 0xFF, ng, nt);
                 g = ng;
                 t = nt;
             }
@@ -329,7 +332,8 @@ RTG_DEV void fk_stream_tile(const TopoView &T, const float *__restrict__ local_r
         wave_sync();
         if (RTG_FK_ALIGNED_STORE) chunk_store_aligned<4>(g_rot, rot, kRotPitch, carry, f0, nfr, J, c0, nC);
         else chunk_store<4>(g_rot, rot, kRotPitch, f0, nfr, J, c0, nC);
-        if (RTG_FK_POS_REGS) {   // the rotation rows are out: reuse the window for the positions
+        if (RTG_EXP_FK_NOPOS) {   // measurement knob: no position rows
+        } else if (RTG_FK_POS_REGS) {   // the rotation rows are out: reuse the window for the positions
             wave_sync();
             if (active) {
                 float *P = rot + lane * kRotPitch;

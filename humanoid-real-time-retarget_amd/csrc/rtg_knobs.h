@@ -64,6 +64,12 @@
 #ifndef RTG_DOF_FK_POS_REGS
 #define RTG_DOF_FK_POS_REGS 1   // k_dof_fk positions staged through the rotation window (as RTG_FK_POS_REGS; measured +7-9 %)
 #endif
+#ifndef RTG_EXP_FK_COPY
+#define RTG_EXP_FK_COPY 0   // measurement knob: k_fk_stream copies its windows out without the chain (wrong answers)
+#endif
+#ifndef RTG_EXP_FK_NOPOS
+#define RTG_EXP_FK_NOPOS 0   // measurement knob: k_fk_stream writes no position rows (wrong answers)
+#endif
 // ---- used by rtg_math.cuh
 #ifndef RTG_FAST_EXACT
 #define RTG_FAST_EXACT 1

@@ -586,6 +586,7 @@ __global__ __launch_bounds__(256, RTG_SIDES_WAVES) void k_solve_sides(SolverCons
         const auto b = view(in0, 63);
         Q R10 = qident(), W = qident();
         ArmPts apL{}, apR{};
+        TipPts tp{};   // RTG_PRELOAD_TIPS: the gripper's hand points, loaded with the wrist fit's points
 #if RTG_SIDES_FLAGS
         int *const fl = sflag[w >> 1];
 #endif
@@ -596,6 +597,7 @@ __global__ __launch_bounds__(256, RTG_SIDES_WAVES) void k_solve_sides(SolverCons
             } else {
                 apL = load_arm<0>(b);
                 apR = load_arm<1>(b);
+                if (RTG_PRELOAD_TIPS) tp = load_tips(view(in2, 60));
                 W = fbp_wrist_fit<1>(C, view(in2, 60), hook1);
             }
         }
@@ -624,6 +626,7 @@ __global__ __launch_bounds__(256, RTG_SIDES_WAVES) void k_solve_sides(SolverCons
             if (live && RTG_SIDES_FLAGS != 2) chain = fbp_arm<1>(C, apR, R10, E);
         } else if (live) {
             emit_fixed_links(E);
+            if (RTG_PRELOAD_TIPS) tp = load_tips(view(in1, 60));
             W = fbp_wrist_fit<0>(C, view(in1, 60), hook2);
         }
         TS(5);
@@ -635,11 +638,12 @@ __global__ __launch_bounds__(256, RTG_SIDES_WAVES) void k_solve_sides(SolverCons
         TS(6);
         if (live) {
             float *brow = body_rot ? body_rot + f * 236 : nullptr;
+            if (!RTG_PRELOAD_TIPS) tp = load_tips(view(side ? in2 : in1, 60));
             if (side) {
-                fbp_side_after_arm<PRECISE, 1>(C, load_tips(view(in2, 60)), R10, chain, W, E, brow);
+                fbp_side_after_arm<PRECISE, 1>(C, tp, R10, chain, W, E, brow);
             } else {
                 const float4 c = sarm[r];
-                fbp_side_after_arm<PRECISE, 0>(C, load_tips(view(in1, 60)), R10, Q{c.x, c.y, c.z, c.w}, W, E, brow);
+                fbp_side_after_arm<PRECISE, 0>(C, tp, R10, Q{c.x, c.y, c.z, c.w}, W, E, brow);
             }
         }
         TS(7);

@@ -147,7 +147,7 @@ def lib() -> ctypes.CDLL:
     return _lib
 
 
-WRONG_ANSWER_KNOBS = ("RTG_EXP_STUB_SVD", "RTG_EXP_NO_TABLE", "RTG_EXP_HOT_INPUTS")
+WRONG_ANSWER_KNOBS = ("RTG_EXP_STUB_SVD", "RTG_EXP_NO_TABLE", "RTG_EXP_HOT_INPUTS", "RTG_EXP_FK_COPY", "RTG_EXP_FK_NOPOS")
 
 
 def build_info(handle=None) -> dict:
