@@ -8,6 +8,7 @@
 #include <cstdarg>
 #include <cstdio>
 #include <cstring>
+#include <ctime>
 #include <new>
 #include <string>
 
@@ -499,6 +500,36 @@ int rtg_frame_server_launch(rtg_solver_t s, const float *in, float *dof, float *
     RTG_TRY(launch_frame_server(s->precise, s->consts, in, dof, local_rot, body_rot, ctl, (uint64_t)idle_ms * 100000u,
                                 as_stream(stream)),
             "k_frame_server");
+    return RTG_OK;
+}
+
+int rtg_frame_server_post(uint32_t *ctl, uint32_t seq, float *in, const float *body, const float *left_hand,
+                          const float *right_hand, const float *dof, const float *local_rot, const float *body_rot,
+                          float *dof_dst, float *local_rot_dst, float *body_rot_dst, uint32_t timeout_us)
+{
+    if (!ctl || !in || !body || !left_hand || !right_hand || !dof)
+        return fail(RTG_ERR_INVALID_ARGUMENT, "rtg_frame_server_post: NULL ctl / in / inputs / dof");
+    if (seq == RTG_SERVER_QUIT) return fail(RTG_ERR_INVALID_ARGUMENT, "rtg_frame_server_post: seq is the quit value");
+    if ((local_rot_dst && !local_rot) || (body_rot_dst && !body_rot))
+        return fail(RTG_ERR_INVALID_ARGUMENT, "rtg_frame_server_post: an output the server does not write");
+    std::memcpy(in, body, 63 * sizeof(float));
+    std::memcpy(in + 63, left_hand, 60 * sizeof(float));
+    std::memcpy(in + 123, right_hand, 60 * sizeof(float));
+    __atomic_store_n(ctl, seq, __ATOMIC_RELEASE);   // after the rows (the device acquires ctl[0] at system scope)
+    struct timespec t0, t;
+    bool timed = false;
+    for (uint32_t spins = 1; __atomic_load_n(ctl + 1, __ATOMIC_ACQUIRE) != seq; ++spins) {
+        if ((spins & 255u) != 0) continue;
+        if (__atomic_load_n(ctl + 2, __ATOMIC_ACQUIRE) && __atomic_load_n(ctl + 1, __ATOMIC_ACQUIRE) != seq)
+            return RTG_SERVER_ENDED;   // it ended on idle before it saw this frame
+        clock_gettime(CLOCK_MONOTONIC, timed ? &t : &t0);
+        if (!timed) { timed = true; continue; }
+        const int64_t us = (int64_t)(t.tv_sec - t0.tv_sec) * 1000000 + (t.tv_nsec - t0.tv_nsec) / 1000;
+        if (us > (int64_t)timeout_us) return fail(RTG_ERR_TIMEOUT, "rtg_frame_server_post: frame %u not served within %u us", seq, timeout_us);
+    }
+    if (dof_dst) std::memcpy(dof_dst, dof, 30 * sizeof(float));
+    if (local_rot_dst) std::memcpy(local_rot_dst, local_rot, 124 * sizeof(float));
+    if (body_rot_dst) std::memcpy(body_rot_dst, body_rot, 236 * sizeof(float));
     return RTG_OK;
 }
 

@@ -42,6 +42,15 @@
 #define RTG_LATENCY_WAVES 5   // 5: k_fbp_latency5 (arm chain concurrent with the wrist fits); 3: k_fbp_latency
 #endif
 // ---- used by rtg_fk.hip
+#ifndef RTG_FK_ROWS
+#define RTG_FK_ROWS 0   // 1: row-staged FK / inverse FK / DOF FK (whole tile rows through LDS, contiguous 1 KiB stores); 0: windowed streaming
+#endif
+#ifndef RTG_FK_ROWS_LDS
+#define RTG_FK_ROWS_LDS 32768   // bytes of row images per wave: sets the frames per tile (36 for the 31-joint Hu)
+#endif
+#ifndef RTG_DOF_FK_ROWS
+#define RTG_DOF_FK_ROWS 0   // HuForwardModel row-staged too (measured 2.5x slower: its sincos-heavy chain wants all 64 lanes)
+#endif
 #ifndef RTG_FK_CHUNK
 #define RTG_FK_CHUNK 8
 #endif
@@ -76,6 +85,9 @@
 #endif
 #ifndef RTG_FAST_NORM
 #define RTG_FAST_NORM 1   // sqrt_clamp_rcp: one v_rsq_f64 + Goldschmidt / Newton for the norm and 1/norm (else cr_sqrt + rcp64)
+#endif
+#ifndef RTG_EXP_MULR_NOBRANCH
+#define RTG_EXP_MULR_NOBRANCH 0   // measurement knob: mulr without its subnormal-quotient branch (wrong answers on rare inputs)
 #endif
 #ifndef RTG_EXP_NO_TABLE
 #define RTG_EXP_NO_TABLE 0

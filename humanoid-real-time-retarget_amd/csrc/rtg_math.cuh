@@ -92,7 +92,9 @@ RTG_DEV float mulr(float a, const Rcp &r)
 {
     const double p = (double)a * r.r;
     float q = (float)p;
+#if !RTG_EXP_MULR_NOBRANCH   // measurement knob: no subnormal-quotient branch (wrong on rare exact subnormal midpoints)
     if (__builtin_expect(__builtin_fabs(p) < 0x1p-126 && p != 0.0, 0)) q = a / r.n;
+#endif
     return q;
 }
 RTG_DEV float clamp_lo(float v, float lo) { return v < lo ? lo : v; }          // NaN passes through

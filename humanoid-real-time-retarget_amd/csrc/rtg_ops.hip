@@ -627,7 +627,7 @@ hipError_t launch_synth_full_body(const TopoView &T, uint64_t seed, int64_t off,
 // ----------------------------------------------------------------------------
 // build configuration (rtg.h rtg_build_info): every RTG_* knob as compiled into this library
 // ----------------------------------------------------------------------------
-#if RTG_EXP_STUB_SVD + RTG_EXP_NO_TABLE + RTG_EXP_HOT_INPUTS + RTG_EXP_FK_COPY + RTG_EXP_FK_NOPOS == 0
+#if RTG_EXP_STUB_SVD + RTG_EXP_NO_TABLE + RTG_EXP_HOT_INPUTS + RTG_EXP_FK_COPY + RTG_EXP_FK_NOPOS + RTG_EXP_MULR_NOBRANCH == 0
 #define RTG_WRONG_ANSWER_KNOBS 0
 #else
 #define RTG_WRONG_ANSWER_KNOBS 1
@@ -641,9 +641,9 @@ extern "C" const char *rtg_build_info(void)
         RTG_KNOB(RTG_FAST_EXACT) RTG_KNOB(RTG_FAST_NORM) RTG_KNOB(RTG_SVD_DIV) RTG_KNOB(RTG_SVD_SQRT) RTG_KNOB(RTG_ANG_TAB_BITS)
         RTG_KNOB(RTG_SOLVER_SIDES) RTG_KNOB(RTG_SIDES_REBALANCE) RTG_KNOB(RTG_SIDES_FIN_LEFT) RTG_KNOB(RTG_SIDES_FLAGS) RTG_KNOB(RTG_SIDES_WAVES)
         RTG_KNOB(RTG_PRELOAD_ARM) RTG_KNOB(RTG_PRELOAD_TIPS) RTG_KNOB(RTG_L2_PREFETCH) RTG_KNOB(RTG_LATENCY_MAX_B)
-        RTG_KNOB(RTG_LATENCY_WAVES) RTG_KNOB(RTG_FK_CHUNK) RTG_KNOB(RTG_FK_POS_REGS) RTG_KNOB(RTG_FK_MIN_WAVES)
+        RTG_KNOB(RTG_LATENCY_WAVES) RTG_KNOB(RTG_FK_ROWS) RTG_KNOB(RTG_FK_ROWS_LDS) RTG_KNOB(RTG_DOF_FK_ROWS) RTG_KNOB(RTG_FK_CHUNK) RTG_KNOB(RTG_FK_POS_REGS) RTG_KNOB(RTG_FK_MIN_WAVES)
         RTG_KNOB(RTG_FK_ALIGNED_STORE) RTG_KNOB(RTG_FK_REG_SLOTS) RTG_KNOB(RTG_FK_NT_STORE) RTG_KNOB(RTG_DOF_FK_POS_REGS)
-        RTG_KNOB(RTG_EXP_TIMESTAMPS) RTG_KNOB(RTG_EXP_STUB_SVD) RTG_KNOB(RTG_EXP_NO_TABLE) RTG_KNOB(RTG_EXP_FK_COPY) RTG_KNOB(RTG_EXP_FK_NOPOS)
+        RTG_KNOB(RTG_EXP_TIMESTAMPS) RTG_KNOB(RTG_EXP_STUB_SVD) RTG_KNOB(RTG_EXP_NO_TABLE) RTG_KNOB(RTG_EXP_FK_COPY) RTG_KNOB(RTG_EXP_FK_NOPOS) RTG_KNOB(RTG_EXP_MULR_NOBRANCH)
         "\"RTG_EXP_HOT_INPUTS\":\"" RTG_STR(RTG_EXP_HOT_INPUTS) "\"},\"wrong_answer_knobs\":"
         RTG_STR(RTG_WRONG_ANSWER_KNOBS) "}";
 }

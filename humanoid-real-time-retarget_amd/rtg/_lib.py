@@ -26,6 +26,8 @@ SOLVER_UPPER_BODY = 1
 SOLVER_FULL_BODY_ROT = 2
 SOLVER_BODY_ROT = 3
 SERVER_QUIT = 0xFFFFFFFF   # rtg.h RTG_SERVER_QUIT
+ERR_TIMEOUT = 5            # rtg.h RTG_ERR_TIMEOUT (rtg_frame_server_post)
+SERVER_ENDED = 6           # rtg.h RTG_SERVER_ENDED (rtg_frame_server_post: relaunch, post again)
 
 # rtg_quat_op
 OP_QUAT_MUL = 0
@@ -108,6 +110,7 @@ SIGNATURES = {
                                  c_void_p, c_void_p, c_void_p]),
     "rtg_frame_server_launch": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, ctypes.c_uint32,
                                         c_void_p]),
+    "rtg_frame_server_post": (c_int, [c_void_p, ctypes.c_uint32] + [c_void_p] * 10 + [ctypes.c_uint32]),
     "rtg_quat_op_f32": (c_int, [c_int, c_void_p, c_void_p, c_void_p, c_int64, c_void_p, c_void_p]),
     "rtg_cal_joint_quat_f32": (c_int, [c_void_p, c_void_p, c_int32, c_int64, c_void_p, c_void_p]),
     "rtg_quat_in_xyz_axis_f32": (c_int, [c_void_p, c_char_p, c_int64, c_void_p, c_void_p]),
@@ -147,7 +150,8 @@ def lib() -> ctypes.CDLL:
     return _lib
 
 
-WRONG_ANSWER_KNOBS = ("RTG_EXP_STUB_SVD", "RTG_EXP_NO_TABLE", "RTG_EXP_HOT_INPUTS", "RTG_EXP_FK_COPY", "RTG_EXP_FK_NOPOS")
+WRONG_ANSWER_KNOBS = ("RTG_EXP_STUB_SVD", "RTG_EXP_NO_TABLE", "RTG_EXP_HOT_INPUTS", "RTG_EXP_FK_COPY", "RTG_EXP_FK_NOPOS",
+                      "RTG_EXP_MULR_NOBRANCH")
 
 
 def build_info(handle=None) -> dict:

@@ -36,6 +36,28 @@ from .runtime import Solver, require_gpu, stream_handle
 from .runtime import IN_TAILS as _IN_TAILS
 
 SENTINEL = np.uint32(0x7FBADBAD)
+_SERVER_ENDED = 6   # rtg.h RTG_SERVER_ENDED
+
+
+def _host_f32_ptr(x, n: int, tail):
+    """(address, owner) of n contiguous float32 values on the host: a CPU tensor or array as it is when it already
+    is one, else a float32 copy."""
+    if isinstance(x, torch.Tensor):
+        if x.device.type != "cpu":
+            raise ValueError("per-frame inputs are host arrays")
+        if x.dtype != torch.float32 or not x.is_contiguous():
+            x = x.detach().to(torch.float32).contiguous()
+        if x.numel() != n:
+            raise ValueError(f"input of {x.numel()} values, expected shape {tail}")
+        return x.data_ptr(), x
+    a = np.ascontiguousarray(x, dtype=np.float32)
+    if a.size != n:
+        raise ValueError(f"input of {a.size} values, expected shape {tail}")
+    return _addr(a), a
+
+
+def _addr(a: np.ndarray) -> int:
+    return a.__array_interface__["data"][0]   # cheaper than a.ctypes.data
 
 
 class FrameGraph:
@@ -136,43 +158,42 @@ class FrameServer:
         self.timeout_s = float(timeout_s)
         self.seq = 0
         self._running = False
+        self._sizes = [int(np.prod(t)) for t in self.tails]
+        self._ctl_ptr, self._in_ptr = self.h_ctl.data_ptr(), self.h_in.data_ptr()
+        self._lr_ptr, self._dof_ptr = out, out + 4 * 124
+        self._br_ptr = out + 4 * 154 if want_body_rot else None
 
     def _launch(self):
         self._ctl[2] = 0
         check(lib().rtg_frame_server_launch(*self._args, stream_handle(self.stream)))
         self._running = True
 
-    def _wait(self, seq):
-        ctl = self._ctl
-        spins, t0 = 0, None
-        while ctl[1] != seq:
-            spins += 1
-            if spins % 1024 == 0:
-                if ctl[2] and ctl[1] != seq and self.stream.query():   # ended on idle before it saw this frame
-                    self._launch()
-                    continue
-                t0 = t0 or time.perf_counter()
-                if time.perf_counter() - t0 > self.timeout_s:
-                    raise RtgError(-1, f"frame server: frame {seq} not served within {self.timeout_s} s")
-
     def __call__(self, *inputs: Sequence):
+        """One frame: the copy in, the post, the wait and the copy out are ONE C call (rtg_frame_server_post)."""
         if len(inputs) != len(self.tails):
             raise ValueError(f"expected {len(self.tails)} inputs")
-        for x, a, b, t in zip(inputs, self._in_offsets[:-1], self._in_offsets[1:], self.tails):
-            arr = x.detach().numpy() if isinstance(x, torch.Tensor) else np.asarray(x)
-            if arr.size != b - a:
-                raise ValueError(f"input of {arr.size} values, expected shape {t}")
-            self._h_in_np[a:b] = arr.reshape(-1)
+        keep, ptrs = [], []
+        for x, n, t in zip(inputs, self._sizes, self.tails):
+            p, x = _host_f32_ptr(x, n, t)
+            keep.append(x)
+            ptrs.append(p)
+        lr = np.empty((31, 4), np.float32)
+        dof = np.empty(30, np.float32)
+        br = np.empty((59, 4), np.float32) if self.want_body_rot else None
         if not self._running or (self._ctl[2] and self.stream.query()):
             self._launch()
         self.seq = self.seq + 1 if self.seq + 1 < int(self._quit) else 1
-        self._ctl[0] = self.seq   # after the inputs (x86 stores are not reordered with older stores)
-        self._wait(self.seq)
-        out = self.h_out.numpy()
-        lr = torch.from_numpy(out[:124].reshape(31, 4).copy())
-        dof = torch.from_numpy(out[124:154].copy())
-        br = torch.from_numpy(out[154:].reshape(59, 4).copy()) if self.want_body_rot else None
-        return lr, dof, br
+        post = lib().rtg_frame_server_post
+        args = [self._ctl_ptr, self.seq, self._in_ptr, *ptrs, self._dof_ptr, self._lr_ptr, self._br_ptr,
+                _addr(dof), _addr(lr), _addr(br) if br is not None else None,
+                int(self.timeout_s * 1e6)]
+        rc = post(*args)
+        while rc == _SERVER_ENDED:   # it idled out before it took the frame: relaunch (the frame is still posted)
+            self.stream.synchronize()
+            self._launch()
+            rc = post(*args)
+        check(rc)
+        return torch.from_numpy(lr), torch.from_numpy(dof), (torch.from_numpy(br) if br is not None else None)
 
     def close(self):
         if self._running:

@@ -35,7 +35,9 @@ typedef enum rtg_status {
     RTG_ERR_INVALID_ARGUMENT = 1,
     RTG_ERR_DEVICE = 2,          /* a HIP runtime call failed */
     RTG_ERR_OUT_OF_MEMORY = 3,
-    RTG_ERR_UNSUPPORTED = 4
+    RTG_ERR_UNSUPPORTED = 4,
+    RTG_ERR_TIMEOUT = 5,         /* rtg_frame_server_post: the frame was not served in time */
+    RTG_SERVER_ENDED = 6         /* rtg_frame_server_post: the server ended (idle) before it took the frame */
 } rtg_status;
 
 /* Frame-batch layout of solver inputs.  AOS: the reference's (B, P, C) rows (e.g. body
@@ -216,6 +218,17 @@ int rtg_retarget_f32(rtg_solver_t solver, const float *in0, const float *in1, co
 #define RTG_SERVER_QUIT 0xFFFFFFFFu
 int rtg_frame_server_launch(rtg_solver_t solver, const float *in, float *dof, float *local_rot, float *body_rot,
                             uint32_t *ctl, uint32_t idle_ms, rtg_stream_t stream);
+
+/* One frame through a running rtg_frame_server_launch server, on the host alone (no HIP call): the whole per-frame
+ * round trip of the teleop loop (sim_full_body_teleop.py:115-119) in one C call.  Copies the frame's rows into the
+ * server's pinned `in` (body (21,3) | left hand (20,3) | right hand (20,3)), posts `seq` (!= the last one posted,
+ * != RTG_SERVER_QUIT) in ctl[0] after them, spins until the device publishes it in ctl[1], then copies the pinned
+ * outputs the server writes (dof 30, local_rot 124, body_rot 236 floats) into the *_dst buffers that are not NULL.
+ * Returns RTG_OK; RTG_SERVER_ENDED if the server ended (idle_ms) before it took the frame -- relaunch it and post
+ * the same seq again; RTG_ERR_TIMEOUT after timeout_us (the frame may still be served later). */
+int rtg_frame_server_post(uint32_t *ctl, uint32_t seq, float *in, const float *body, const float *left_hand,
+                          const float *right_hand, const float *dof, const float *local_rot, const float *body_rot,
+                          float *dof_dst, float *local_rot_dst, float *body_rot_dst, uint32_t timeout_us);
 
 /* ------------------------------------------------------------------------
  * Elementwise primitives (poselib rotation3d.py, retarget transform3d.py)

@@ -283,3 +283,54 @@ def test_serializable_json_and_npy_roundtrip(tmp_path):
                 assert back.fps == 30 and torch.equal(back.global_angular_velocity, obj.global_angular_velocity)
     with pytest.raises(AssertionError):
         SkeletonState.from_file(str(tmp_path / "SkeletonTree.json"))
+
+
+def test_frame_server_post_protocol_on_the_host():
+    """rtg_frame_server_post (the teleop per-frame round trip in one C call) against a host thread standing in for
+    k_frame_server: the frame's rows land in `in` before ctl[0] = seq, the outputs are copied out only after
+    ctl[1] = seq, a server that ended before taking the frame reports RTG_SERVER_ENDED, a silent one times out."""
+    import threading
+    import time
+    from rtg import _lib
+    lib = _lib.lib()
+    vp = ctypes.c_void_p
+    ctl = np.zeros(4, np.uint32)
+    inb = np.zeros(183, np.float32)
+    out = np.zeros(390, np.float32)   # local_rot 124 | dof 30 | body_rot 236, as FrameServer lays out its pinned buffer
+    rng = np.random.default_rng(5)
+    body, lh, rh = (rng.normal(size=s).astype(np.float32) for s in ((21, 3), (20, 3), (20, 3)))
+    seen = {}
+
+    def device(seq):
+        while ctl[0] != seq:
+            time.sleep(0)
+        seen["in"] = inb.copy()
+        out[:] = np.arange(390, dtype=np.float32) + seq
+        ctl[1] = seq
+
+    def post(seq, timeout_us=2_000_000):
+        dof, lr, br = np.empty(30, np.float32), np.empty((31, 4), np.float32), np.empty((59, 4), np.float32)
+        a = lambda x: vp(x.ctypes.data)
+        rc = lib.rtg_frame_server_post(a(ctl), seq, a(inb), a(body), a(lh), a(rh), vp(out.ctypes.data + 4 * 124),
+                                       a(out), vp(out.ctypes.data + 4 * 154), a(dof), a(lr), a(br), timeout_us)
+        return rc, dof, lr, br
+
+    th = threading.Thread(target=device, args=(7,))
+    th.start()
+    rc, dof, lr, br = post(7)
+    th.join()
+    assert rc == 0
+    np.testing.assert_array_equal(seen["in"], np.concatenate([body.ravel(), lh.ravel(), rh.ravel()]))
+    np.testing.assert_array_equal(lr.ravel(), np.arange(124, dtype=np.float32) + 7)
+    np.testing.assert_array_equal(dof, np.arange(124, 154, dtype=np.float32) + 7)
+    np.testing.assert_array_equal(br.ravel(), np.arange(154, 390, dtype=np.float32) + 7)
+    ctl[2] = 1                                       # the server has ended (idle) and never takes frame 8
+    assert post(8)[0] == _lib.SERVER_ENDED
+    ctl[2] = 0
+    t0 = time.perf_counter()
+    assert post(9, timeout_us=20_000)[0] == _lib.ERR_TIMEOUT
+    assert time.perf_counter() - t0 < 5.0
+    assert b"not served" in lib.rtg_last_error()
+    assert lib.rtg_frame_server_post(None, 1, *([None] * 10), 10) == 1
+    assert lib.rtg_frame_server_post(vp(ctl.ctypes.data), _lib.SERVER_QUIT, *([vp(inb.ctypes.data)] * 5),
+                                     *([None] * 5), 10) == 1
