@@ -57,7 +57,12 @@ struct SC { float s, c; };
 RTG_DEV SC cr_sincos(double x)
 {
     const crm::SinCos r = crm::crm_sincos(x);
-    return SC{r.s_ok ? r.s : (float)::sin(x), r.c_ok ? r.c : (float)::cos(x)};
+    SC out{r.s, r.c};
+    if (__builtin_expect(!(r.s_ok && r.c_ok), 0)) {   // one rare-case branch for the pair
+        if (!r.s_ok) out.s = (float)::sin(x);
+        if (!r.c_ok) out.c = (float)::cos(x);
+    }
+    return out;
 }
 // k float divisions by one denominator n: RN(a/n) == (float)((double)a * RN(1/(double)n))
 // for all f32 a, n.  (An f32 quotient is never within 2^-50 relative of an f32
@@ -97,6 +102,40 @@ RTG_DEV float mulr(float a, const Rcp &r)
 #endif
     return q;
 }
+// K quotients by one denominator behind ONE rare-case branch: each is (float)(a_i * 1/n) as in mulr, and if any
+// product is a nonzero subnormal, every quotient of the group takes the IEEE division -- identical to separate mulr
+// calls (for a normal quotient the IEEE division equals the product, by mulr's argument), one branch instead of K.
+template <int K>
+RTG_DEV void mulr_k(const float (&a)[K], const Rcp &r, float (&q)[K])
+{
+    bool sub = false;
+#pragma unroll
+    for (int i = 0; i < K; ++i) {
+        const double p = (double)a[i] * r.r;
+        q[i] = (float)p;
+        sub = sub || (__builtin_fabs(p) < 0x1p-126 && p != 0.0);
+    }
+#if !RTG_EXP_MULR_NOBRANCH
+    if (__builtin_expect(sub, 0)) {
+#pragma unroll
+        for (int i = 0; i < K; ++i) q[i] = a[i] / r.n;
+    }
+#endif
+}
+RTG_DEV Q mulr_q(Q v, const Rcp &r)
+{
+    const float a[4] = {v.x, v.y, v.z, v.w};
+    float q[4];
+    mulr_k<4>(a, r, q);
+    return Q{q[0], q[1], q[2], q[3]};
+}
+RTG_DEV V mulr_v(V v, const Rcp &r)
+{
+    const float a[3] = {v.x, v.y, v.z};
+    float q[3];
+    mulr_k<3>(a, r, q);
+    return V{q[0], q[1], q[2]};
+}
 RTG_DEV float clamp_lo(float v, float lo) { return v < lo ? lo : v; }          // NaN passes through
 // n = max(RN32(sqrt(s)), lo) and its reciprocal for mulr -- the normalisation step every quat_unit / quat_normalize /
 // axis normalisation takes (clamp(norm, 1e-9), then k divisions by it).  cr_sqrt + rcp64 issue three f64
@@ -112,28 +151,32 @@ struct NormRcp {
 RTG_DEV NormRcp sqrt_clamp_rcp(float s, float lo)
 {
 #if RTG_FAST_NORM
+    // the fast path runs unconditionally (on s <= 0 / inf / NaN its values are discarded) and ONE rare-case branch
+    // takes the cr_sqrt + rcp64 path when s is not a positive finite number or n needs the clamp
     const double d = (double)s;
-    if (__builtin_expect(d > 0.0 && d < __builtin_inf(), 1)) {
-        const double y = __builtin_amdgcn_rsq(d);
-        double g = d * y, h = 0.5 * y;
-        double e = __builtin_fma(-g, h, 0.5);
-        g = __builtin_fma(g, e, g);
-        h = __builtin_fma(h, e, h);
-        e = __builtin_fma(-g, h, 0.5);
-        g = __builtin_fma(g, e, g);
-        h = __builtin_fma(h, e, h);
-        const float n = (float)g;
-        if (__builtin_expect(n >= lo, 1)) {
-            const double dn = (double)n, r0 = h + h;
-            const double e0 = __builtin_fma(-dn, r0, 1.0);
-            const double r1 = __builtin_fma(r0, e0, r0);
-            const double e1 = __builtin_fma(-dn, r1, 1.0);
-            return NormRcp{n, Rcp{__builtin_fma(r1, e1, r1), n}};
-        }
+    const double y = __builtin_amdgcn_rsq(d);
+    double g = d * y, h = 0.5 * y;
+    double e = __builtin_fma(-g, h, 0.5);
+    g = __builtin_fma(g, e, g);
+    h = __builtin_fma(h, e, h);
+    e = __builtin_fma(-g, h, 0.5);
+    g = __builtin_fma(g, e, g);
+    h = __builtin_fma(h, e, h);
+    const float n = (float)g;
+    const double dn = (double)n, r0 = h + h;
+    const double e0 = __builtin_fma(-dn, r0, 1.0);
+    const double r1 = __builtin_fma(r0, e0, r0);
+    const double e1 = __builtin_fma(-dn, r1, 1.0);
+    NormRcp out{n, Rcp{__builtin_fma(r1, e1, r1), n}};
+    if (__builtin_expect(!(d > 0.0 && d < __builtin_inf() && n >= lo), 0)) {
+        const float nc = clamp_lo(cr_sqrt(s), lo);
+        out = NormRcp{nc, rcp64(nc)};
     }
-#endif
+    return out;
+#else
     const float n = clamp_lo(cr_sqrt(s), lo);
     return NormRcp{n, rcp64(n)};
+#endif
 }
 
 RTG_DEV float tsign(float v) { return v > 0.0f ? 1.0f : (v < 0.0f ? -1.0f : 0.0f); }
@@ -246,21 +289,22 @@ RTG_DEV Q qnormalize(Q q)  // quat_unit(quat_pos(q)) :30-56,92-98
     const float f = 1.0f - 2.0f * (q.w < 0.0f ? 1.0f : 0.0f);
     q.x = f * q.x; q.y = f * q.y; q.z = f * q.z; q.w = f * q.w;
     const Rcp r = sqrt_clamp_rcp(((q.x * q.x + q.y * q.y) + q.z * q.z) + q.w * q.w, 1e-9f).r;
-    return Q{mulr(q.x, r), mulr(q.y, r), mulr(q.z, r), mulr(q.w, r)};
+    return mulr_q(q, r);
 }
 RTG_DEV Q qmul_norm(Q a, Q b) { return qnormalize(qmul(a, b)); }
 RTG_DEV float qabs(Q q) { return cr_sqrt(((q.x * q.x + q.y * q.y) + q.z * q.z) + q.w * q.w); }   // :41-47
 RTG_DEV Q qunit(Q q)                                                                                 // :50-56
 {
     const Rcp r = sqrt_clamp_rcp(((q.x * q.x + q.y * q.y) + q.z * q.z) + q.w * q.w, 1e-9f).r;
-    return Q{mulr(q.x, r), mulr(q.y, r), mulr(q.z, r), mulr(q.w, r)};
+    return mulr_q(q, r);
 }
 // quat_angle_axis (:230-240): angle = acos(clamp(2 w^2 - 1)), axis = xyz / max(|xyz|, 1e-9)
 RTG_DEV Q qangle_axis_abs(Q q)
 {
     const float s = clamp_lohi(2.0f * (q.w * q.w) - 1.0f, -1.0f, 1.0f);
     const Rcp r = sqrt_clamp_rcp((q.x * q.x + q.y * q.y) + q.z * q.z, 1e-9f).r;
-    return Q{cr_acos(s), mulr(q.x, r), mulr(q.y, r), mulr(q.z, r)};
+    const V ax = mulr_v(V{q.x, q.y, q.z}, r);
+    return Q{cr_acos(s), ax.x, ax.y, ax.z};
 }
 
 RTG_DEV V qrotate(Q q, V v)  // :205-211, two Hamilton products
@@ -275,7 +319,8 @@ RTG_DEV Q qfrom_angle_axis(float angle, V axis)  // :122-143
     // axis.norm(p=2, dim=-1) of a 3-vector: torch's fma chain (measured: 100 % vs 90 % for the plain left fold)
     const Rcp r = sqrt_clamp_rcp(__builtin_fmaf(axis.z, axis.z, __builtin_fmaf(axis.y, axis.y, axis.x * axis.x)),
                                  1e-9f).r;
-    const float ax = mulr(axis.x, r), ay = mulr(axis.y, r), az = mulr(axis.z, r);
+    const V u = mulr_v(axis, r);
+    const float ax = u.x, ay = u.y, az = u.z;
     const SC t = cr_sincos((double)theta);
     const float s = t.s, c = t.c;
     return qnormalize(Q{ax * s, ay * s, az * s, c});
@@ -340,8 +385,8 @@ RTG_DEV Q qangle_axis(Q q)
     angle = normalize_angle(angle);
     const bool mask = fabsf(sin_theta) > 1e-5f;
     const Rcp r = rcp64(sin_theta);
-    return Q{mask ? angle : 0.0f, mask ? mulr(q.x, r) : 0.0f, mask ? mulr(q.y, r) : 0.0f,
-             mask ? mulr(q.z, r) : 1.0f};
+    const V u = mulr_v(V{q.x, q.y, q.z}, r);
+    return Q{mask ? angle : 0.0f, mask ? u.x : 0.0f, mask ? u.y : 0.0f, mask ? u.z : 1.0f};
 }
 RTG_DEV float qexp_component(Q q, int k)
 {
@@ -418,6 +463,29 @@ RTG_DEV float exp_dof_tab(float w, float qk, const uint32_t *__restrict__ tab)
     if (__builtin_expect(mask && code == 0u, 0)) angle = normalize_angle(2.0f * cr_acos(w));
     return mask ? angle * (qk / sin_theta) : 0.0f;
 }
+// exp_dof_tab split for a batch of read-outs that shares ONE rare-case branch (Emit::finalize): the table angle
+// and whether this w needs the exact path; then exp_dof_finish.  Same operations, same values as exp_dof_tab.
+struct ExpDof {
+    float angle, sin_theta;
+    bool mask, exact;
+};
+RTG_DEV ExpDof exp_dof_table_part(float w, const uint32_t *__restrict__ tab)
+{
+    const uint32_t i = __float_as_uint(w) - kAngTabLo;
+    const bool in = i < kAngTabEntries;
+    const uint32_t wd = ang_tab_word(i);
+#if RTG_EXP_NO_TABLE
+    const uint32_t word = 0x24924924u + 0u * tab[0];
+#else
+    const uint32_t word = tab[in ? wd : 0u];
+#endif
+    const float sin_theta = cr_sqrt(1.0f - w * w);
+    const bool mask = fabsf(sin_theta) > 1e-5f;
+    const float P = exp_angle_estimate(w);
+    const uint32_t code = in ? (word >> ((i - wd * kAngTabPer) * kAngTabBits)) & ((1u << kAngTabBits) - 1u) : 0u;
+    return ExpDof{__uint_as_float(__float_as_uint(P) + code - kAngTabBias), sin_theta, mask, mask && code == 0u};
+}
+RTG_DEV float exp_dof_finish(const ExpDof &e, float qk) { return e.mask ? e.angle * (qk / e.sin_theta) : 0.0f; }
 RTG_DEV float qexp_component_tab(Q q, int k, const uint32_t *__restrict__ tab)
 {
     return exp_dof_tab(q.w, k == 0 ? q.x : (k == 1 ? q.y : q.z), tab);
@@ -438,14 +506,14 @@ RTG_DEV V vsub(V a, V b) { return V{a.x - b.x, a.y - b.y, a.z - b.z}; }
 RTG_DEV V vdiv(V a, float s)
 {
     const Rcp r = rcp64(s);
-    return V{mulr(a.x, r), mulr(a.y, r), mulr(a.z, r)};
+    return mulr_v(a, r);
 }
 RTG_DEV V vmul(V a, float s) { return V{s * a.x, s * a.y, s * a.z}; }
 // v / torch.linalg.norm(v): vdiv(v, lnorm3(v)) through one sqrt_clamp_rcp (lo = 0 clamps nothing)
 RTG_DEV V vunit(V a)
 {
     const Rcp r = sqrt_clamp_rcp(__builtin_fmaf(a.z, a.z, __builtin_fmaf(a.y, a.y, a.x * a.x)), 0.0f).r;
-    return V{mulr(a.x, r), mulr(a.y, r), mulr(a.z, r)};
+    return mulr_v(a, r);
 }
 
 RTG_DEV V proj_in_plane(V v, V n)  // :61-75
@@ -483,7 +551,8 @@ RTG_DEV Q exp_map_angle_axis(V e)
     const Rcp r = nr.r;
     const float a = normalize_angle(n);
     const bool mask = fabsf(a) > 1e-5f;
-    return Q{mask ? a : 0.0f, mask ? mulr(e.x, r) : 0.0f, mask ? mulr(e.y, r) : 0.0f, mask ? mulr(e.z, r) : 1.0f};
+    const V u = mulr_v(e, r);
+    return Q{mask ? a : 0.0f, mask ? u.x : 0.0f, mask ? u.y : 0.0f, mask ? u.z : 1.0f};
 }
 // quat_slerp (transform3d.py:152-174), t per row
 RTG_DEV Q qslerp(Q q0, Q q1, float t)
@@ -602,21 +671,29 @@ RTG_DEV void la_lartg(float f, float g, float &c, float &s, float &r)   // SLART
     const float safmin = 1.17549435e-38f, safmax = 1.0f / safmin;
     const float rtmin = 1.08420217e-19f, rtmax = 1.30438176e+19f;   // sqrt(safmin), sqrt(safmax / 2)
     const float f1 = fabsf(f), g1 = fabsf(g);
-    if (g == 0.0f) { c = 1.0f; s = 0.0f; r = f; }
-    else if (f == 0.0f) { c = 0.0f; s = __builtin_copysignf(1.0f, g); r = g1; }
-    else if (f1 > rtmin && f1 < rtmax && g1 > rtmin && g1 < rtmax) {
+    // the common case (f, g nonzero and in range) runs unconditionally; the other three cases of SLARTG redo the
+    // outputs behind ONE rare-case branch -- the same operations per case as the reference's cascade
+    {
         const float d = la_sqrt(f * f + g * g);
         const Rcp rd = rcp64(d);
-        c = mulr(f1, rd);
+        const float num[2] = {f1, g};
+        float quo[2];
+        mulr_k<2>(num, rd, quo);
+        c = quo[0];
         r = __builtin_copysignf(d, f);
-        s = f < 0.0f ? -mulr(g, rd) : mulr(g, rd);   // g / r with r = +-d (RN is sign-symmetric)
-    } else {
-        const float u = fminf(safmax, fmaxf(safmin, fmaxf(f1, g1)));
-        const float fs = fdiv(f, u), gs = fdiv(g, u), d = la_sqrt(fs * fs + gs * gs);
-        c = fdiv(fabsf(fs), d);
-        r = __builtin_copysignf(d, f);
-        s = fdiv(gs, r);
-        r *= u;
+        s = f < 0.0f ? -quo[1] : quo[1];   // g / r with r = +-d (RN is sign-symmetric)
+    }
+    if (__builtin_expect(!(g != 0.0f && f != 0.0f && f1 > rtmin && f1 < rtmax && g1 > rtmin && g1 < rtmax), 0)) {
+        if (g == 0.0f) { c = 1.0f; s = 0.0f; r = f; }
+        else if (f == 0.0f) { c = 0.0f; s = __builtin_copysignf(1.0f, g); r = g1; }
+        else {
+            const float u = fminf(safmax, fmaxf(safmin, fmaxf(f1, g1)));
+            const float fs = fdiv(f, u), gs = fdiv(g, u), d = la_sqrt(fs * fs + gs * gs);
+            c = fdiv(fabsf(fs), d);
+            r = __builtin_copysignf(d, f);
+            s = fdiv(gs, r);
+            r *= u;
+        }
     }
 }
 RTG_DEV float la_las2_min(float f, float g, float h)   // SLAS2, SSMIN only (the shift)
@@ -675,11 +752,19 @@ RTG_DEV void la_lasv2(float f, float g, float h, float &ssmin, float &ssmax, flo
             else t = (fdiv(m, s + t) + fdiv(m, r + l)) * (1.0f + a);
             const float l2 = la_sqrt(t * t + 4.0f);
             const Rcp rl = rcp64(l2);
-            crt = mulr(2.0f, rl);
-            srt = mulr(t, rl);
+            {
+                const float num[2] = {2.0f, t};
+                float quo[2];
+                mulr_k<2>(num, rl, quo);
+                crt = quo[0];
+                srt = quo[1];
+            }
             const Rcp ra = rcp64(a);
-            clt = mulr(crt + srt * m, ra);
-            slt = mulr(fdiv(ht, ft) * srt, ra);
+            const float num[2] = {crt + srt * m, fdiv(ht, ft) * srt};
+            float quo[2];
+            mulr_k<2>(num, ra, quo);
+            clt = quo[0];
+            slt = quo[1];
         }
     }
     if (swap) { csl = srt; snl = crt; csr = slt; snr = clt; }

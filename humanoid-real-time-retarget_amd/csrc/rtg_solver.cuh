@@ -50,14 +50,28 @@ struct Emit {
     }
     // The DOF read-out of slots [s0, s0 + n) in one batch: the table loads of all links are in flight together
     // and their arithmetic interleaves, instead of one exposed load latency per link.
+    // The slots' exact-path fallbacks (w outside the table or a code-0 entry, rare) share one branch, and inside it
+    // one loop (not unrolled: a single copy of the exact path) redoes just those slots.  Same values.
     RTG_DEV void finalize(int s0, int n) const
     {
+        uint32_t exact = 0;
 #pragma unroll
         for (int j = 0; j < 14; ++j)
             if (j >= s0 && j < s0 + n) {
                 const float2 v = st[j * sst];
-                row[j < 7 ? 11 + j : 13 + j] = exp_dof_tab(v.x, v.y, ang);
+                const ExpDof e = exp_dof_table_part(v.x, ang);
+                exact |= (uint32_t)e.exact << j;
+                row[j < 7 ? 11 + j : 13 + j] = exp_dof_finish(e, v.y);
             }
+        if (__builtin_expect(exact != 0u, 0)) {
+#pragma unroll 1
+            for (int j = s0; j < s0 + n; ++j)
+                if ((exact >> j) & 1u) {
+                    const float2 v = st[j * sst];
+                    const float angle = normalize_angle(2.0f * cr_acos(v.x));
+                    row[j < 7 ? 11 + j : 13 + j] = angle * (v.y / cr_sqrt(1.0f - v.x * v.x));   // mask holds here
+                }
+        }
     }
 };
 

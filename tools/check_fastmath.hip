@@ -3,7 +3,9 @@
 //  [2] (float)((double)a * rcp64(n)) == IEEE f32 a / n for 2^32 hashed (a, n) pairs (full bit patterns,
 //      clustered exponents, n near 1) plus every pair of 64 special values (0, denormals, inf, NaN, extremes);
 //  [3] qexp_component_tab (exp-map angle table) == qexp_component for every f32 w bit pattern;
-//  [4] sqrt_clamp_rcp (one v_rsq_f64) == clamp(cr_sqrt) + rcp64, bitwise, for every f32 s.
+//  [4] sqrt_clamp_rcp (one v_rsq_f64) == clamp(cr_sqrt) + rcp64, bitwise, for every f32 s;
+//  [5] mulr_k (K quotients by one denominator behind one subnormal branch) == K IEEE f32 divisions, on 2^30
+//      hashed (a0, a1, a2, n) with a quarter of the groups steered to a subnormal first quotient.
 // Built with the library's flags by __graft_entry__.build(); run by tests/test_gpu_parity.py.
 #include <hip/hip_runtime.h>
 #include <cstdio>
@@ -18,7 +20,7 @@ __device__ __forceinline__ bool same(float a, float b)
     return __float_as_uint(a) == __float_as_uint(b) || (a != a && b != b);
 }
 
-__device__ unsigned long long g_done[5];   // threads that ran each check (a failed launch must not read as a pass)
+__device__ unsigned long long g_done[6];   // threads that ran each check (a failed launch must not read as a pass)
 __device__ __forceinline__ void ran(int k)
 {
     if (threadIdx.x == 0) atomicAdd(&g_done[k], (unsigned long long)blockDim.x);
@@ -120,11 +122,30 @@ __global__ void k_normrcp(uint64_t base, unsigned long long *bad)
     }
 }
 
+// [5] the grouped form: one subnormal quotient in the group sends all three to the IEEE division
+__global__ void k_divk(uint64_t base, unsigned long long *bad)
+{
+    const uint64_t i = base + (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const uint64_t h = mix(i), h2 = mix(i ^ 0x5DEECE66Dull);
+    uint32_t un = (uint32_t)(h >> 32);
+    const uint32_t ua[3] = {(uint32_t)h, (uint32_t)h2, (uint32_t)(h2 >> 32)};
+    if ((i & 3) == 1) {   // exponent of n = exponent of a0 + 126 .. 149: a0 / n subnormal or just normal
+        const uint32_t ea = (ua[0] >> 23) & 0xFFu, en = ea + 126u + (uint32_t)((h2 >> 8) % 24u);
+        if (ea > 0u && en < 255u) un = (un & 0x807FFFFFu) | (en << 23);
+    }
+    float a[3], q[3];
+    for (int k = 0; k < 3; ++k) a[k] = __uint_as_float(ua[k]);
+    const float n = __uint_as_float(un);
+    ran(5);
+    mulr_k<3>(a, rcp64(n), q);
+    if (!same(q[0], a[0] / n) || !same(q[1], a[1] / n) || !same(q[2], a[2] / n)) atomicAdd(bad + 5, 1ull);
+}
+
 int main()
 {
     unsigned long long *bad;
-    (void)hipMalloc(&bad, 5 * sizeof(unsigned long long));
-    (void)hipMemset(bad, 0, 5 * sizeof(unsigned long long));
+    (void)hipMalloc(&bad, 6 * sizeof(unsigned long long));
+    (void)hipMemset(bad, 0, 6 * sizeof(unsigned long long));
     uint32_t *tab;
     (void)hipMalloc(&tab, kAngTabWords * sizeof(uint32_t));
     hipLaunchKernelGGL(k_build_tab, dim3((kAngTabWords + 255u) / 256u), dim3(256), 0, 0, tab);
@@ -135,16 +156,17 @@ int main()
         hipLaunchKernelGGL(k_exptab, dim3((unsigned)(chunk / 256)), dim3(256), 0, 0, base, tab, bad);
         hipLaunchKernelGGL(k_normrcp, dim3((unsigned)(chunk / 256)), dim3(256), 0, 0, base, bad);
     }
+    hipLaunchKernelGGL(k_divk, dim3((unsigned)(chunk / 256)), dim3(256), 0, 0, 0ull, bad);
     hipLaunchKernelGGL(k_div_special, dim3(64), dim3(64), 0, 0, bad);
     if (hipDeviceSynchronize() != hipSuccess || hipGetLastError() != hipSuccess) {
         printf("launch/run failure: %s\n", hipGetErrorString(hipGetLastError()));
         return 2;
     }
-    unsigned long long h[5] = {0, 0, 0, 0, 0}, d[5] = {0, 0, 0, 0, 0};
+    unsigned long long h[6] = {0, 0, 0, 0, 0, 0}, d[6] = {0, 0, 0, 0, 0, 0};
     (void)hipMemcpy(h, bad, sizeof h, hipMemcpyDeviceToHost);
     (void)hipMemcpyFromSymbol(d, HIP_SYMBOL(g_done), sizeof d);
-    const unsigned long long want[5] = {1ull << 32, 1ull << 32, 4096ull, 1ull << 32, 1ull << 32};
-    for (int k = 0; k < 5; ++k)
+    const unsigned long long want[6] = {1ull << 32, 1ull << 32, 4096ull, 1ull << 32, 1ull << 32, 1ull << 30};
+    for (int k = 0; k < 6; ++k)
         if (d[k] != want[k]) {
             printf("check %d covered %llu of %llu inputs\n", k, d[k], want[k]);
             return 2;
@@ -154,10 +176,11 @@ int main()
     printf("[2b] rcp64 division, special values: 4096 pairs, %llu mismatches\n", h[2]);
     printf("[3] exp-map angle table: 4294967296 w bit patterns, %llu mismatches\n", h[3]);
     printf("[4] sqrt_clamp_rcp: 4294967296 inputs x 2 clamps, %llu mismatches\n", h[4]);
+    printf("[5] grouped mulr_k<3>: 1073741824 groups, %llu mismatches\n", h[5]);
     uint32_t f[16];
     (void)hipMemcpyFromSymbol(f, HIP_SYMBOL(g_first), sizeof f);
     for (unsigned k = 0; k < (h[1] < 4 ? h[1] : 4); ++k)
         printf("  a=%08x n=%08x fast=%08x ieee=%08x\n", f[4 * k], f[4 * k + 1], f[4 * k + 2], f[4 * k + 3]);
     (void)hipFree(tab);
-    return (h[0] || h[1] || h[2] || h[3] || h[4]) ? 1 : 0;
+    return (h[0] || h[1] || h[2] || h[3] || h[4] || h[5]) ? 1 : 0;
 }
