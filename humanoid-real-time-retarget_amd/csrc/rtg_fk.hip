@@ -102,14 +102,16 @@ static inline size_t lds_slot_floats(int nslots)
 {
     return nslots > RTG_FK_REG_SLOTS ? (size_t)(nslots - RTG_FK_REG_SLOTS) * 7 * kFkTile : 0;
 }
-static inline size_t fk_stream_lds_bytes(int nslots)
+static inline size_t fk_stream_lds_bytes(int nslots)   // (+ RTG_FK_LDS_PAD: an occupancy experiment, fewer waves per CU)
 {
-    return sizeof(float) * ((size_t)kFkTile * kRotPitch + (size_t)kPosWin + kCarryFloats + lds_slot_floats(nslots));
+    return sizeof(float) * ((size_t)kFkTile * kRotPitch + (size_t)kPosWin + kCarryFloats + lds_slot_floats(nslots)) +
+           RTG_FK_LDS_PAD;
 }
 constexpr int kDofPosWin = RTG_DOF_FK_POS_REGS ? 0 : kFkTile * kPosPitch;
 static inline size_t dof_fk_lds_bytes(int nslots)
 {
-    return sizeof(float) * ((size_t)kFkTile * kRotPitch + (size_t)kDofPosWin + kCarryFloats + lds_slot_floats(nslots));
+    return sizeof(float) * ((size_t)kFkTile * kRotPitch + (size_t)kDofPosWin + kCarryFloats + lds_slot_floats(nslots)) +
+           RTG_FK_LDS_PAD;
 }
 
 // A streaming tile is one wave, so ordering its LDS traffic needs no block

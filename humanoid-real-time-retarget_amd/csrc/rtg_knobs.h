@@ -38,6 +38,12 @@
 #ifndef RTG_EXP_TIMESTAMPS
 #define RTG_EXP_TIMESTAMPS 0   // measurement knob: block 0's lane 0 of each wave records the 100 MHz wall clock at
 #endif                         // each phase into body_rot (as u32 pairs) -- wrong body_rot, tools/latency_phases.py
+#ifndef RTG_FRAME1_LANES
+#define RTG_FRAME1_LANES 1   // B = 1 (and the frame server): k_fbp_frame1, the frame's independent sub-steps on separate lanes
+#endif
+#ifndef RTG_SERVER_FRAME1
+#define RTG_SERVER_FRAME1 1   // k_frame_server runs each frame as k_fbp_frame1's tile (0: k_fbp_latency5's tile at B = 1)
+#endif
 #ifndef RTG_LATENCY_WAVES
 #define RTG_LATENCY_WAVES 5   // 5: k_fbp_latency5 (arm chain concurrent with the wrist fits); 3: k_fbp_latency
 #endif
@@ -50,6 +56,9 @@
 #endif
 #ifndef RTG_DOF_FK_ROWS
 #define RTG_DOF_FK_ROWS 0   // HuForwardModel row-staged too (measured 2.5x slower: its sincos-heavy chain wants all 64 lanes)
+#endif
+#ifndef RTG_FK_LDS_PAD
+#define RTG_FK_LDS_PAD 0   // extra LDS bytes per streaming-FK wave: fewer waves per CU (an L2-footprint experiment)
 #endif
 #ifndef RTG_FK_CHUNK
 #define RTG_FK_CHUNK 8

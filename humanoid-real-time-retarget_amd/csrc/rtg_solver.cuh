@@ -982,6 +982,209 @@ RTG_DEV void fbp_latency5_tile(const SolverConsts &C, const float *__restrict__ 
     TS(7);
 }
 
+// ----------------------------------------------------------------------------
+// ONE frame (B = 1: the teleop path -- k_frame_server and rtg_retarget_f32 at B = 1) on k_fbp_latency5's five
+// waves, with the frame's independent sub-steps on separate LANES of a wave (they idle at B = 1 otherwise):
+//   * each arm map (cal_shoulderPR / cal_elbowP_and_shoulderY): the pitch (yaw) angle on lane 0, the roll (elbow)
+//     angle on lane 1 -- one radians_between + one quat_from_angle_axis instruction stream instead of two;
+//   * the scipy Euler split of each wrist: its three atan2 on lanes 0-2, then one elementary quaternion per lane;
+//   * the exp-map DOF read-out: one link per lane.
+// Every value is computed by the same device functions on the same operands as in the batched kernels (the pitch
+// angle as radians_between of the exact unit axes, which is radians_between_axes bit for bit), so the bits are the
+// batched kernels' (test_frame_server_matches_batched, test_solver_batch_invariance).
+// ----------------------------------------------------------------------------
+RTG_DEV float rdl(float v, int l) { return __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, v), l)); }
+RTG_DEV Q rdl(Q q, int l) { return Q{rdl(q.x, l), rdl(q.y, l), rdl(q.z, l), rdl(q.w, l)}; }
+RTG_DEV double rdl(double v, int l)
+{
+    const uint64_t u = __builtin_bit_cast(uint64_t, v);
+    const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)u, l);
+    const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(u >> 32), l);
+    return __builtin_bit_cast(double, ((uint64_t)hi << 32) | lo);
+}
+// shoulder_pr (SHOULDER) / elbow_py of one frame: lane 0 the first angle's quaternion, lane 1 the second's
+template <bool SHOULDER>
+RTG_DEV void arm_pair_lanes(V v1, ArmZero z0, Q parent, Q &first, Q &second)
+{
+    const int lane = threadIdx.x & 63;
+    Q q = qident();
+    if (lane < 2) {
+        const V ex{1.f, 0.f, 0.f}, ey{0.f, 1.f, 0.f}, ez{0.f, 0.f, 1.f};
+        const V pn = SHOULDER ? ey : ez;   // the plane of the first angle
+        const V v1r = qrotate(qconj(parent), v1);
+        const V v1p = proj_in_plane(v1r, pn);
+        const bool l0 = lane == 0;
+        const V a{l0 ? 1.f : v1p.x, l0 ? 0.f : v1p.y, l0 ? 0.f : v1p.z};
+        const V b = l0 ? v1p : v1r;
+        const V c = SHOULDER ? cross3(v1p, ey) : cross3(ez, v1p);
+        const V n = l0 ? pn : c;
+        const float ang = radians_between(a, b, n);
+        const V ax = l0 ? pn : (SHOULDER ? ex : ey);
+        q = qfrom_angle_unit_axis(ang - (l0 ? z0.th0 : z0.ph0), ax);
+    }
+    first = rdl(q, 0);
+    second = rdl(q, 1);
+}
+// Emit::link with a run-time link index (lane-parallel writers)
+RTG_DEV void link_rt(const Emit &E, int link, Q q)
+{
+    const int k = kHuDofAxis[link - 1];
+    E.st[(link <= 18 ? link - 12 : link - 14) * E.sst] = make_float2(q.w, k == 0 ? q.x : (k == 1 ? q.y : q.z));
+    if (E.lr) st4(E.lr + 4 * link, q);
+}
+template <int L0>
+RTG_DEV Q solve_arm_lanes(const Emit &E, V upper, V fore, ArmZero zs, ArmZero ze, Q parent)
+{
+    const int lane = threadIdx.x & 63;
+    Q p, r, y, e;
+    arm_pair_lanes<true>(upper, zs, parent, p, r);
+    if (lane == 0) { E.link<L0>(p); E.link<L0 + 1>(r); }
+    arm_pair_lanes<false>(fore, ze, qmul(qmul(parent, p), r), y, e);
+    if (lane == 0) { E.link<L0 + 2>(y); E.link<L0 + 3>(e); }
+    return qmul(qmul(qmul(p, r), y), e);
+}
+// emit_euler_xyz (quat_in_xyz_axis 'XYZ', scipy_as_euler's arithmetic) with the three atan2 on lanes 0-2 and one
+// elementary quaternion per lane
+template <int L0>
+RTG_DEV void emit_euler_xyz_lanes(const Emit &E, Q qf)
+{
+    const int lane = threadIdx.x & 63;
+    // scipy_as_euler(q, 0, 1, 2, intrinsic): i = 2, j = 1, k = 0, not symmetric, sign = (2-1)(1-0)(0-2)/2 = -1
+    double q[4] = {(double)qf.x, (double)qf.y, (double)qf.z, (double)qf.w};
+    const double nrm = sqrt(q[0] * q[0] + q[1] * q[1] + q[2] * q[2] + q[3] * q[3]);
+    q[0] /= nrm; q[1] /= nrm; q[2] /= nrm; q[3] /= nrm;
+    const int sign = -1;
+    const double qi = q[2], qj = q[1], qk = q[0];
+    const double a = q[3] - qj, b = qi + qk * sign, c = qj + q[3], d = qk * sign - qi;
+    double at = 0.0;
+    if (lane < 3) {
+        const double Y = lane == 0 ? ::hypot(c, d) : (lane == 1 ? b : d);
+        const double X = lane == 0 ? ::hypot(a, b) : (lane == 1 ? a : c);
+        at = ::atan2(Y, X);
+    }
+    double ang[3];
+    ang[1] = 2.0 * rdl(at, 0);
+    const double half_sum = rdl(at, 1), half_diff = rdl(at, 2);
+    int kase = 0;
+    if (fabs(ang[1]) <= 1e-7) kase = 1;
+    else if (fabs(ang[1] - M_PI) <= 1e-7) kase = 2;
+    if (kase == 0) {
+        ang[0] = half_sum - half_diff;
+        ang[2] = half_sum + half_diff;
+    } else {
+        ang[0] = 0.0;
+        ang[2] = kase == 1 ? 2.0 * half_sum : 2.0 * half_diff;
+    }
+    ang[2] *= sign;
+    ang[1] -= M_PI / 2.0;
+    { const double tt = ang[0]; ang[0] = ang[2]; ang[2] = tt; }
+#pragma unroll
+    for (int t = 0; t < 3; ++t) {
+        if (ang[t] < -M_PI) ang[t] += 2.0 * M_PI;
+        else if (ang[t] > M_PI) ang[t] -= 2.0 * M_PI;
+    }
+    if (lane < 3) link_rt(E, L0 + lane, elementary_quat(lane, lane == 0 ? ang[0] : (lane == 1 ? ang[1] : ang[2])));
+}
+// Emit::finalize with one slot per lane (slots s0 .. s0 + n - 1)
+RTG_DEV void finalize_lanes(const Emit &E, int s0, int n)
+{
+    const int lane = threadIdx.x & 63;
+    if (lane < n) {
+        const int j = s0 + lane;
+        const float2 v = E.st[j * E.sst];
+        const ExpDof e = exp_dof_table_part(v.x, E.ang);
+        float val = exp_dof_finish(e, v.y);
+        if (__builtin_expect(e.exact, 0)) val = normalize_angle(2.0f * cr_acos(v.x)) * (v.y / e.sin_theta);
+        E.row[j < 7 ? 11 + j : 13 + j] = val;
+    }
+}
+
+template <bool PRECISE>
+RTG_DEV void fbp_frame1_tile(const SolverConsts &C, const float *in0, const float *in1, const float *in2,
+                             float *__restrict__ dof, float *__restrict__ local_rot, float *__restrict__ body_rot)
+{
+    __shared__ float sdof[32];
+    __shared__ float4 sfit, schain[2];
+    __shared__ float2 sst[14];
+    __shared__ int sflag[3];   // R10 ready, left arm ready, right arm ready
+    const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    if (threadIdx.x < 3) sflag[threadIdx.x] = 0;
+    __syncthreads();
+    const Emit E{sdof, local_rot, C.ang_tab, sst, 1};
+    const FV<false> b{in0};
+    if (w == 0) {
+        if (lane == 0) {
+            const Q q = fbp_torso(C, b);
+            sfit = make_float4(q.x, q.y, q.z, q.w);
+        }
+        lds_signal(&sflag[0]);
+        if (lane == 0) emit_fixed_links(E);
+    } else if (w >= 3) {
+        const int side = w - 3;
+        const ArmPts ap = side ? load_arm<1>(b) : load_arm<0>(b);
+        lds_wait(&sflag[0]);
+        const float4 t = sfit;
+        const Q R10{t.x, t.y, t.z, t.w};
+        const V up = vsub(ap.el, ap.sh), fo = vsub(ap.wr, ap.el);
+        const Q ch = side ? solve_arm_lanes<21>(E, up, fo, C.rsh, C.rel, R10)
+                          : solve_arm_lanes<12>(E, up, fo, C.lsh, C.lel, R10);
+        if (lane == 0) schain[side] = make_float4(ch.x, ch.y, ch.z, ch.w);
+        lds_signal(&sflag[1 + side]);
+        finalize_lanes(E, side ? 7 : 0, 4);
+    } else {
+        const int side = w - 1;
+        const FV<false> H{side ? in2 : in1};
+        Q W = qident();
+        float a = 0.0f;
+        if (lane == 0) {
+            W = side ? fbp_wrist_fit<1>(C, H) : fbp_wrist_fit<0>(C, H);
+            const TipPts tp = load_tips(H);
+            a = hand_x_mean(qconj(W), tp.h0, tp.t);   // the gripper needs only W (:142-158 / :165-175)
+        }
+        W = rdl(W, 0);
+        lds_wait(&sflag[1 + side]);   // the arm waited for R10 first: both are visible (release / acquire chain)
+        const float4 t = sfit, c = schain[side];
+        const Q R10{t.x, t.y, t.z, t.w}, chain{c.x, c.y, c.z, c.w};
+        if (lane == 0) {
+            const int D0 = side ? 27 : 18;
+            if (PRECISE) {
+                const float sc = clamp_lohi(a / C.orig - 0.5f, 0.0f, 0.5f) / 0.5f;
+                E.row[D0] = sc * 0.044f;
+                E.row[D0 + 1] = sc * -0.044f;
+            } else {
+                const bool closed = a / C.orig < 0.7f;
+                E.row[D0] = closed ? 0.0f : 0.044f;
+                E.row[D0 + 1] = closed ? 0.0f : -0.044f;
+            }
+            if (body_rot) {   // body_global_rotation rows (:116, :172-173), as solve_fbp_side
+                st4(body_rot + 4 * (side ? 39 : 14), W);
+                if (!side)
+                    for (int j = 0; j < 59; ++j)
+                        if (j != 14 && j != 39) st4(body_rot + 4 * j, j == 10 ? R10 : qident());
+            }
+        }
+        const Q loc = qmul_norm(qconj(qmul_norm(R10, chain)), W);
+        if (side) emit_euler_xyz_lanes<25>(E, loc);
+        else emit_euler_xyz_lanes<16>(E, loc);
+        finalize_lanes(E, side ? 11 : 4, 3);
+    }
+    __syncthreads();
+    if (threadIdx.x < 30) dof[threadIdx.x] = sdof[threadIdx.x];
+}
+template <bool PRECISE>
+__global__ __launch_bounds__(320) void k_fbp_frame1(SolverConsts C, const float *__restrict__ in0,
+                                                    const float *__restrict__ in1, const float *__restrict__ in2,
+                                                    float *__restrict__ dof, float *__restrict__ local_rot,
+                                                    float *__restrict__ body_rot)
+{
+    // the frame's rows cross into LDS once, all loads in flight together (one round trip even from host memory)
+    __shared__ float sframe[184];
+    const int t = threadIdx.x;
+    if (t < 183) sframe[t] = t < 63 ? in0[t] : (t < 123 ? in1[t - 63] : in2[t - 123]);
+    __syncthreads();
+    fbp_frame1_tile<PRECISE>(C, sframe, sframe + 63, sframe + 123, dof, local_rot, body_rot);
+}
+
 template <bool PRECISE, bool SOA>
 __global__ __launch_bounds__(320) void k_fbp_latency5(SolverConsts C, const float *__restrict__ in0,
                                                       const float *__restrict__ in1, const float *__restrict__ in2,
@@ -1005,6 +1208,7 @@ __global__ __launch_bounds__(320) void k_frame_server(SolverConsts C, const floa
                                                       float *body_rot, uint32_t *ctl, uint64_t idle_ticks)
 {
     __shared__ uint32_t scmd;
+    __shared__ float sframe[184];
     uint32_t last = 0;
     if (threadIdx.x == 0) last = __hip_atomic_load(ctl + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     for (int frame = 0; frame < (1 << 30); ++frame) {
@@ -1026,7 +1230,12 @@ __global__ __launch_bounds__(320) void k_frame_server(SolverConsts C, const floa
         const uint32_t cmd = scmd;
         if (cmd == RTG_SERVER_QUIT) break;   // block-uniform
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");   // this wave's loads see the host's frame, not cached lines
-        fbp_latency5_tile<PRECISE, false>(C, in, in + 63, in + 123, 1, 0, dof, local_rot, body_rot);
+        // the frame's 183 floats cross the host link ONCE, all in flight together, into LDS; the tile's dependent
+        // loads (tips after the wrist fit, arm points after R10) then read LDS instead of host memory
+        if (threadIdx.x < 183) sframe[threadIdx.x] = in[threadIdx.x];
+        __syncthreads();
+        if (RTG_SERVER_FRAME1) fbp_frame1_tile<PRECISE>(C, sframe, sframe + 63, sframe + 123, dof, local_rot, body_rot);
+        else fbp_latency5_tile<PRECISE, false>(C, sframe, sframe + 63, sframe + 123, 1, 0, dof, local_rot, body_rot);
         __syncthreads();   // every lane of every wave has issued its output stores (a convergent point) ...
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");   // ... so this wave's release covers all of them
         __syncthreads();
@@ -1048,6 +1257,13 @@ template <int KIND, bool PRECISE, bool SOA>
 static void launch_kind(const SolverConsts &C, const float *in0, const float *in1, const float *in2,
                         const float *in3, int64_t B, float *dof, float *local_rot, float *body_rot, hipStream_t s)
 {
+    if constexpr (KIND == RTG_SOLVER_FULL_BODY_POS && RTG_FRAME1_LANES) {
+        if (B == 1) {   // at B = 1 SoA and AoS are the same memory
+            hipLaunchKernelGGL((k_fbp_frame1<PRECISE>), dim3(1), dim3(320), 0, s, C, in0, in1, in2, dof, local_rot,
+                               body_rot);
+            return;
+        }
+    }
     if constexpr (KIND == RTG_SOLVER_FULL_BODY_POS && RTG_LATENCY_WAVES == 5) {
         if (B <= RTG_LATENCY_MAX_B) {
             hipLaunchKernelGGL((k_fbp_latency5<PRECISE, SOA>), dim3(grid_for(B, kLatFrames)), dim3(320), 0, s, C,
