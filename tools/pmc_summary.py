@@ -81,7 +81,7 @@ def solver_record(SOLVER, fetch, write, sq, nt, factor, kb):
 
 def main() -> None:
     d = sys.argv[1]
-    out_path = sys.argv[2] if len(sys.argv) > 2 else "profiles/pmc_r02.json"
+    out_path = sys.argv[2] if len(sys.argv) > 2 else "profiles/pmc_r03.json"
     kb = 1024.0   # FETCH_SIZE / WRITE_SIZE are in KB
     fetch, write, sq = load(os.path.join(d, "fetch")), load(os.path.join(d, "write")), load(os.path.join(d, "sq"))
     res = {"sources": sorted(os.path.relpath(p, d) for p in glob.glob(os.path.join(d, "*", "*counter_collection.csv")))}
