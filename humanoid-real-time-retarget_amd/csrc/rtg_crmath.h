@@ -59,13 +59,12 @@ RTG_HD bool round_ok(double y, float &out)
 RTG_HD SinCos crm_sincos(double x)
 {
     SinCos r;
-    const double ax = x < 0 ? -x : x;
-    if (!(ax <= 0x1p17) || x == 0.0) {   // NaN / inf / huge: fallback; +-0: exact
-        r.s = (float)x;
-        r.c = 1.0f;
-        r.s_ok = r.c_ok = (x == 0.0);
-        return r;
-    }
+    const double ax0 = x < 0 ? -x : x;
+    // NaN / inf / huge: fallback; +-0: exact.  Selected at the end (no branch): the reduction below runs on a finite
+    // stand-in for those x and its values are discarded.
+    const bool special = !(ax0 <= 0x1p17) || x == 0.0;
+    const double x0 = x;
+    x = special ? 0.5 : x;
     // pi/2 = P1 + P2 + P3 + P3T (fdlibm pio2_1, pio2_2, pio2_3: 33 significant bits each)
     const double P1 = 1.57079632673412561417e+00, P2 = 6.07710050630396597660e-11,
                  P3 = 2.02226624871116645580e-21, P3T = 8.47842766036889956997e-32;
@@ -99,6 +98,10 @@ RTG_HD SinCos crm_sincos(double x)
     const double vc = (n == 0) ? cs : (n == 1) ? -sn : (n == 2) ? -cs : sn;
     r.s_ok = round_ok(vs, r.s);
     r.c_ok = round_ok(vc, r.c);
+    r.s = special ? (float)x0 : r.s;
+    r.c = special ? 1.0f : r.c;
+    r.s_ok = special ? (x0 == 0.0) : r.s_ok;
+    r.c_ok = special ? (x0 == 0.0) : r.c_ok;
     return r;
 }
 

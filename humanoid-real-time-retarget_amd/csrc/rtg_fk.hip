@@ -86,7 +86,11 @@ static_assert(kFkChunk == 4 || kFkChunk == 8, "window of 4 or 8 joints");
 constexpr int kRotPitch = 4 * (kFkChunk + 1);   // floats per frame row (LDS)
 constexpr int kPosPitch = 3 * kFkChunk + 1;
 
-constexpr int kPosWin = RTG_FK_POS_REGS ? 0 : kFkTile * kPosPitch;   // floats of the separate position window
+// RTG_FK_POS_WIN16: positions collect in a 16-joint LDS window and leave every second window as 192-byte row pieces
+constexpr int kPos16Pitch = 3 * 16 + 1;
+static_assert(kFkChunk == 8 || !(RTG_FK_POS_WIN16 || RTG_FK_MULTI_POS16), "the 16-joint position window pairs 8-joint windows");
+template <bool POS16>
+constexpr int pos_win() { return POS16 ? kFkTile * kPos16Pitch : (RTG_FK_POS_REGS ? 0 : kFkTile * kPosPitch); }
 
 // Branch-parent slots: the first RTG_FK_REG_SLOTS live in registers (a slot is private to its lane, and its
 // index is launch-uniform, so the choice is a scalar branch), the rest in LDS.  Every shipped skeleton needs <= 2
@@ -102,9 +106,10 @@ static inline size_t lds_slot_floats(int nslots)
 {
     return nslots > RTG_FK_REG_SLOTS ? (size_t)(nslots - RTG_FK_REG_SLOTS) * 7 * kFkTile : 0;
 }
-static inline size_t fk_stream_lds_bytes(int nslots)   // (+ RTG_FK_LDS_PAD: an occupancy experiment, fewer waves per CU)
+static inline size_t fk_stream_lds_bytes(int nslots, bool pos16 = RTG_FK_POS_WIN16)   // (+ RTG_FK_LDS_PAD: an occupancy experiment)
 {
-    return sizeof(float) * ((size_t)kFkTile * kRotPitch + (size_t)kPosWin + kCarryFloats + lds_slot_floats(nslots)) +
+    const size_t pw = pos16 ? pos_win<true>() : pos_win<false>();
+    return sizeof(float) * ((size_t)kFkTile * kRotPitch + pw + kCarryFloats + lds_slot_floats(nslots)) +
            RTG_FK_LDS_PAD;
 }
 constexpr int kDofPosWin = RTG_DOF_FK_POS_REGS ? 0 : kFkTile * kPosPitch;
@@ -196,6 +201,23 @@ RTG_DEV void chunk_store(float *__restrict__ g, const float *lds, int pitch, int
     }
 }
 
+// A window of JW joints (W floats each) of rows f0.. from LDS (row pitch `pitch`): JW lanes per frame piece.
+template <int W, int JW>
+RTG_DEV void chunk_store_n(float *__restrict__ g, const float *lds, int pitch, int64_t f0, int nfr, int J, int c0, int nC)
+{
+#pragma unroll
+    for (int it = 0; it < JW; ++it) {
+        const int v = it * kFkTile + (int)threadIdx.x;
+        const int fr = v / JW, k = v % JW;
+        if (fr < nfr && k < nC) {
+            float *gp = g + ((f0 + fr) * J + c0 + k) * W;
+            const float *lp = lds + fr * pitch + k * W;
+#pragma unroll
+            for (int c = 0; c < W; ++c) gp[c] = lp[c];
+        }
+    }
+}
+
 // Sector-aligned streaming store of one window (RTG_FK_ALIGNED_STORE).  A window's piece of a frame's output row is
 // 96 or 128 bytes at a 16-byte-aligned, not 64-byte-aligned, offset (the row stride is J x 12 / 16 bytes), so the
 // per-window store left two partly written 64-byte sectors per frame and window -- measured as 1.43x the
@@ -272,7 +294,7 @@ RTG_DEV void slot_get(const Slots &S, int s, Q &q, V &t)
 }
 static_assert(RTG_FK_REG_SLOTS >= 0 && RTG_FK_REG_SLOTS <= 2, "0..2 register slots");
 
-template <bool STATE>
+template <bool STATE, bool POS16 = RTG_FK_POS_WIN16>
 RTG_DEV void fk_stream_tile(const TopoView &T, const float *__restrict__ local_rot, const float *__restrict__ root_t,
                             int64_t B, int64_t f0, float *__restrict__ g_rot, float *__restrict__ g_pos, float *lds)
 {
@@ -280,7 +302,7 @@ RTG_DEV void fk_stream_tile(const TopoView &T, const float *__restrict__ local_r
     const int nfr = (int)((B - f0) < kFkTile ? (B - f0) : kFkTile);
     float *rot = lds;                                   // [64][kRotPitch]
     float *pos = lds + kFkTile * kRotPitch;             // [64][kPosPitch] (RTG_FK_POS_REGS: none)
-    float *carry = pos + kPosWin;                       // [2][64][16] (RTG_FK_ALIGNED_STORE)
+    float *carry = pos + pos_win<POS16>();              // [2][64][16] (RTG_FK_ALIGNED_STORE)
     Slots slots{carry + kCarryFloats, qident(), qident(), V{0.0f, 0.0f, 0.0f}, V{0.0f, 0.0f, 0.0f}};
     const int lane = threadIdx.x;
     const bool active = lane < nfr;
@@ -324,7 +346,10 @@ RTG_DEV void fk_stream_tile(const TopoView &T, const float *__restrict__ local_r
                     nt = V{rv.x + t.x, rv.y + t.y, rv.z + t.z};
                 }
                 R[4 * k] = ng.x; R[4 * k + 1] = ng.y; R[4 * k + 2] = ng.z; R[4 * k + 3] = ng.w;
-                if (RTG_FK_POS_REGS) pk[k] = nt;
+                if (POS16) {
+                    float *P16 = pos + lane * kPos16Pitch + 3 * (k + (c0 & 8));
+                    P16[0] = nt.x; P16[1] = nt.y; P16[2] = nt.z;
+                } else if (RTG_FK_POS_REGS) pk[k] = nt;
                 else { P[3 * k] = nt.x; P[3 * k + 1] = nt.y; P[3 * k + 2] = nt.z; }
                 if (!RTG_EXP_FK_COPY && ((sc >> 8) & 0xFF) != kNoSlot) slot_put(slots, (sc >> 8) & 0xFF, ng, nt);
                 g = ng;
@@ -335,6 +360,11 @@ RTG_DEV void fk_stream_tile(const TopoView &T, const float *__restrict__ local_r
         if (RTG_FK_ALIGNED_STORE) chunk_store_aligned<4>(g_rot, rot, kRotPitch, carry, f0, nfr, J, c0, nC);
         else chunk_store<4>(g_rot, rot, kRotPitch, f0, nfr, J, c0, nC);
         if (RTG_EXP_FK_NOPOS) {   // measurement knob: no position rows
+        } else if (POS16) {   // every second window (and the last): 16 joints' positions per frame piece
+            if ((c0 & 8) || c0 + nC == J) {
+                const int c16 = c0 & ~15;
+                chunk_store_n<3, 16>(g_pos, pos, kPos16Pitch, f0, nfr, J, c16, c0 + nC - c16);
+            }
         } else if (RTG_FK_POS_REGS) {   // the rotation rows are out: reuse the window for the positions
             wave_sync();
             if (active) {
@@ -365,14 +395,14 @@ __global__ __launch_bounds__(kFkTile) RTG_FK_WAVES void k_fk_stream(TopoView T, 
 
 // inverse FK, streamed the same way: local[j] = normalise(conj(g[p]) * g[j]) (kinematics.py:41-63).
 // The previous joint's global rotation stays in registers; branch parents come from slots.
-template <bool STATE>
+template <bool STATE, bool POS16 = RTG_FK_POS_WIN16>
 RTG_DEV void local_rotation_tile(const TopoView &T, const float *__restrict__ g_rot, int64_t B, int64_t f0,
                                  float *__restrict__ local_rot, float *fk_lds)
 {
     const int J = T.J;
     const int nfr = (int)((B - f0) < kFkTile ? (B - f0) : kFkTile);
     float *win = fk_lds;                                 // [64][kRotPitch]
-    float *carry = fk_lds + kFkTile * kRotPitch + kPosWin;
+    float *carry = fk_lds + kFkTile * kRotPitch + pos_win<POS16>();
     Slots slots{carry + kCarryFloats, qident(), qident(), V{0.0f, 0.0f, 0.0f},
                 V{0.0f, 0.0f, 0.0f}};   // the same LDS slot offset as fk_stream_tile
     const int lane = threadIdx.x;
@@ -433,8 +463,8 @@ __global__ __launch_bounds__(kFkTile) RTG_FK_WAVES void k_fk_multi_stream(FkMult
         if (i < A.n && (int64_t)blockIdx.x >= A.block_start[i]) s = i;
     const FkSeg &S = A.seg[s];
     const int64_t f0 = ((int64_t)blockIdx.x - A.block_start[s]) * kFkTile;
-    if (S.op == 0) fk_stream_tile<false>(S.T, S.local_rot, S.root_t, S.B, f0, S.g_rot, S.g_pos, fk_lds);
-    else local_rotation_tile<false>(S.T, S.local_rot, S.B, f0, S.g_rot, fk_lds);
+    if (S.op == 0) fk_stream_tile<false, RTG_FK_MULTI_POS16>(S.T, S.local_rot, S.root_t, S.B, f0, S.g_rot, S.g_pos, fk_lds);
+    else local_rotation_tile<false, RTG_FK_MULTI_POS16>(S.T, S.local_rot, S.B, f0, S.g_rot, fk_lds);
 }
 
 // Joint-angle FK (HuForwardModel.forward_kinematics, hu_forward_model.py:17-33): the streaming tile of
@@ -897,7 +927,7 @@ hipError_t launch_fk_multi(FkMultiArgs &A, hipStream_t s)
     for (int i = A.n; i < RTG_MAX_SEGMENTS; ++i) A.block_start[i] = blocks;
     if (blocks == 0) return hipSuccess;
     if (stream)
-        hipLaunchKernelGGL(k_fk_multi_stream, dim3((unsigned)blocks), dim3(kFkTile), fk_stream_lds_bytes(maxS), s, A);
+        hipLaunchKernelGGL(k_fk_multi_stream, dim3((unsigned)blocks), dim3(kFkTile), fk_stream_lds_bytes(maxS, RTG_FK_MULTI_POS16), s, A);
     else
         hipLaunchKernelGGL(k_fk_multi, dim3((unsigned)blocks), dim3(256), 0, s, A);
     return hipGetLastError();

@@ -67,6 +67,12 @@
 #define RTG_FK_POS_REGS 1   // 1 (measured +3-4 %, bit-exact): positions held in registers and staged through the rotation window after it is
                             //    stored (no separate position window: 12.8 instead of 19.2 KiB per wave)
 #endif
+#ifndef RTG_FK_POS_WIN16
+#define RTG_FK_POS_WIN16 0   // 1: k_fk_stream positions via a 16-joint LDS window, stored every second window (Hu FK +3 %: off)
+#endif
+#ifndef RTG_FK_MULTI_POS16
+#define RTG_FK_MULTI_POS16 1   // the mixed launch (config 5) with the 16-joint position window (measured: 151 -> 130 us, stable)
+#endif
 #ifndef RTG_FK_MIN_WAVES
 #define RTG_FK_MIN_WAVES 0   // >0: min waves per SIMD asked of the streaming FK kernels (4: <= 128 VGPRs, 16 waves/CU)
 #endif
