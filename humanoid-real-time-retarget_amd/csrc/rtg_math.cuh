@@ -644,10 +644,10 @@ RTG_DEV float la_larfg(float &alpha, float &x0, float &x1)
 {
     const float safmin = 1.17549435e-38f / 5.96046448e-08f, rsafmn = 1.0f / safmin;
     float xn = NX == 1 ? fabsf(x0) : la_lapy2(x0, x1);
-    if (xn == 0.0f) return 0.0f;
-    float beta = -__builtin_copysignf(la_lapy2(alpha, xn), alpha);
+    float beta = -__builtin_copysignf(la_lapy2(alpha, xn), alpha);   // discarded when xn == 0
     int knt = 0;
-    if (__builtin_expect(fabsf(beta) < safmin, 0)) {
+    if (__builtin_expect(xn == 0.0f || fabsf(beta) < safmin, 0)) {   // ONE rare-case branch for both cases
+        if (xn == 0.0f) return 0.0f;
         do {
             ++knt;
             x0 *= rsafmn;
