@@ -41,6 +41,9 @@
 #ifndef RTG_FRAME1_LANES
 #define RTG_FRAME1_LANES 1   // B = 1 (and the frame server): k_fbp_frame1, the frame's independent sub-steps on separate lanes
 #endif
+#ifndef RTG_GROUP_MAX_B
+#define RTG_GROUP_MAX_B 0   // 2 <= B <= this: k_fbp_group<16> (16 frames per block, 4 lanes per frame); 0: off
+#endif
 #ifndef RTG_SERVER_FRAME1
 #define RTG_SERVER_FRAME1 1   // k_frame_server runs each frame as k_fbp_frame1's tile (0: k_fbp_latency5's tile at B = 1)
 #endif

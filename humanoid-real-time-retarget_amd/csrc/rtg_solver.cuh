@@ -994,7 +994,6 @@ RTG_DEV void fbp_latency5_tile(const SolverConsts &C, const float *__restrict__ 
 // batched kernels' (test_frame_server_matches_batched, test_solver_batch_invariance).
 // ----------------------------------------------------------------------------
 RTG_DEV float rdl(float v, int l) { return __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, v), l)); }
-RTG_DEV Q rdl(Q q, int l) { return Q{rdl(q.x, l), rdl(q.y, l), rdl(q.z, l), rdl(q.w, l)}; }
 RTG_DEV double rdl(double v, int l)
 {
     const uint64_t u = __builtin_bit_cast(uint64_t, v);
@@ -1002,18 +1001,37 @@ RTG_DEV double rdl(double v, int l)
     const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(u >> 32), l);
     return __builtin_bit_cast(double, ((uint64_t)hi << 32) | lo);
 }
-// shoulder_pr (SHOULDER) / elbow_py of one frame: lane 0 the first angle's quaternion, lane 1 the second's
-template <bool SHOULDER>
+// G frames per block, L = 64 / G lanes per frame: lane = frame-in-group * L + sub.  gb<G>(v, k): sub-lane k's v of
+// this lane's frame (G == 1: v_readlane; else a shuffle inside the frame's L lanes).  Called with every lane active.
+template <int G>
+RTG_DEV float gb(float v, int k)
+{
+    if constexpr (G == 1) return rdl(v, k);
+    else return __shfl(v, (int)((threadIdx.x & 63) & ~(64 / G - 1)) + k, 64);
+}
+template <int G>
+RTG_DEV double gb(double v, int k)
+{
+    if constexpr (G == 1) return rdl(v, k);
+    else return __shfl(v, (int)((threadIdx.x & 63) & ~(64 / G - 1)) + k, 64);
+}
+template <int G>
+RTG_DEV Q gb(Q q, int k) { return Q{gb<G>(q.x, k), gb<G>(q.y, k), gb<G>(q.z, k), gb<G>(q.w, k)}; }
+template <int G>
+RTG_DEV int sub_lane() { return (int)(threadIdx.x & 63) & (64 / G - 1); }
+
+// shoulder_pr (SHOULDER) / elbow_py of one frame: sub-lane 0 the first angle's quaternion, sub-lane 1 the second's
+template <int G, bool SHOULDER>
 RTG_DEV void arm_pair_lanes(V v1, ArmZero z0, Q parent, Q &first, Q &second)
 {
-    const int lane = threadIdx.x & 63;
+    const int sub = sub_lane<G>();
     Q q = qident();
-    if (lane < 2) {
+    if (sub < 2) {
         const V ex{1.f, 0.f, 0.f}, ey{0.f, 1.f, 0.f}, ez{0.f, 0.f, 1.f};
         const V pn = SHOULDER ? ey : ez;   // the plane of the first angle
         const V v1r = qrotate(qconj(parent), v1);
         const V v1p = proj_in_plane(v1r, pn);
-        const bool l0 = lane == 0;
+        const bool l0 = sub == 0;
         const V a{l0 ? 1.f : v1p.x, l0 ? 0.f : v1p.y, l0 ? 0.f : v1p.z};
         const V b = l0 ? v1p : v1r;
         const V c = SHOULDER ? cross3(v1p, ey) : cross3(ez, v1p);
@@ -1022,8 +1040,8 @@ RTG_DEV void arm_pair_lanes(V v1, ArmZero z0, Q parent, Q &first, Q &second)
         const V ax = l0 ? pn : (SHOULDER ? ex : ey);
         q = qfrom_angle_unit_axis(ang - (l0 ? z0.th0 : z0.ph0), ax);
     }
-    first = rdl(q, 0);
-    second = rdl(q, 1);
+    first = gb<G>(q, 0);
+    second = gb<G>(q, 1);
 }
 // Emit::link with a run-time link index (lane-parallel writers)
 RTG_DEV void link_rt(const Emit &E, int link, Q q)
@@ -1032,23 +1050,23 @@ RTG_DEV void link_rt(const Emit &E, int link, Q q)
     E.st[(link <= 18 ? link - 12 : link - 14) * E.sst] = make_float2(q.w, k == 0 ? q.x : (k == 1 ? q.y : q.z));
     if (E.lr) st4(E.lr + 4 * link, q);
 }
-template <int L0>
-RTG_DEV Q solve_arm_lanes(const Emit &E, V upper, V fore, ArmZero zs, ArmZero ze, Q parent)
+template <int G, int L0>
+RTG_DEV Q solve_arm_lanes(const Emit &E, V upper, V fore, ArmZero zs, ArmZero ze, Q parent, bool live)
 {
-    const int lane = threadIdx.x & 63;
+    const bool w0 = live && sub_lane<G>() == 0;
     Q p, r, y, e;
-    arm_pair_lanes<true>(upper, zs, parent, p, r);
-    if (lane == 0) { E.link<L0>(p); E.link<L0 + 1>(r); }
-    arm_pair_lanes<false>(fore, ze, qmul(qmul(parent, p), r), y, e);
-    if (lane == 0) { E.link<L0 + 2>(y); E.link<L0 + 3>(e); }
+    arm_pair_lanes<G, true>(upper, zs, parent, p, r);
+    if (w0) { E.link<L0>(p); E.link<L0 + 1>(r); }
+    arm_pair_lanes<G, false>(fore, ze, qmul(qmul(parent, p), r), y, e);
+    if (w0) { E.link<L0 + 2>(y); E.link<L0 + 3>(e); }
     return qmul(qmul(qmul(p, r), y), e);
 }
-// emit_euler_xyz (quat_in_xyz_axis 'XYZ', scipy_as_euler's arithmetic) with the three atan2 on lanes 0-2 and one
-// elementary quaternion per lane
-template <int L0>
-RTG_DEV void emit_euler_xyz_lanes(const Emit &E, Q qf)
+// emit_euler_xyz (quat_in_xyz_axis 'XYZ', scipy_as_euler's arithmetic) with the three atan2 on sub-lanes 0-2 and one
+// elementary quaternion per sub-lane
+template <int G, int L0>
+RTG_DEV void emit_euler_xyz_lanes(const Emit &E, Q qf, bool live)
 {
-    const int lane = threadIdx.x & 63;
+    const int sub = sub_lane<G>();
     // scipy_as_euler(q, 0, 1, 2, intrinsic): i = 2, j = 1, k = 0, not symmetric, sign = (2-1)(1-0)(0-2)/2 = -1
     double q[4] = {(double)qf.x, (double)qf.y, (double)qf.z, (double)qf.w};
     const double nrm = sqrt(q[0] * q[0] + q[1] * q[1] + q[2] * q[2] + q[3] * q[3]);
@@ -1057,14 +1075,14 @@ RTG_DEV void emit_euler_xyz_lanes(const Emit &E, Q qf)
     const double qi = q[2], qj = q[1], qk = q[0];
     const double a = q[3] - qj, b = qi + qk * sign, c = qj + q[3], d = qk * sign - qi;
     double at = 0.0;
-    if (lane < 3) {
-        const double Y = lane == 0 ? ::hypot(c, d) : (lane == 1 ? b : d);
-        const double X = lane == 0 ? ::hypot(a, b) : (lane == 1 ? a : c);
+    if (sub < 3) {
+        const double Y = sub == 0 ? ::hypot(c, d) : (sub == 1 ? b : d);
+        const double X = sub == 0 ? ::hypot(a, b) : (sub == 1 ? a : c);
         at = ::atan2(Y, X);
     }
     double ang[3];
-    ang[1] = 2.0 * rdl(at, 0);
-    const double half_sum = rdl(at, 1), half_diff = rdl(at, 2);
+    ang[1] = 2.0 * gb<G>(at, 0);
+    const double half_sum = gb<G>(at, 1), half_diff = gb<G>(at, 2);
     int kase = 0;
     if (fabs(ang[1]) <= 1e-7) kase = 1;
     else if (fabs(ang[1] - M_PI) <= 1e-7) kase = 2;
@@ -1083,14 +1101,15 @@ RTG_DEV void emit_euler_xyz_lanes(const Emit &E, Q qf)
         if (ang[t] < -M_PI) ang[t] += 2.0 * M_PI;
         else if (ang[t] > M_PI) ang[t] -= 2.0 * M_PI;
     }
-    if (lane < 3) link_rt(E, L0 + lane, elementary_quat(lane, lane == 0 ? ang[0] : (lane == 1 ? ang[1] : ang[2])));
+    if (live && sub < 3) link_rt(E, L0 + sub, elementary_quat(sub, sub == 0 ? ang[0] : (sub == 1 ? ang[1] : ang[2])));
 }
-// Emit::finalize with one slot per lane (slots s0 .. s0 + n - 1)
-RTG_DEV void finalize_lanes(const Emit &E, int s0, int n)
+// Emit::finalize with one slot per sub-lane (slots s0 .. s0 + n - 1)
+template <int G>
+RTG_DEV void finalize_lanes(const Emit &E, int s0, int n, bool live)
 {
-    const int lane = threadIdx.x & 63;
-    if (lane < n) {
-        const int j = s0 + lane;
+    const int sub = sub_lane<G>();
+    if (live && sub < n) {
+        const int j = s0 + sub;
         const float2 v = E.st[j * E.sst];
         const ExpDof e = exp_dof_table_part(v.x, E.ang);
         float val = exp_dof_finish(e, v.y);
@@ -1099,53 +1118,59 @@ RTG_DEV void finalize_lanes(const Emit &E, int s0, int n)
     }
 }
 
-template <bool PRECISE>
-RTG_DEV void fbp_frame1_tile(const SolverConsts &C, const float *in0, const float *in1, const float *in2,
-                             float *__restrict__ dof, float *__restrict__ local_rot, float *__restrict__ body_rot)
+// G frames (f0 .. f0 + nfr - 1) whose rows (body 63 | left hand 60 | right hand 60 floats) are in `rows`, G x 183
+template <bool PRECISE, int G>
+RTG_DEV void fbp_group_tile(const SolverConsts &C, const float *rows, int nfr, int64_t f0, float *__restrict__ dof,
+                            float *__restrict__ local_rot, float *__restrict__ body_rot)
 {
-    __shared__ float sdof[32];
-    __shared__ float4 sfit, schain[2];
-    __shared__ float2 sst[14];
+    static_assert(G == 1 || G == 2 || G == 4 || G == 8 || G == 16, "at least 4 lanes per frame");
+    __shared__ float sdof[G * kDofStride];
+    __shared__ float4 sfit[G], schain[2][G];
+    __shared__ float2 sst[14 * G];
     __shared__ int sflag[3];   // R10 ready, left arm ready, right arm ready
     const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int g = lane / (64 / G), sub = sub_lane<G>();
+    const bool live = g < nfr, w0 = live && sub == 0;
+    const int64_t f = f0 + g;
     if (threadIdx.x < 3) sflag[threadIdx.x] = 0;
     __syncthreads();
-    const Emit E{sdof, local_rot, C.ang_tab, sst, 1};
-    const FV<false> b{in0};
+    const Emit E{sdof + g * kDofStride, live && local_rot ? local_rot + f * 124 : nullptr, C.ang_tab, sst + g, G};
+    const float *row = rows + g * 183;
+    const FV<false> b{row};
     if (w == 0) {
-        if (lane == 0) {
+        if (w0) {
             const Q q = fbp_torso(C, b);
-            sfit = make_float4(q.x, q.y, q.z, q.w);
+            sfit[g] = make_float4(q.x, q.y, q.z, q.w);
         }
         lds_signal(&sflag[0]);
-        if (lane == 0) emit_fixed_links(E);
+        if (w0) emit_fixed_links(E);
     } else if (w >= 3) {
         const int side = w - 3;
         const ArmPts ap = side ? load_arm<1>(b) : load_arm<0>(b);
         lds_wait(&sflag[0]);
-        const float4 t = sfit;
+        const float4 t = sfit[g];
         const Q R10{t.x, t.y, t.z, t.w};
         const V up = vsub(ap.el, ap.sh), fo = vsub(ap.wr, ap.el);
-        const Q ch = side ? solve_arm_lanes<21>(E, up, fo, C.rsh, C.rel, R10)
-                          : solve_arm_lanes<12>(E, up, fo, C.lsh, C.lel, R10);
-        if (lane == 0) schain[side] = make_float4(ch.x, ch.y, ch.z, ch.w);
+        const Q ch = side ? solve_arm_lanes<G, 21>(E, up, fo, C.rsh, C.rel, R10, live)
+                          : solve_arm_lanes<G, 12>(E, up, fo, C.lsh, C.lel, R10, live);
+        if (w0) schain[side][g] = make_float4(ch.x, ch.y, ch.z, ch.w);
         lds_signal(&sflag[1 + side]);
-        finalize_lanes(E, side ? 7 : 0, 4);
+        finalize_lanes<G>(E, side ? 7 : 0, 4, live);
     } else {
         const int side = w - 1;
-        const FV<false> H{side ? in2 : in1};
+        const FV<false> H{row + (side ? 123 : 63)};
         Q W = qident();
         float a = 0.0f;
-        if (lane == 0) {
+        if (w0) {
             W = side ? fbp_wrist_fit<1>(C, H) : fbp_wrist_fit<0>(C, H);
             const TipPts tp = load_tips(H);
             a = hand_x_mean(qconj(W), tp.h0, tp.t);   // the gripper needs only W (:142-158 / :165-175)
         }
-        W = rdl(W, 0);
+        W = gb<G>(W, 0);
         lds_wait(&sflag[1 + side]);   // the arm waited for R10 first: both are visible (release / acquire chain)
-        const float4 t = sfit, c = schain[side];
+        const float4 t = sfit[g], c = schain[side][g];
         const Q R10{t.x, t.y, t.z, t.w}, chain{c.x, c.y, c.z, c.w};
-        if (lane == 0) {
+        if (w0) {
             const int D0 = side ? 27 : 18;
             if (PRECISE) {
                 const float sc = clamp_lohi(a / C.orig - 0.5f, 0.0f, 0.5f) / 0.5f;
@@ -1157,32 +1182,47 @@ RTG_DEV void fbp_frame1_tile(const SolverConsts &C, const float *in0, const floa
                 E.row[D0 + 1] = closed ? 0.0f : -0.044f;
             }
             if (body_rot) {   // body_global_rotation rows (:116, :172-173), as solve_fbp_side
-                st4(body_rot + 4 * (side ? 39 : 14), W);
+                float *brow = body_rot + f * 236;
+                st4(brow + 4 * (side ? 39 : 14), W);
                 if (!side)
                     for (int j = 0; j < 59; ++j)
-                        if (j != 14 && j != 39) st4(body_rot + 4 * j, j == 10 ? R10 : qident());
+                        if (j != 14 && j != 39) st4(brow + 4 * j, j == 10 ? R10 : qident());
             }
         }
         const Q loc = qmul_norm(qconj(qmul_norm(R10, chain)), W);
-        if (side) emit_euler_xyz_lanes<25>(E, loc);
-        else emit_euler_xyz_lanes<16>(E, loc);
-        finalize_lanes(E, side ? 11 : 4, 3);
+        if (side) emit_euler_xyz_lanes<G, 25>(E, loc, live);
+        else emit_euler_xyz_lanes<G, 16>(E, loc, live);
+        finalize_lanes<G>(E, side ? 11 : 4, 3, live);
     }
     __syncthreads();
-    if (threadIdx.x < 30) dof[threadIdx.x] = sdof[threadIdx.x];
+    for (int i = threadIdx.x; i < nfr * 30; i += blockDim.x) {   // the group's contiguous DOF rows
+        const int r = i / 30;
+        dof[f0 * 30 + i] = sdof[r * kDofStride + (i - r * 30)];
+    }
 }
-template <bool PRECISE>
-__global__ __launch_bounds__(320) void k_fbp_frame1(SolverConsts C, const float *__restrict__ in0,
-                                                    const float *__restrict__ in1, const float *__restrict__ in2,
-                                                    float *__restrict__ dof, float *__restrict__ local_rot,
-                                                    float *__restrict__ body_rot)
+// The frames' rows cross into LDS once, all loads in flight together (one round trip even from host memory); SoA
+// inputs are read component-major (consecutive threads, consecutive frames).
+template <bool PRECISE, bool SOA, int G>
+__global__ __launch_bounds__(320) void k_fbp_group(SolverConsts C, const float *__restrict__ in0,
+                                                   const float *__restrict__ in1, const float *__restrict__ in2,
+                                                   int64_t B, float *__restrict__ dof, float *__restrict__ local_rot,
+                                                   float *__restrict__ body_rot)
 {
-    // the frame's rows cross into LDS once, all loads in flight together (one round trip even from host memory)
-    __shared__ float sframe[184];
-    const int t = threadIdx.x;
-    if (t < 183) sframe[t] = t < 63 ? in0[t] : (t < 123 ? in1[t - 63] : in2[t - 123]);
+    __shared__ float rows[G * 183 + 1];
+    const int64_t f0 = (int64_t)blockIdx.x * G;
+    const int nfr = (int)((B - f0) < G ? (B - f0) : G);
+    for (int t = threadIdx.x; t < G * 183; t += blockDim.x) {
+        const int g = SOA ? t % G : t / 183, e = SOA ? t / G : t % 183;
+        float v = 0.0f;
+        if (g < nfr) {
+            const int64_t fg = f0 + g;
+            if (SOA) v = e < 63 ? in0[e * B + fg] : (e < 123 ? in1[(e - 63) * B + fg] : in2[(e - 123) * B + fg]);
+            else v = e < 63 ? in0[fg * 63 + e] : (e < 123 ? in1[fg * 60 + e - 63] : in2[fg * 60 + e - 123]);
+        }
+        rows[g * 183 + e] = v;
+    }
     __syncthreads();
-    fbp_frame1_tile<PRECISE>(C, sframe, sframe + 63, sframe + 123, dof, local_rot, body_rot);
+    fbp_group_tile<PRECISE, G>(C, rows, nfr, f0, dof, local_rot, body_rot);
 }
 
 template <bool PRECISE, bool SOA>
@@ -1234,7 +1274,7 @@ __global__ __launch_bounds__(320) void k_frame_server(SolverConsts C, const floa
         // loads (tips after the wrist fit, arm points after R10) then read LDS instead of host memory
         if (threadIdx.x < 183) sframe[threadIdx.x] = in[threadIdx.x];
         __syncthreads();
-        if (RTG_SERVER_FRAME1) fbp_frame1_tile<PRECISE>(C, sframe, sframe + 63, sframe + 123, dof, local_rot, body_rot);
+        if (RTG_SERVER_FRAME1) fbp_group_tile<PRECISE, 1>(C, sframe, 1, 0, dof, local_rot, body_rot);
         else fbp_latency5_tile<PRECISE, false>(C, sframe, sframe + 63, sframe + 123, 1, 0, dof, local_rot, body_rot);
         __syncthreads();   // every lane of every wave has issued its output stores (a convergent point) ...
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");   // ... so this wave's release covers all of them
@@ -1258,9 +1298,14 @@ static void launch_kind(const SolverConsts &C, const float *in0, const float *in
                         const float *in3, int64_t B, float *dof, float *local_rot, float *body_rot, hipStream_t s)
 {
     if constexpr (KIND == RTG_SOLVER_FULL_BODY_POS && RTG_FRAME1_LANES) {
-        if (B == 1) {   // at B = 1 SoA and AoS are the same memory
-            hipLaunchKernelGGL((k_fbp_frame1<PRECISE>), dim3(1), dim3(320), 0, s, C, in0, in1, in2, dof, local_rot,
-                               body_rot);
+        if (B == 1) {   // one frame on 64 lanes per frame
+            hipLaunchKernelGGL((k_fbp_group<PRECISE, SOA, 1>), dim3(1), dim3(320), 0, s, C, in0, in1, in2, B, dof,
+                               local_rot, body_rot);
+            return;
+        }
+        if (B <= RTG_GROUP_MAX_B) {   // 16 frames per block, 4 lanes per frame
+            hipLaunchKernelGGL((k_fbp_group<PRECISE, SOA, 16>), dim3(grid_for(B, 16)), dim3(320), 0, s, C, in0, in1,
+                               in2, B, dof, local_rot, body_rot);
             return;
         }
     }

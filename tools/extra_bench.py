@@ -170,7 +170,7 @@ def sweep():
                assets.parents("vtrdyn_full"), True)
     Tf = topo("vtrdyn_full")
     res = {}
-    for B in (4096, 8192, 16384, 24576, 32768, 49152, 65536, 98304, 131072):
+    for B in (256, 1024, 2048, 4096, 8192, 16384, 24576, 32768, 49152, 65536, 98304, 131072):
         body, lh, rh = ops.synth_full_body(Tf, B, seed=7)[:3]
         dof = torch.empty((B, 30), device="cuda")
         ms = time_events(lambda: S.retarget([body, lh, rh], out_dof=dof))
