@@ -14,6 +14,11 @@
 #define RTG_SIDES_FLAGS 1   // balanced FULL_BODY_POS side kernel: per-tile LDS flags instead of the two block barriers
                             // (2: right arm before the hand-over, left wave takes more read-out -- measured 2-4% slower)
 #endif
+#ifndef RTG_SIDES_TILE_STORE
+#define RTG_SIDES_TILE_STORE 1   // balanced FULL_BODY_POS side kernel (with flags): a tile's two waves meet at an LDS
+                                 // counter instead of the block's last barrier; the second stores the tile's DOF rows
+                                 // and the first exits, freeing its wave slot for the next block
+#endif
 #ifndef RTG_SIDES_WAVES
 #define RTG_SIDES_WAVES 1   // min waves per SIMD for the side kernel (1: the compiler picks; measured best)
 #endif

@@ -639,7 +639,7 @@ extern "C" const char *rtg_build_info(void)
 {
     return "{\"abi\":" RTG_STR(RTG_ABI_VERSION) ",\"arch\":\"gfx950\",\"knobs\":{"
         RTG_KNOB(RTG_FAST_EXACT) RTG_KNOB(RTG_FAST_NORM) RTG_KNOB(RTG_SVD_DIV) RTG_KNOB(RTG_SVD_SQRT) RTG_KNOB(RTG_ANG_TAB_BITS)
-        RTG_KNOB(RTG_SOLVER_SIDES) RTG_KNOB(RTG_SIDES_REBALANCE) RTG_KNOB(RTG_SIDES_FIN_LEFT) RTG_KNOB(RTG_SIDES_FLAGS) RTG_KNOB(RTG_SIDES_WAVES)
+        RTG_KNOB(RTG_SOLVER_SIDES) RTG_KNOB(RTG_SIDES_REBALANCE) RTG_KNOB(RTG_SIDES_FIN_LEFT) RTG_KNOB(RTG_SIDES_FLAGS) RTG_KNOB(RTG_SIDES_TILE_STORE) RTG_KNOB(RTG_SIDES_WAVES)
         RTG_KNOB(RTG_PRELOAD_ARM) RTG_KNOB(RTG_PRELOAD_TIPS) RTG_KNOB(RTG_L2_PREFETCH) RTG_KNOB(RTG_LATENCY_MAX_B)
         RTG_KNOB(RTG_LATENCY_WAVES) RTG_KNOB(RTG_FRAME1_LANES) RTG_KNOB(RTG_GROUP_MAX_B) RTG_KNOB(RTG_SERVER_FRAME1) RTG_KNOB(RTG_FK_ROWS) RTG_KNOB(RTG_FK_ROWS_LDS) RTG_KNOB(RTG_DOF_FK_ROWS) RTG_KNOB(RTG_FK_LDS_PAD) RTG_KNOB(RTG_FK_CHUNK) RTG_KNOB(RTG_FK_POS_REGS) RTG_KNOB(RTG_FK_POS_WIN16) RTG_KNOB(RTG_FK_MULTI_POS16) RTG_KNOB(RTG_FK_MIN_WAVES)
         RTG_KNOB(RTG_FK_ALIGNED_STORE) RTG_KNOB(RTG_FK_REG_SLOTS) RTG_KNOB(RTG_FK_NT_STORE) RTG_KNOB(RTG_DOF_FK_POS_REGS)

@@ -564,9 +564,10 @@ __global__ __launch_bounds__(256, RTG_SIDES_WAVES) void k_solve_sides(SolverCons
     // the flag -- 2 KiB less LDS, 32.3 KiB per block, so 5 blocks (5 waves / SIMD) fit a CU's 160 KiB
     float4 *const sarm = RTG_SIDES_FLAGS ? storso : sarm_own;
 #if RTG_SIDES_FLAGS
-    __shared__ int sflag[2][2];   // per tile: [0] R10 ready (left -> right), [1] left chain ready (right -> left)
+    // per tile: [0] R10 ready (left -> right), [1] left chain ready (right -> left), [2] waves done (RTG_SIDES_TILE_STORE)
+    __shared__ int sflag[2][3];
     if (KIND == RTG_SOLVER_FULL_BODY_POS && RTG_SIDES_REBALANCE) {
-        if (threadIdx.x < 4) (&sflag[0][0])[threadIdx.x] = 0;
+        if (threadIdx.x < 6) (&sflag[0][0])[threadIdx.x] = 0;
         __syncthreads();
     }
 #endif
@@ -730,6 +731,39 @@ __global__ __launch_bounds__(256, RTG_SIDES_WAVES) void k_solve_sides(SolverCons
         E.finalize(side ? NL : 0, side ? 14 - NL : NL);
     }
     TS(8);
+#if RTG_SIDES_FLAGS && RTG_SIDES_TILE_STORE
+    if (KIND == RTG_SOLVER_FULL_BODY_POS && RTG_SIDES_REBALANCE) {
+        // The tile's two waves meet at an LDS counter instead of the block barrier: the first to arrive exits (its
+        // VGPRs free for the next block, whose LDS already fits beside this one's), the second stores the tile's rows.
+        // The side programs are unequal (the left wave runs two SVDs, the right one SVD and both arm chains), so
+        // one wave of each tile used to idle at the barrier.  acq_rel: the first wave's sdof writes are visible to
+        // the second wave's reads below.
+        const int lane = threadIdx.x & 63;
+        int prev = 0;
+        if (lane == 0)
+            prev = __hip_atomic_fetch_add(&sflag[w >> 1][2], 1, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_WORKGROUP);
+        if (__builtin_amdgcn_readfirstlane(prev) == 0) return;   // wave-uniform: lane 0 is active here
+        TS(9);
+        const int64_t t0 = f0 + (w >> 1) * 64;
+        const int64_t nrows = (B - t0) < 64 ? (B - t0) : 64;
+        if (nrows <= 0) return;
+        const int nvals = (int)nrows * 30;
+        float *dst = dof + t0 * 30;   // (f0 + 64 t) * 120 bytes: 16-byte aligned
+        const float *src = sdof + (w >> 1) * 64 * kDofStride;
+        auto at = [&](int i) {
+            const int rr = i / 30;
+            return src[rr * kDofStride + (i - rr * 30)];
+        };
+        const int nvec = nvals >> 2;
+        for (int v = lane; v < nvec; v += 64) {
+            const int i = v << 2;
+            *reinterpret_cast<float4 *>(dst + i) = make_float4(at(i), at(i + 1), at(i + 2), at(i + 3));
+        }
+        for (int i = (nvec << 2) + lane; i < nvals; i += 64) dst[i] = at(i);
+        TS(12);
+        return;
+    }
+#endif
     __syncthreads();
     TS(9);
     const int64_t nrows = (B - f0) < kSideFrames ? (B - f0) : kSideFrames;

@@ -1,7 +1,7 @@
 #!/usr/bin/env bash
 # PMC passes over a short bench run, one rocprofv3 run per pass (gfx950 slot limits:
 # <= 8 SQ counters per pass).  Output: gpurun_out/pmc_<tag>_<pass>/...
-# usage: tools/pmc_passes.sh <tag> [pass ...]   (passes: sq valu misc; default all)
+# usage: tools/pmc_passes.sh <tag> [pass ...]   (passes: sq valu misc icache; default all)
 set -eu
 tag=${1:-r01}
 shift || true
@@ -21,5 +21,6 @@ for p in $passes; do
           SQ_INSTS_VALU_ADD_F32 SQ_INSTS_VALU_MUL_F32 SQ_INSTS_VALU_FMA_F32 SQ_INSTS_VALU_TRANS_F32 ;;
     misc) run misc SQ_INSTS_VALU_INT32 SQ_INSTS_VALU_INT64 SQ_INSTS_VALU_CVT SQ_INSTS_VMEM_RD SQ_INSTS_LDS \
           SQ_INSTS_BRANCH SQ_INSTS_SMEM SQ_BUSY_CYCLES ;;
+    icache) run icache SQC_ICACHE_HITS SQC_ICACHE_MISSES SQ_IFETCH SQ_WAVE_CYCLES SQ_WAIT_INST_ANY SQ_WAVES ;;
   esac
 done
