@@ -122,6 +122,17 @@ def barrier(world, backend=None):
         torch.cuda.synchronize()
 
 
+def rocm_smi_clocks(dev: int):
+    """Current sclk / mclk as rocm-smi reports them for this device (None when rocm-smi is unavailable)."""
+    try:
+        r = subprocess.run(["rocm-smi", "-d", str(dev), "--showclocks", "--json"], capture_output=True, text=True,
+                           timeout=30)
+        card = next(iter(json.loads(r.stdout).values()))
+        return {k: v for k, v in card.items() if "sclk" in k or "mclk" in k}
+    except Exception:  # noqa: BLE001
+        return None
+
+
 def cpu_share() -> int:
     """CPUs this process may use: the affinity mask, capped by a cgroup v2 CPU quota (the GPU box exposes the
     whole machine in os.cpu_count() but grants one GPU's share of it)."""
@@ -449,6 +460,14 @@ class DeviceBackend:
     def sync(self):
         self.torch.cuda.synchronize()
 
+    def probe(self):
+        """rtg_box_probe: the shader clock under load, f32 FMA rate and HBM copy bandwidth of this GPU right now,
+        plus the clocks rocm-smi reports (kept in the line so numbers from different boxes can be compared)."""
+        from rtg import ops
+        rec = ops.box_probe()
+        rec["rocm_smi"] = rocm_smi_clocks(self.dev.index)
+        return rec
+
     def start(self):
         # kernel time: one HIP event pair around the K launches on the launch stream (a pair per launch would add
         # each event's own packet and cache release to every launch, ~10 us, which rocprofv3's trace does not see)
@@ -482,6 +501,8 @@ def rank_flow(world, rank, backend, B, steps, warmup, ring):
         b, l, r_ = backend.synth(topo, B, 1234 + rank, r * B)
         sets.append((b, l, r_, backend.new_dof(B)))
     backend.sync()
+    probe = getattr(backend, "probe", None)   # the box's clock and bandwidth, measured before the timed region
+    box = {"before": probe()} if probe is not None else None
     for i in range(warmup):
         b, l, r_, d = sets[i % ring]
         backend.solve(solver, b, l, r_, d)
@@ -514,8 +535,10 @@ def rank_flow(world, rank, backend, B, steps, warmup, ring):
                                        backend.comm_device)
         per_rank = [{"rank": r, "frames": gold["frames"], "max_abs_err": v[0], "frac_frames_le_1e-5": v[1],
                      "kern_ms": v[2]} for r, v in enumerate(vals)]
+    if box is not None:
+        box["after"] = probe()
     out = {"wall": wall, "kern_ms": kern_ms, "frames": world * B * steps, "sets": sets, "topo": topo,
-           "solver": solver, "zl": lt, "zg": zg, "parents": parents, "golden_per_rank": per_rank}
+           "solver": solver, "zl": lt, "zg": zg, "parents": parents, "golden_per_rank": per_rank, "box": box}
     if world > 1:   # final DOF gather to rank 0 (untimed region, reported separately)
         d = sets[(steps - 1) % ring][3]
         backend.sync()
@@ -570,6 +593,7 @@ def main():
                          "compute": compute_roofline(rec, kern_ms)},
         }
         line["golden_per_rank"] = res["golden_per_rank"]
+        line["box"] = res["box"]
         if "gather_ms" in res:
             line["gather_ms"] = res["gather_ms"]
         from rtg import ops

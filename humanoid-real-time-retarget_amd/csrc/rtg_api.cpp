@@ -11,6 +11,7 @@
 #include <ctime>
 #include <new>
 #include <string>
+#include <utility>
 
 #include "rtg_kernels.cuh"
 
@@ -40,6 +41,7 @@ struct rtg_solver_s {
     int precise = 0;
     SolverConsts consts{};
     uint32_t *d_ang_tab = nullptr;   // exp-map angle table (consts.ang_tab), device of creation
+    uint32_t *h_err = nullptr;       // the device error word (consts.err is its device alias), pinned host memory
 };
 
 namespace {
@@ -444,30 +446,55 @@ int rtg_solver_create(int kind, const float *zl, const float *zg, const int32_t 
         return rc;
     }
     C.ang_tab = tab;
-    rtg_solver_s *s = new (std::nothrow) rtg_solver_s();
+    // the error word: host-mapped, so the device's report is read on the next call without a HIP call
+    uint32_t *h_err = nullptr;
+    rc = hip_check(hipHostMalloc(reinterpret_cast<void **>(&h_err), sizeof(uint32_t), hipHostMallocMapped),
+                   "hipHostMalloc(error word)");
+    if (rc == RTG_OK) {
+        *h_err = 0;
+        rc = hip_check(hipHostGetDevicePointer(reinterpret_cast<void **>(&C.err), h_err, 0), "hipHostGetDevicePointer");
+    }
+    rtg_solver_s *s = rc == RTG_OK ? new (std::nothrow) rtg_solver_s() : nullptr;
     if (!s) {
         (void)hipFree(tab);
-        return fail(RTG_ERR_OUT_OF_MEMORY, "rtg_solver_create: host allocation failed");
+        if (h_err) (void)hipHostFree(h_err);
+        return rc != RTG_OK ? rc : fail(RTG_ERR_OUT_OF_MEMORY, "rtg_solver_create: host allocation failed");
     }
     s->kind = kind;
     s->precise = precise_gripper ? 1 : 0;
     s->consts = C;
     s->d_ang_tab = tab;
+    s->h_err = h_err;
     *out = s;
     return RTG_OK;
 }
 
 int rtg_solver_destroy(rtg_solver_t s)
 {
-    if (s) (void)hipFree(s->d_ang_tab);
+    if (s) {
+        (void)hipFree(s->d_ang_tab);
+        if (s->h_err) (void)hipHostFree(s->h_err);
+    }
     delete s;
     return RTG_OK;
+}
+
+// A device error a previous launch of this solver reported (rtg.h RTG_DEVERR_*): returned once, then cleared.
+static int take_device_error(uint32_t *word, const char *fn)
+{
+    const uint32_t e = word ? __atomic_exchange_n(word, 0u, __ATOMIC_ACQ_REL) : 0u;
+    if (e == 0) return RTG_OK;
+    return fail(RTG_ERR_DEVICE, "%s: a previous launch reported device error 0x%x%s", fn, e,
+                (e & RTG_DEVERR_HANDOVER_TIMEOUT) ? " (a wave hand-over timed out: that launch's outputs are not valid)"
+                                                  : "");
 }
 
 int rtg_retarget_f32(rtg_solver_t s, const float *in0, const float *in1, const float *in2, const float *in3,
                      int64_t B, int layout, float *dof, float *local_rot, float *body_rot, rtg_stream_t stream)
 {
     if (!s) return fail(RTG_ERR_INVALID_ARGUMENT, "rtg_retarget_f32: NULL solver");
+    int rc = take_device_error(s->h_err, "rtg_retarget_f32");
+    if (rc != RTG_OK) return rc;
     if (B < 0) return fail(RTG_ERR_INVALID_ARGUMENT, "rtg_retarget_f32: negative batch");
     if (layout != RTG_LAYOUT_AOS && layout != RTG_LAYOUT_SOA)
         return fail(RTG_ERR_INVALID_ARGUMENT, "rtg_retarget_f32: bad layout %d", layout);
@@ -530,7 +557,7 @@ int rtg_frame_server_post(uint32_t *ctl, uint32_t seq, float *in, const float *b
     if (dof_dst) std::memcpy(dof_dst, dof, 30 * sizeof(float));
     if (local_rot_dst) std::memcpy(local_rot_dst, local_rot, 124 * sizeof(float));
     if (body_rot_dst) std::memcpy(body_rot_dst, body_rot, 236 * sizeof(float));
-    return RTG_OK;
+    return take_device_error(ctl + 3, "rtg_frame_server_post");
 }
 
 // ---------------------------------------------------------------- primitives
@@ -635,6 +662,68 @@ int rtg_angular_velocity_f32(const float *r, int64_t nseq, int64_t L, int64_t J,
     if (rc != RTG_OK) return rc;
     RTG_TRY(launch_angular_velocity(r, nseq, L, J, dt, w ? &taps : nullptr, tmp, out, as_stream(stream)), "k_angular_raw");
     return RTG_OK;
+}
+
+// ---------------------------------------------------------------- box probe
+int rtg_box_probe(double *out, int32_t n_out, rtg_stream_t stream)
+{
+    if (!out || n_out < RTG_PROBE_FIELDS)
+        return fail(RTG_ERR_INVALID_ARGUMENT, "rtg_box_probe: out needs %d doubles", RTG_PROBE_FIELDS);
+    hipStream_t s = as_stream(stream);
+    int dev = 0;
+    hipDeviceProp_t prop{};
+    RTG_TRY(hipGetDevice(&dev), "hipGetDevice");
+    RTG_TRY(hipGetDeviceProperties(&prop, dev), "hipGetDeviceProperties");
+    const int nblk = prop.multiProcessorCount * 8;   // 8 workgroups of 4 waves per CU: 8 waves per SIMD
+    const int nrec = (nblk + 63) / 64;
+    const int64_t nf4 = (int64_t)1 << 26;             // 1 GiB per buffer: far beyond the 256 MiB Infinity Cache
+    float *src = nullptr, *dst = nullptr;
+    uint64_t *clk = nullptr;
+    hipEvent_t e0 = nullptr, e1 = nullptr;
+    int rc = hip_check(hipMalloc(&src, nf4 * 16), "hipMalloc(probe)");
+    if (rc == RTG_OK) rc = hip_check(hipMalloc(&dst, nf4 * 16), "hipMalloc(probe)");
+    if (rc == RTG_OK) rc = hip_check(hipMalloc(&clk, nrec * 2 * sizeof(uint64_t)), "hipMalloc(probe)");
+    if (rc == RTG_OK) rc = hip_check(hipEventCreate(&e0), "hipEventCreate");
+    if (rc == RTG_OK) rc = hip_check(hipEventCreate(&e1), "hipEventCreate");
+    if (rc == RTG_OK) rc = hip_check(hipMemsetAsync(src, 0, nf4 * 16, s), "hipMemsetAsync");
+    float best_valu = 1e30f, best_copy = 1e30f, ms = 0.0f;
+    for (int rep = 0; rc == RTG_OK && rep < 4; ++rep) {   // rep 0 warms up; the best of the other three counts
+        rc = hip_check(hipEventRecord(e0, s), "hipEventRecord");
+        if (rc == RTG_OK) rc = hip_check(launch_probe_valu(nblk, dst, clk, s), "k_probe_valu");
+        if (rc == RTG_OK) rc = hip_check(hipEventRecord(e1, s), "hipEventRecord");
+        if (rc == RTG_OK) rc = hip_check(hipEventSynchronize(e1), "hipEventSynchronize");
+        if (rc == RTG_OK) rc = hip_check(hipEventElapsedTime(&ms, e0, e1), "hipEventElapsedTime");
+        if (rc == RTG_OK && rep > 0 && ms < best_valu) best_valu = ms;
+        if (rc == RTG_OK) rc = hip_check(hipEventRecord(e0, s), "hipEventRecord");
+        if (rc == RTG_OK) rc = hip_check(launch_probe_copy(src, dst, nf4, s), "k_probe_copy");
+        if (rc == RTG_OK) rc = hip_check(hipEventRecord(e1, s), "hipEventRecord");
+        if (rc == RTG_OK) rc = hip_check(hipEventSynchronize(e1), "hipEventSynchronize");
+        if (rc == RTG_OK) rc = hip_check(hipEventElapsedTime(&ms, e0, e1), "hipEventElapsedTime");
+        if (rc == RTG_OK && rep > 0 && ms < best_copy) best_copy = ms;
+    }
+    uint64_t h[2 * 64] = {};
+    const int nr = nrec < 64 ? nrec : 64;
+    if (rc == RTG_OK) rc = hip_check(hipMemcpy(h, clk, nr * 2 * sizeof(uint64_t), hipMemcpyDeviceToHost), "hipMemcpy");
+    if (rc == RTG_OK) {
+        double mhz[64];   // shader cycles per 100 MHz tick of each recording workgroup (the last rep), median
+        int m = 0;
+        for (int i = 0; i < nr; ++i)
+            if (h[2 * i + 1] > 0) mhz[m++] = 100.0 * (double)h[2 * i] / (double)h[2 * i + 1];
+        for (int i = 1; i < m; ++i)
+            for (int j = i; j > 0 && mhz[j - 1] > mhz[j]; --j) std::swap(mhz[j - 1], mhz[j]);
+        out[0] = m ? mhz[m / 2] : 0.0;
+        out[1] = (double)nblk * 256 * probe_valu_iters() * 8 / (best_valu * 1e-3) / 1e12;
+        out[2] = 2.0 * (double)nf4 * 16 / (best_copy * 1e-3) / 1e9;
+        out[3] = best_valu;
+        out[4] = best_copy;
+        out[5] = prop.multiProcessorCount;
+    }
+    (void)hipFree(src);
+    (void)hipFree(dst);
+    (void)hipFree(clk);
+    if (e0) (void)hipEventDestroy(e0);
+    if (e1) (void)hipEventDestroy(e1);
+    return rc;
 }
 
 // ---------------------------------------------------------------- synthetic input

@@ -37,6 +37,8 @@ struct SolverConsts {
     float orig;       // their mean (gripper denominator), filled by k_solver_prep
     int32_t par[4];   // BODY_ROT: parents of joints 18, 14, 19, 15
     const uint32_t *ang_tab;   // exp-map angle table (kAngTabWords words, device), owned by the solver handle
+    uint32_t *err;             // host-mapped error word of the solver handle: a wave hand-over that timed out ORs
+                               // RTG_DEVERR_HANDOVER_TIMEOUT in (rtg_retarget_f32 reports it on the next call)
 };
 
 // Joint-angle forward model (HuForwardModel): per-DOF axis and optional limits, device memory.
@@ -98,5 +100,8 @@ hipError_t launch_angular_velocity(const float *r, int64_t nseq, int64_t L, int6
                                    const GaussTaps *taps, float *tmp, float *out, hipStream_t s);
 hipError_t launch_synth_full_body(const TopoView &T, uint64_t seed, int64_t off, int64_t B, float *body, float *lh,
                                   float *rh, float *body_rot, int layout, hipStream_t s);
+hipError_t launch_probe_valu(int nblocks, float *sink, uint64_t *clk, hipStream_t s);
+hipError_t launch_probe_copy(const float *src, float *dst, int64_t nfloat4, hipStream_t s);
+int probe_valu_iters();
 
 }  // namespace rtg

@@ -1,60 +1,26 @@
 // rtg_knobs.h -- every compile-time knob of librtg_hip.so with its product default, in one place: each kernel
-// TU sees the same values, and rtg_build_info() (rtg_ops.hip) reports them.  RTG_EXP_* are measurement-only;
-// STUB_SVD / NO_TABLE / HOT_INPUTS change results and the Python binding refuses a library built with them.
+// TU sees the same values, and rtg_build_info() (rtg_ops.hip) reports them.  A knob here either selects a shipped
+// path or builds a measurement variant (tools/build_variants.sh).  RTG_EXP_* are measurement-only, and those that
+// change results (RTG_WRONG_ANSWER_KNOBS in rtg_ops.hip) make the Python binding refuse the library.  Variants
+// measured and rejected are gone from the source; DESIGN.md keeps their numbers and git history their code.
 #pragma once
 
 // ---- used by rtg_solver.cuh
-#ifndef RTG_SIDES_REBALANCE
-#define RTG_SIDES_REBALANCE 1   // FULL_BODY_POS side kernel: the right wave also runs the LEFT arm chain (it needs only
-#endif                          // R10) while the left wave runs the left wrist fit -- 1.5 SVD-equivalents per wave
-#ifndef RTG_SIDES_FIN_LEFT
-#define RTG_SIDES_FIN_LEFT 7    // exp-map slots (of 14) the left wave reads out in the balanced kernel (7, 8, 9: within noise)
-#endif
-#ifndef RTG_SIDES_FLAGS
-#define RTG_SIDES_FLAGS 1   // balanced FULL_BODY_POS side kernel: per-tile LDS flags instead of the two block barriers
-                            // (2: right arm before the hand-over, left wave takes more read-out -- measured 2-4% slower)
-#endif
-#ifndef RTG_SIDES_TILE_STORE
-#define RTG_SIDES_TILE_STORE 1   // balanced FULL_BODY_POS side kernel (with flags): a tile's two waves meet at an LDS
-                                 // counter instead of the block's last barrier; the second stores the tile's DOF rows
-                                 // and the first exits, freeing its wave slot for the next block
-#endif
 #ifndef RTG_SIDES_WAVES
 #define RTG_SIDES_WAVES 1   // min waves per SIMD for the side kernel (1: the compiler picks; measured best)
 #endif
-#ifndef RTG_EXP_HOT_INPUTS
-#define RTG_EXP_HOT_INPUTS 0
-#endif
-#ifndef RTG_SOLVER_SIDES
-#define RTG_SOLVER_SIDES 1   // 0: always the fused one-lane-per-frame kernels (k_retarget), for comparison
-#endif
-#ifndef RTG_L2_PREFETCH
-#define RTG_L2_PREFETCH 0    // 1: each side wave pulls the input rows it reads late into L2 at kernel start
-#endif
-#ifndef RTG_PRELOAD_ARM
-#define RTG_PRELOAD_ARM 1    // (measured -4 %) 1: a side's arm points load at kernel start, with the torso / wrist-fit loads
-#endif
-#ifndef RTG_PRELOAD_TIPS
-#define RTG_PRELOAD_TIPS 0   // 1: the gripper's hand points load with the wrist-fit points
-#endif
 #ifndef RTG_LATENCY_MAX_B
-#define RTG_LATENCY_MAX_B 49152   // batches up to this size use the latency kernel (swept: faster up to 49152, slower at 65536)
+#define RTG_LATENCY_MAX_B 49152   // 2 <= B <= this: k_fbp_latency5 (swept: faster up to 49152, slower at 65536)
+#endif
+#ifndef RTG_EXP_HOT_INPUTS
+#define RTG_EXP_HOT_INPUTS 0   // measurement knob: every side-kernel tile reads the first block's rows (wrong answers)
 #endif
 #ifndef RTG_EXP_TIMESTAMPS
-#define RTG_EXP_TIMESTAMPS 0   // measurement knob: block 0's lane 0 of each wave records the 100 MHz wall clock at
-#endif                         // each phase into body_rot (as u32 pairs) -- wrong body_rot, tools/latency_phases.py
-#ifndef RTG_FRAME1_LANES
-#define RTG_FRAME1_LANES 1   // B = 1 (and the frame server): k_fbp_frame1, the frame's independent sub-steps on separate lanes
-#endif
-#ifndef RTG_GROUP_MAX_B
-#define RTG_GROUP_MAX_B 0   // 2 <= B <= this: k_fbp_group<16> (16 frames per block, 4 lanes per frame); 0: off
-#endif
-#ifndef RTG_SERVER_FRAME1
-#define RTG_SERVER_FRAME1 1   // k_frame_server runs each frame as k_fbp_frame1's tile (0: k_fbp_latency5's tile at B = 1)
-#endif
-#ifndef RTG_LATENCY_WAVES
-#define RTG_LATENCY_WAVES 5   // 5: k_fbp_latency5 (arm chain concurrent with the wrist fits); 3: k_fbp_latency
-#endif
+#define RTG_EXP_TIMESTAMPS 0   // measurement knob: lane 0 of each wave records the 100 MHz wall clock at each phase
+#endif                         // into body_rot (as u32 pairs) -- wrong body_rot, tools/latency_phases.py / side_phases.py
+#ifndef RTG_EXP_SKIP_SIGNAL
+#define RTG_EXP_SKIP_SIGNAL 0   // measurement knob: block 0's first R10 hand-over is never raised, so its partner wave
+#endif                          // times out (tests the RTG_DEVERR_HANDOVER_TIMEOUT report; wrong answers)
 // ---- used by rtg_fk.hip
 #ifndef RTG_FK_ROWS
 #define RTG_FK_ROWS 0   // 1: row-staged FK / inverse FK / DOF FK (whole tile rows through LDS, contiguous 1 KiB stores); 0: windowed streaming

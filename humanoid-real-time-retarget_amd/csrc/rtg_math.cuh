@@ -1096,8 +1096,11 @@ RTG_DEV void kabsch_rot(const float A[9], float R[9])
 struct NoHook {
     RTG_DEV void operator()(int) const {}
 };
+// `svd_nan` is set when A has a NaN entry: torch.linalg.svd refuses such a matrix (LAPACK sgesdd returns info = -4
+// on a NaN norm and torch raises "linalg.svd: ... contained non-finite values", transform3d.py:40), so the reference
+// frame raises there (an inf entry alone does not raise).
 template <int N, typename Hook = NoHook>
-RTG_DEV Q cal_joint_quat(const V (&Z)[N], const V (&M)[N], const Hook &hook = Hook{})
+RTG_DEV Q cal_joint_quat(const V (&Z)[N], const V (&M)[N], bool &svd_nan, const Hook &hook = Hook{})
 {
     float A[9];
 #pragma unroll
@@ -1114,20 +1117,33 @@ RTG_DEV Q cal_joint_quat(const V (&Z)[N], const V (&M)[N], const Hook &hook = Ho
             }
             A[i * 3 + k] = acc;
         }
+    bool nan = false;
+#pragma unroll
+    for (int i = 0; i < 9; ++i) nan |= A[i] != A[i];
+    svd_nan = nan;
     hook(0);
     float R[9];
     kabsch_rot(A, R);
     hook(1);
     return qfrom_rotmat(R);
 }
+template <int N, typename Hook = NoHook>
+RTG_DEV Q cal_joint_quat(const V (&Z)[N], const V (&M)[N], const Hook &hook = Hook{})
+{
+    bool unused;
+    return cal_joint_quat<N>(Z, M, unused, hook);
+}
 
 // ------------------------------------------------ scipy Rotation (float64)
 // from_quat(q).as_euler(seq): quaternion method of Bernardes & Viollet (2022),
-// as scipy 1.15 implements it; seq given as axis indices + intrinsic flag.
-RTG_DEV void scipy_as_euler(Q qf, int s0, int s1, int s2, bool extrinsic, double ang[3])
+// as scipy 1.15 implements it; seq given as axis indices + intrinsic flag.  Returns true when from_quat would
+// refuse q: its float64 norm is not > 0 (all four components zero, or a NaN) -- scipy raises
+// "ValueError: Found zero norm quaternions in `quat`." there (transform3d.py:53).
+RTG_DEV bool scipy_as_euler(Q qf, int s0, int s1, int s2, bool extrinsic, double ang[3])
 {
     double q[4] = {(double)qf.x, (double)qf.y, (double)qf.z, (double)qf.w};
     const double nrm = sqrt(q[0] * q[0] + q[1] * q[1] + q[2] * q[2] + q[3] * q[3]);
+    const bool refused = !(nrm > 0.0);
     q[0] /= nrm; q[1] /= nrm; q[2] /= nrm; q[3] /= nrm;
     int i = extrinsic ? s0 : s2, j = s1, k = extrinsic ? s2 : s0;
     const bool symmetric = i == k;
@@ -1167,6 +1183,7 @@ RTG_DEV void scipy_as_euler(Q qf, int s0, int s1, int s2, bool extrinsic, double
         if (ang[t] < -M_PI) ang[t] += 2.0 * M_PI;
         else if (ang[t] > M_PI) ang[t] -= 2.0 * M_PI;
     }
+    return refused;
 }
 
 // from_euler(axis, angle).as_quat() for one elementary rotation, cast to float32
@@ -1178,14 +1195,15 @@ RTG_DEV Q elementary_quat(int axis, double angle)
     return Q{axis == 0 ? s : 0.0f, axis == 1 ? s : 0.0f, axis == 2 ? s : 0.0f, c};
 }
 
-// quat_in_xyz_axis (transform3d.py:52-59)
-RTG_DEV void quat_in_xyz_axis(Q q, int s0, int s1, int s2, bool extrinsic, Q out[3])
+// quat_in_xyz_axis (transform3d.py:52-59); true where the reference raises (scipy_as_euler)
+RTG_DEV bool quat_in_xyz_axis(Q q, int s0, int s1, int s2, bool extrinsic, Q out[3])
 {
     double ang[3];
-    scipy_as_euler(q, s0, s1, s2, extrinsic, ang);
+    const bool refused = scipy_as_euler(q, s0, s1, s2, extrinsic, ang);
     out[0] = elementary_quat(s0, ang[0]);
     out[1] = elementary_quat(s1, ang[1]);
     out[2] = elementary_quat(s2, ang[2]);
+    return refused;
 }
 
 // ------------------------------------------------ arm joint maps

@@ -328,9 +328,10 @@ __global__ __launch_bounds__(256) void k_quat_as_euler(const float *__restrict__
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
     double ang[3];
-    scipy_as_euler(ld4(q + 4 * i), s0, s1, s2, extrinsic != 0, ang);
+    const bool refused = scipy_as_euler(ld4(q + 4 * i), s0, s1, s2, extrinsic != 0, ang);
+    const double marked = __builtin_bit_cast(double, 0x7FF8000000000000ull | RTG_FRAME_ZERO_NORM_QUAT);
 #pragma unroll
-    for (int t = 0; t < 3; ++t) out[3 * i + t] = degrees ? ang[t] * (180.0 / M_PI) : ang[t];   // np.rad2deg
+    for (int t = 0; t < 3; ++t) out[3 * i + t] = refused ? marked : (degrees ? ang[t] * (180.0 / M_PI) : ang[t]);   // np.rad2deg
 }
 
 template <int N>
@@ -345,7 +346,10 @@ __global__ __launch_bounds__(256) void k_cal_joint_quat(const float *__restrict_
         z[j] = ld3(Z + (i * N + j) * 3);
         m[j] = ld3(M + (i * N + j) * 3);
     }
-    st4(out + 4 * i, cal_joint_quat<N>(z, m));
+    bool svd_nan;
+    const Q q = cal_joint_quat<N>(z, m, svd_nan);
+    const float marked = __builtin_bit_cast(float, RTG_FRAME_NAN | RTG_FRAME_SVD_NONFINITE);
+    st4(out + 4 * i, svd_nan ? Q{marked, marked, marked, marked} : q);
 }
 
 __global__ __launch_bounds__(256) void k_quat_in_xyz_axis(const float *__restrict__ q, int s0, int s1, int s2,
@@ -354,9 +358,10 @@ __global__ __launch_bounds__(256) void k_quat_in_xyz_axis(const float *__restric
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
     Q e[3];
-    quat_in_xyz_axis(ld4(q + 4 * i), s0, s1, s2, extrinsic != 0, e);
+    const bool refused = quat_in_xyz_axis(ld4(q + 4 * i), s0, s1, s2, extrinsic != 0, e);
+    const float marked = __builtin_bit_cast(float, RTG_FRAME_NAN | RTG_FRAME_ZERO_NORM_QUAT);
 #pragma unroll
-    for (int t = 0; t < 3; ++t) st4(out + (i * 3 + t) * 4, e[t]);
+    for (int t = 0; t < 3; ++t) st4(out + (i * 3 + t) * 4, refused ? Q{marked, marked, marked, marked} : e[t]);
 }
 
 // ----------------------------------------------------------------------------
@@ -622,12 +627,65 @@ hipError_t launch_synth_full_body(const TopoView &T, uint64_t seed, int64_t off,
     return hipGetLastError();
 }
 
+// ----------------------------------------------------------------------------
+// box probe (rtg.h rtg_box_probe): what this GPU delivers right now, so a throughput number from one box can be
+// set against another's.  k_probe_valu keeps every SIMD busy with independent f32 FMA chains; one lane of
+// every 64th workgroup reads the shader-cycle counter and the 100 MHz wall clock around its own loop, so
+// cycles / wall time is the shader clock under load.  k_probe_copy streams a buffer (16 B per lane per
+// access, a grid-stride loop) into another: HBM copy bandwidth.
+// ----------------------------------------------------------------------------
+constexpr int kProbeIters = 4096;
+__global__ __launch_bounds__(256) void k_probe_valu(float seed, float *__restrict__ sink, uint64_t *__restrict__ clk)
+{
+    float a[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) a[k] = seed + (float)(threadIdx.x + k);
+    const bool rec = (blockIdx.x & 63) == 0 && threadIdx.x == 0;
+    uint64_t c0 = 0, w0 = 0;
+    if (rec) {
+        c0 = clock64();
+        w0 = wall_clock64();
+    }
+    for (int i = 0; i < kProbeIters; ++i) {
+#pragma unroll
+        for (int k = 0; k < 8; ++k) a[k] = __builtin_fmaf(a[k], 0.999999f, 1e-7f);
+    }
+    if (rec) {
+        const uint64_t c1 = clock64(), w1 = wall_clock64();
+        clk[2 * (blockIdx.x >> 6)] = c1 - c0;
+        clk[2 * (blockIdx.x >> 6) + 1] = w1 - w0;
+    }
+    float s = 0.0f;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) s += a[k];
+    if (s == 12345.678f) sink[threadIdx.x] = s;   // never true; keeps the chains alive
+}
+__global__ __launch_bounds__(256) void k_probe_copy(const float4 *__restrict__ src, float4 *__restrict__ dst,
+                                                    int64_t n)
+{
+    for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) dst[i] = src[i];
+}
+
+hipError_t launch_probe_valu(int nblocks, float *sink, uint64_t *clk, hipStream_t s)
+{
+    hipLaunchKernelGGL(k_probe_valu, dim3(nblocks), dim3(256), 0, s, 1.0f, sink, clk);
+    return hipGetLastError();
+}
+hipError_t launch_probe_copy(const float *src, float *dst, int64_t nfloat4, hipStream_t s)
+{
+    hipLaunchKernelGGL(k_probe_copy, dim3(256 * 32), dim3(256), 0, s, reinterpret_cast<const float4 *>(src),
+                       reinterpret_cast<float4 *>(dst), nfloat4);
+    return hipGetLastError();
+}
+int probe_valu_iters() { return kProbeIters; }
+
 }  // namespace rtg
 
 // ----------------------------------------------------------------------------
 // build configuration (rtg.h rtg_build_info): every RTG_* knob as compiled into this library
 // ----------------------------------------------------------------------------
-#if RTG_EXP_STUB_SVD + RTG_EXP_NO_TABLE + RTG_EXP_HOT_INPUTS + RTG_EXP_FK_COPY + RTG_EXP_FK_NOPOS + RTG_EXP_MULR_NOBRANCH == 0
+#if RTG_EXP_STUB_SVD + RTG_EXP_NO_TABLE + RTG_EXP_HOT_INPUTS + RTG_EXP_FK_COPY + RTG_EXP_FK_NOPOS + RTG_EXP_MULR_NOBRANCH + \
+    RTG_EXP_TIMESTAMPS + RTG_EXP_SKIP_SIGNAL == 0
 #define RTG_WRONG_ANSWER_KNOBS 0
 #else
 #define RTG_WRONG_ANSWER_KNOBS 1
@@ -639,11 +697,9 @@ extern "C" const char *rtg_build_info(void)
 {
     return "{\"abi\":" RTG_STR(RTG_ABI_VERSION) ",\"arch\":\"gfx950\",\"knobs\":{"
         RTG_KNOB(RTG_FAST_EXACT) RTG_KNOB(RTG_FAST_NORM) RTG_KNOB(RTG_SVD_DIV) RTG_KNOB(RTG_SVD_SQRT) RTG_KNOB(RTG_ANG_TAB_BITS)
-        RTG_KNOB(RTG_SOLVER_SIDES) RTG_KNOB(RTG_SIDES_REBALANCE) RTG_KNOB(RTG_SIDES_FIN_LEFT) RTG_KNOB(RTG_SIDES_FLAGS) RTG_KNOB(RTG_SIDES_TILE_STORE) RTG_KNOB(RTG_SIDES_WAVES)
-        RTG_KNOB(RTG_PRELOAD_ARM) RTG_KNOB(RTG_PRELOAD_TIPS) RTG_KNOB(RTG_L2_PREFETCH) RTG_KNOB(RTG_LATENCY_MAX_B)
-        RTG_KNOB(RTG_LATENCY_WAVES) RTG_KNOB(RTG_FRAME1_LANES) RTG_KNOB(RTG_GROUP_MAX_B) RTG_KNOB(RTG_SERVER_FRAME1) RTG_KNOB(RTG_FK_ROWS) RTG_KNOB(RTG_FK_ROWS_LDS) RTG_KNOB(RTG_DOF_FK_ROWS) RTG_KNOB(RTG_FK_LDS_PAD) RTG_KNOB(RTG_FK_CHUNK) RTG_KNOB(RTG_FK_POS_REGS) RTG_KNOB(RTG_FK_POS_WIN16) RTG_KNOB(RTG_FK_MULTI_POS16) RTG_KNOB(RTG_FK_MIN_WAVES)
+        RTG_KNOB(RTG_SIDES_WAVES) RTG_KNOB(RTG_LATENCY_MAX_B) RTG_KNOB(RTG_FK_ROWS) RTG_KNOB(RTG_FK_ROWS_LDS) RTG_KNOB(RTG_DOF_FK_ROWS) RTG_KNOB(RTG_FK_LDS_PAD) RTG_KNOB(RTG_FK_CHUNK) RTG_KNOB(RTG_FK_POS_REGS) RTG_KNOB(RTG_FK_POS_WIN16) RTG_KNOB(RTG_FK_MULTI_POS16) RTG_KNOB(RTG_FK_MIN_WAVES)
         RTG_KNOB(RTG_FK_ALIGNED_STORE) RTG_KNOB(RTG_FK_REG_SLOTS) RTG_KNOB(RTG_FK_NT_STORE) RTG_KNOB(RTG_DOF_FK_POS_REGS)
-        RTG_KNOB(RTG_EXP_TIMESTAMPS) RTG_KNOB(RTG_EXP_STUB_SVD) RTG_KNOB(RTG_EXP_NO_TABLE) RTG_KNOB(RTG_EXP_FK_COPY) RTG_KNOB(RTG_EXP_FK_NOPOS) RTG_KNOB(RTG_EXP_MULR_NOBRANCH)
+        RTG_KNOB(RTG_EXP_TIMESTAMPS) RTG_KNOB(RTG_EXP_SKIP_SIGNAL) RTG_KNOB(RTG_EXP_STUB_SVD) RTG_KNOB(RTG_EXP_NO_TABLE) RTG_KNOB(RTG_EXP_FK_COPY) RTG_KNOB(RTG_EXP_FK_NOPOS) RTG_KNOB(RTG_EXP_MULR_NOBRANCH)
         "\"RTG_EXP_HOT_INPUTS\":\"" RTG_STR(RTG_EXP_HOT_INPUTS) "\"},\"wrong_answer_knobs\":"
         RTG_STR(RTG_WRONG_ANSWER_KNOBS) "}";
 }

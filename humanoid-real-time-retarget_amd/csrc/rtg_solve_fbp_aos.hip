@@ -14,9 +14,11 @@ hipError_t launch_fbp_aos(int precise, const SolverConsts &C, const float *in0, 
     return hipGetLastError();
 }
 
-hipError_t launch_frame_server(int precise, const SolverConsts &C, const float *in, float *dof, float *local_rot,
+hipError_t launch_frame_server(int precise, const SolverConsts &C0, const float *in, float *dof, float *local_rot,
                                float *body_rot, uint32_t *ctl, uint64_t idle_ticks, hipStream_t s)
 {
+    SolverConsts C = C0;
+    C.err = ctl + 3;   // the server reports into its own control block (rtg.h rtg_frame_server_launch)
     if (precise)
         hipLaunchKernelGGL((k_frame_server<true>), dim3(1), dim3(320), 0, s, C, in, dof, local_rot, body_rot, ctl,
                            idle_ticks);

@@ -9,6 +9,8 @@ exact and done with tensor indexing.
 from __future__ import annotations
 
 import math
+
+import numpy as np
 from typing import List, Optional
 
 import torch
@@ -335,4 +337,7 @@ def quat_to_eular(q):
     """rotation3d.py:658-661: scipy ``from_quat(q).as_euler('xyz', degrees=True)`` -- evaluated in float64 on
     the device (the scipy restatement of quat_in_xyz_axis); returns a float64 numpy array like scipy."""
     t = as_tensor(q)
-    return ops.quat_as_euler(t, "xyz", degrees=True).cpu().numpy()
+    out = ops.quat_as_euler(t, "xyz", degrees=True).cpu().numpy()
+    if (out.reshape(-1).view(np.uint64) == np.uint64(0x7FF8000000000002)).any():   # rtg.h: scipy refuses q
+        raise ValueError("Found zero norm quaternions in `quat`.")
+    return out

@@ -15,7 +15,7 @@ import torch
 from robot_kinematics_model import RobotZeroPose, cal_forward_kinematics
 from rtg import _lib
 from rtg.bridge import as_tensor, back, home_device
-from rtg.runtime import Solver, dev_f32
+from rtg.runtime import Solver, dev_f32, frame_status, raise_frame_error
 
 
 class BaseHumanoidRetargeter(ABC):
@@ -62,7 +62,8 @@ class BaseHumanoidRetargeter(ABC):
     def _solve(self, inputs: Sequence, batched: bool, want_body_rot=False):
         """Run the device solver on (B, ...) or single-frame inputs; returns (local_rot, dof, body_rot).
         A single frame of host inputs (the live teleop loop) goes to the resident frame server (FULL_BODY_POS) or a
-        one-launch frame call over pinned memory (rtg.realtime.per_frame_runner)."""
+        one-launch frame call over pinned memory (rtg.realtime.per_frame_runner).  A single frame the reference
+        raises on raises the same exception here (rtg.h rtg_frame_error); a batch marks such frames instead."""
         dev = home_device(*inputs)
         if not batched and dev.type == "cpu":
             if self._frame_runner is None:   # one runner per solver; FULL_BODY_POS always carries body_rot
@@ -70,14 +71,33 @@ class BaseHumanoidRetargeter(ABC):
                 self._frame_runner = per_frame_runner(self.solver, self.SOLVER_KIND == _lib.SOLVER_FULL_BODY_POS,
                                                       server=self.frame_server, idle_ms=self.idle_ms)
             lr, dof, br = self._frame_runner(*inputs)
+            if dof[0] != dof[0]:   # NaN DOF 0: the frame is marked (the solvers never write DOF 0 otherwise)
+                raise_frame_error(frame_status(dof.reshape(1, 30))[0])
             return lr, dof, (br if want_body_rot else None)
         tails = [tuple(as_tensor(x).shape[-2:]) for x in inputs]
         xs = [dev_f32(as_tensor(x).reshape(-1, *t)) for x, t in zip(inputs, tails)]
         dof, lr, br = self.solver.retarget(xs, want_local_rot=True, want_body_rot=want_body_rot)
         if not batched:
+            raise_frame_error(frame_status(dof)[0].item())
             dof, lr = dof[0], lr[0]
             br = br[0] if br is not None else None
         return back(lr, dev), back(dof, dev), (back(br, dev) if br is not None else None)
+
+    @staticmethod
+    def frame_ok(dof) -> torch.Tensor:
+        """Per-frame mask of a batch's dof rows (B, 30): False where the reference raises on the frame -- those rows
+        are NaN and rtg.runtime.frame_status(dof) gives the exception (1: torch.linalg.svd RuntimeError,
+        2: scipy ValueError, transform3d.py:40 / :53)."""
+        return frame_status(as_tensor(dof)) == 0
+
+    def _batch_out(self, lr, dof, record: bool, return_ok: bool):
+        """A batch's outputs: records (like the per-frame calls) only the frames the reference returns a result
+        for, and appends the ok mask when asked."""
+        ok = self.frame_ok(dof) if (record or return_ok) else None
+        if record:
+            keep = ok.to(torch.bool)
+            self._record(lr[keep], dof[keep])
+        return ok
 
     def close(self):
         """End the per-frame runner (a resident frame server occupies its stream until it ends or idles out)."""

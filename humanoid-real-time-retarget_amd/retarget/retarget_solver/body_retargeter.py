@@ -24,11 +24,12 @@ class Mocap2HuBodyRetargeter(BaseHumanoidRetargeter):
         self._record(lr, dof)
         return lr, dof
 
-    def retarget_batch(self, source_global_rotation, record=False):
+    def retarget_batch(self, source_global_rotation, record=False, return_ok=False):
+        """B frames (B,21,4) -> (local_rot (B,31,4), dof (B,30)[, ok (B,)]); frames the reference raises on are NaN
+        rows with ok False (BaseHumanoidRetargeter.frame_ok)."""
         lr, dof, _ = self._solve([source_global_rotation], batched=True)
-        if record:
-            self._record(lr, dof)
-        return lr, dof
+        ok = self._batch_out(lr, dof, record, return_ok)
+        return (lr, dof, ok) if return_ok else (lr, dof)
 
     def retarget_test(self, source_global_rotation):
         """Debug mapping of raw local rotations (:83-99)."""

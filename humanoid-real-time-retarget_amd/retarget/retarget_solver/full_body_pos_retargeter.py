@@ -22,20 +22,23 @@ class VtrdynFullBodyPosRetargeter(BaseHumanoidRetargeter):
         self.precise_gripper = precise_gripper
 
     def retarget(self, body_global_translation, left_hand_global_translation, right_hand_global_translation):
-        """One frame: body (21,3), hands (20,3) -> (local_rot (31,4), dof (30,), body_global_rotation (59,4))."""
+        """One frame: body (21,3), hands (20,3) -> (local_rot (31,4), dof (30,), body_global_rotation (59,4)).
+        Raises where the reference raises: RuntimeError (torch.linalg.svd of a NaN Kabsch matrix, transform3d.py:40)
+        or ValueError (scipy's zero-norm quaternion, transform3d.py:53); nothing is recorded then."""
         lr, dof, br = self._solve([body_global_translation, left_hand_global_translation,
                                    right_hand_global_translation], batched=False, want_body_rot=True)
         self._record(lr, dof)
         return lr, dof, br
 
     def retarget_batch(self, body_global_translation, left_hand_global_translation, right_hand_global_translation,
-                       record=False, want_body_rot=False):
-        """B frames: (B,21,3), (B,20,3), (B,20,3) -> (local_rot (B,31,4), dof (B,30), body_rot (B,59,4) | None)."""
+                       record=False, want_body_rot=False, return_ok=False):
+        """B frames: (B,21,3), (B,20,3), (B,20,3) -> (local_rot (B,31,4), dof (B,30), body_rot (B,59,4) | None
+        [, ok (B,)]).  Frames the reference raises on (a zero-length or axis-aligned arm segment, a straight elbow,
+        a NaN point: rtg.h rtg_frame_error) come back as NaN rows with ok False; record keeps only the others."""
         lr, dof, br = self._solve([body_global_translation, left_hand_global_translation,
                                    right_hand_global_translation], batched=True, want_body_rot=want_body_rot)
-        if record:
-            self._record(lr, dof)
-        return lr, dof, br
+        ok = self._batch_out(lr, dof, record, return_ok)
+        return (lr, dof, br, ok) if return_ok else (lr, dof, br)
 
 
 def cal_elbowP_and_shoulderY(v1, v0, parent_global_rotation):

@@ -25,9 +25,10 @@ class VtrdynFullBodyRetargeter(BaseHumanoidRetargeter):
         return lr, dof
 
     def retarget_batch(self, body_global_rotation, body_global_translation, left_hand_global_translation,
-                       right_hand_global_translation, record=False):
+                       right_hand_global_translation, record=False, return_ok=False):
+        """B frames -> (local_rot (B,31,4), dof (B,30)[, ok (B,)]); frames the reference raises on are NaN rows with
+        ok False (BaseHumanoidRetargeter.frame_ok)."""
         lr, dof, _ = self._solve([body_global_rotation, body_global_translation, left_hand_global_translation,
                                   right_hand_global_translation], batched=True)
-        if record:
-            self._record(lr, dof)
-        return lr, dof
+        ok = self._batch_out(lr, dof, record, return_ok)
+        return (lr, dof, ok) if return_ok else (lr, dof)

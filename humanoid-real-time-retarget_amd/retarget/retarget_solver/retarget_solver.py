@@ -28,9 +28,8 @@ class HuUpperBodyFromMocapRetarget(BaseHumanoidRetargeter):
         self._record(lr, dof)
         return lr, dof
 
-    def retarget_batch(self, source_global_translation, record=False):
+    def retarget_batch(self, source_global_translation, record=False, return_ok=False):
         """(B,21,3) -> (local_rot (B,31,4), dof (B,30))."""
         lr, dof, _ = self._solve([source_global_translation], batched=True)
-        if record:
-            self._record(lr, dof)
-        return lr, dof
+        ok = self._batch_out(lr, dof, record, return_ok)
+        return (lr, dof, ok) if return_ok else (lr, dof)

@@ -14,8 +14,9 @@ import torch
 from scipy.spatial.transform import Rotation as sRot  # noqa: F401
 
 from poselib.poselib.core.rotation3d import *  # noqa: F401,F403  (the reference re-exports rotation3d)
-from rtg import ops
+from rtg import _lib, ops
 from rtg.bridge import as_tensor, back, home_device
+from rtg.runtime import raise_frame_error
 
 
 def quat_between_two_vecs(vec1, vec2):
@@ -35,16 +36,28 @@ def coord_transform(p, order: list = None, dir=None):
     return p
 
 
+def _raise_if_marked(t: torch.Tensor, code: int) -> None:
+    """The reference raises for the whole call when one element is refused (rtg.h rtg_frame_error); the kernels
+    mark such elements with RTG_FRAME_NAN | code."""
+    if t.numel() and bool((t.reshape(-1).view(torch.int32) == (_lib.FRAME_NAN | code)).any()):
+        raise_frame_error(code)
+
+
 def cal_joint_quat(zero_pose_local_translation, motion_local_translation):
-    """Kabsch fit (:31-50): (B, n, 3) zero-pose vectors vs (B, n, 3) motion vectors -> (B, 4)."""
+    """Kabsch fit (:31-50): (B, n, 3) zero-pose vectors vs (B, n, 3) motion vectors -> (B, 4).  Raises torch's
+    RuntimeError where a fit's matrix has a NaN entry (torch.linalg.svd, :40)."""
     dev = home_device(zero_pose_local_translation, motion_local_translation)
-    return back(ops.cal_joint_quat(as_tensor(zero_pose_local_translation), as_tensor(motion_local_translation)), dev)
+    q = ops.cal_joint_quat(as_tensor(zero_pose_local_translation), as_tensor(motion_local_translation))
+    _raise_if_marked(q, _lib.FRAME_SVD_NONFINITE)
+    return back(q, dev)
 
 
 def quat_in_xyz_axis(q, seq: str = "xyz"):
-    """scipy Euler split into three single-axis quaternions (:52-59)."""
+    """scipy Euler split into three single-axis quaternions (:52-59).  Raises scipy's ValueError on a zero-norm or
+    NaN quaternion (from_quat, :53)."""
     dev = home_device(q)
     a, b, c = ops.quat_in_xyz_axis(as_tensor(q), seq)
+    _raise_if_marked(a, _lib.FRAME_ZERO_NORM_QUAT)
     return back(a, dev), back(b, dev), back(c, dev)
 
 

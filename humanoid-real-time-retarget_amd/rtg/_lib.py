@@ -14,7 +14,7 @@ PKG_ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 LIB_PATH = os.environ.get("RTG_LIB", os.path.join(PKG_ROOT, "librtg_hip.so"))
 
 RTG_OK = 0
-ABI_VERSION = 2
+ABI_VERSION = 3
 
 # rtg_layout (input frame-batch layout of the solvers / producers)
 LAYOUT_AOS = 0
@@ -28,6 +28,12 @@ SOLVER_BODY_ROT = 3
 SERVER_QUIT = 0xFFFFFFFF   # rtg.h RTG_SERVER_QUIT
 ERR_TIMEOUT = 5            # rtg.h RTG_ERR_TIMEOUT (rtg_frame_server_post)
 SERVER_ENDED = 6           # rtg.h RTG_SERVER_ENDED (rtg_frame_server_post: relaunch, post again)
+
+# rtg_frame_error: frames the reference raises on (rtg.h); the code rides in dof[f, 0]'s NaN payload
+FRAME_OK = 0
+FRAME_SVD_NONFINITE = 1
+FRAME_ZERO_NORM_QUAT = 2
+FRAME_NAN = 0x7FC00000     # rtg.h RTG_FRAME_NAN
 
 # rtg_quat_op
 OP_QUAT_MUL = 0
@@ -121,7 +127,9 @@ SIGNATURES = {
                                          c_void_p, c_void_p]),
     "rtg_synth_full_body_f32": (c_int, [c_void_p, c_uint64, c_int64, c_int64, c_int, c_void_p, c_void_p, c_void_p,
                                         c_void_p, c_void_p]),
+    "rtg_box_probe": (c_int, [POINTER(ctypes.c_double), c_int32, c_void_p]),
 }
+PROBE_FIELDS = 6   # rtg.h RTG_PROBE_FIELDS
 
 _lib = None
 
@@ -151,7 +159,7 @@ def lib() -> ctypes.CDLL:
 
 
 WRONG_ANSWER_KNOBS = ("RTG_EXP_STUB_SVD", "RTG_EXP_NO_TABLE", "RTG_EXP_HOT_INPUTS", "RTG_EXP_FK_COPY", "RTG_EXP_FK_NOPOS",
-                      "RTG_EXP_MULR_NOBRANCH")
+                      "RTG_EXP_MULR_NOBRANCH", "RTG_EXP_TIMESTAMPS", "RTG_EXP_SKIP_SIGNAL")
 
 
 def build_info(handle=None) -> dict:

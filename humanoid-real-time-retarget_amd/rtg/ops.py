@@ -502,3 +502,13 @@ def quat_as_euler(q, seq: str, degrees: bool = False):
     check(lib().rtg_quat_as_euler_f64(ptr(q), seq.encode(), int(bool(degrees)), int(torch.Size(lead).numel()),
                                       ptr(out), stream_handle()))
     return out
+
+
+def box_probe() -> dict:
+    """rtg_box_probe (rtg.h): the current GPU's shader clock under load, f32 FMA rate and HBM copy bandwidth,
+    measured now -- recorded beside every bench line so throughput from different boxes can be compared."""
+    require_gpu()
+    out = (ctypes.c_double * _lib.PROBE_FIELDS)()
+    check(lib().rtg_box_probe(out, _lib.PROBE_FIELDS, stream_handle()))
+    return {"sclk_mhz_under_load": out[0], "valu_f32_fma_T_lane_ops_s": out[1], "hbm_copy_GBs": out[2],
+            "valu_kernel_ms": out[3], "copy_kernel_ms": out[4], "compute_units": int(out[5])}

@@ -128,6 +128,31 @@ class DofModel:
             self._h = None
 
 
+# Frames the reference raises on (rtg.h rtg_frame_error): the batched solve marks them -- every dof of the row NaN,
+# dof[f, 0] = RTG_FRAME_NAN | code -- and the per-frame calls raise what the reference raises.
+FRAME_ERRORS = {
+    _lib.FRAME_SVD_NONFINITE: (RuntimeError, "linalg.svd: (Batch element 0): The algorithm failed to converge because "
+                                             "the input matrix contained non-finite values."),   # transform3d.py:40
+    _lib.FRAME_ZERO_NORM_QUAT: (ValueError, "Found zero norm quaternions in `quat`."),           # transform3d.py:53
+}
+
+
+def frame_status(dof: torch.Tensor) -> torch.Tensor:
+    """Per-frame rtg_frame_error code (int8, dof's device) of solver outputs dof (..., 30): 0 where the reference
+    returns a result, 1 where its torch.linalg.svd raises, 2 where scipy's from_quat raises."""
+    d0 = dof[..., 0].contiguous().view(torch.int32)
+    marked = (d0 & ~0xF) == _lib.FRAME_NAN
+    return torch.where(marked, d0 & 0xF, torch.zeros_like(d0)).to(torch.int8)
+
+
+def raise_frame_error(code: int) -> None:
+    """Raise the exception the reference raises on a frame with this rtg_frame_error code (no-op for 0)."""
+    code = int(code)
+    if code:
+        exc, msg = FRAME_ERRORS.get(code, (RuntimeError, f"rtg frame error {code}"))
+        raise exc(msg)
+
+
 # per-frame input rows of each solver kind (rtg.h rtg_solver_kind): (points, components)
 IN_TAILS = {_lib.SOLVER_FULL_BODY_POS: [(21, 3), (20, 3), (20, 3)], _lib.SOLVER_UPPER_BODY: [(21, 3)],
             _lib.SOLVER_FULL_BODY_ROT: [(21, 4), (21, 3), (20, 3), (20, 3)], _lib.SOLVER_BODY_ROT: [(21, 4)]}

@@ -28,7 +28,8 @@
 extern "C" {
 #endif
 
-#define RTG_ABI_VERSION 2   /* 2: the input-layout argument of rtg_retarget_f32 / rtg_ingest_vtrdyn_f32 / rtg_synth_full_body_f32 */
+#define RTG_ABI_VERSION 3   /* 3: frames the reference raises on are marked (rtg_frame_error), the solver error word, ctl[3];
+                               2: the input-layout argument of rtg_retarget_f32 / rtg_ingest_vtrdyn_f32 / rtg_synth_full_body_f32 */
 
 typedef enum rtg_status {
     RTG_OK = 0,
@@ -56,8 +57,9 @@ const char *rtg_last_error(void);
 /* Number of visible devices (0 when no GPU / driver). */
 int rtg_device_count(void);
 /* The compile-time configuration of this library as a JSON object: every RTG_* build knob and its value, and
- * "wrong_answer_knobs" = how many measurement-only knobs that change results (RTG_EXP_STUB_SVD, RTG_EXP_NO_TABLE,
- * RTG_EXP_HOT_INPUTS) are on.  A product library has 0; the Python binding refuses any other. */
+ * "wrong_answer_knobs" = 1 when any measurement-only knob that changes results is on (RTG_EXP_STUB_SVD, _NO_TABLE,
+ * _HOT_INPUTS, _FK_COPY, _FK_NOPOS, _MULR_NOBRANCH, _TIMESTAMPS, _SKIP_SIGNAL).  A product library has 0; the Python
+ * binding refuses any other. */
 const char *rtg_build_info(void);
 
 /* ------------------------------------------------------------------------
@@ -194,10 +196,37 @@ int rtg_solver_create(int kind, const float *src_zero_local_t, const float *src_
                       const int32_t *src_parents, int32_t Js, int precise_gripper, rtg_solver_t *out);
 int rtg_solver_destroy(rtg_solver_t solver);
 
+/* Frames on which the reference raises.  The reference solves one frame per call and, on some degenerate
+ * frames, raises instead of returning:
+ *   RTG_FRAME_SVD_NONFINITE   cal_joint_quat's Kabsch matrix has a NaN entry: torch.linalg.svd raises
+ *                             RuntimeError "linalg.svd: (Batch element 0): The algorithm failed to converge because
+ *                             the input matrix contained non-finite values." (transform3d.py:40);
+ *   RTG_FRAME_ZERO_NORM_QUAT  the quaternion handed to quat_in_xyz_axis is all zero or has a NaN: scipy raises
+ *                             ValueError "Found zero norm quaternions in `quat`." (transform3d.py:53) -- e.g. a
+ *                             zero-length arm segment, an upper arm along the shoulder plane's normal, a straight
+ *                             elbow (radians_between_vecs of a zero projection is NaN, transform3d.py:77-100).
+ * The code is the first raise in the reference's own order (torso fit, left wrist fit, left Euler split, right
+ * wrist fit, right Euler split; full_body_pos_retargeter.py:68-167).  A batched launch marks such a frame instead
+ * of raising: every dof of its row is NaN, and dof[f*30 + 0] -- exactly 0 for every other frame, the solvers never
+ * write DOF 0 -- has the bit pattern RTG_FRAME_NAN | code; its local_rot / body_rot rows are RTG_FRAME_NAN. */
+typedef enum rtg_frame_error {
+    RTG_FRAME_OK = 0,
+    RTG_FRAME_SVD_NONFINITE = 1,
+    RTG_FRAME_ZERO_NORM_QUAT = 2
+} rtg_frame_error;
+#define RTG_FRAME_NAN 0x7FC00000u   /* quiet NaN; the low payload bits carry the rtg_frame_error code in dof[f*30] */
+
+/* Errors a launch reports on the solver's NEXT call (launches never synchronise): the device ORs these into the
+ * solver's host-mapped error word and rtg_retarget_f32 returns RTG_ERR_DEVICE with the word in rtg_last_error(),
+ * then clears it.  A wave that waited ~0.1 s for its partner wave's hand-over flag gives up and sets
+ * RTG_DEVERR_HANDOVER_TIMEOUT: that launch's outputs are not to be trusted. */
+#define RTG_DEVERR_HANDOVER_TIMEOUT 0x1u
+
 /* Batched retarget of B frames.  dof (B,30) required; local_rot (B,31,4) and
  * body_rot (B,59,4, FULL_BODY_POS only: the returned body_global_rotation) may
  * be NULL.  Unused in* must be NULL.  layout (rtg_layout) describes the inputs
- * only; the outputs are always (B, ...) rows.  Replaces the per-frame
+ * only; the outputs are always (B, ...) rows.  Frames on which the reference
+ * raises are marked as described at rtg_frame_error.  Replaces the per-frame
  * .retarget calls of sim_full_body_teleop.py:115-119 / sim_teleop_mujoco.py:104-108
  * / sim_teleop.py:102. */
 int rtg_retarget_f32(rtg_solver_t solver, const float *in0, const float *in1, const float *in2,
@@ -209,9 +238,11 @@ int rtg_retarget_f32(rtg_solver_t solver, const float *in0, const float *in1, co
  * resident workgroup that serves FULL_BODY_POS frames from host-mapped (pinned) memory without a launch per frame.
  *   in        183 floats: body (21,3) | left hand (20,3) | right hand (20,3), rows as rtg_retarget_f32's AoS inputs
  *   dof (30), local_rot (31,4, may be NULL), body_rot (59,4, may be NULL): written per frame
- *   ctl       3 x uint32: [0] frame sequence number, written by the host after the frame's inputs;
+ *   ctl       4 x uint32: [0] frame sequence number, written by the host after the frame's inputs;
  *             [1] the last sequence number served, written by the device after that frame's outputs;
- *             [2] set to 1 by the device when the server has ended.  Zero ctl[1], ctl[2] before the launch.
+ *             [2] set to 1 by the device when the server has ended;
+ *             [3] the server's error word (RTG_DEVERR_*), set before [1] of the frame it concerns.
+ *             Zero ctl[1..3] before the launch.
  * Writing RTG_SERVER_QUIT into ctl[0] ends the server; so does idle_ms (1..60000) without a new frame.  All
  * buffers must be device-accessible host memory (hipHostMalloc / pinned).  The stream is occupied until the
  * server ends.  Outputs are bit-identical to rtg_retarget_f32 at B = 1. */
@@ -225,7 +256,9 @@ int rtg_frame_server_launch(rtg_solver_t solver, const float *in, float *dof, fl
  * != RTG_SERVER_QUIT) in ctl[0] after them, spins until the device publishes it in ctl[1], then copies the pinned
  * outputs the server writes (dof 30, local_rot 124, body_rot 236 floats) into the *_dst buffers that are not NULL.
  * Returns RTG_OK; RTG_SERVER_ENDED if the server ended (idle_ms) before it took the frame -- relaunch it and post
- * the same seq again; RTG_ERR_TIMEOUT after timeout_us (the frame may still be served later). */
+ * the same seq again; RTG_ERR_TIMEOUT after timeout_us (the frame may still be served later); RTG_ERR_DEVICE if
+ * the server set its error word (ctl[3]) while serving the frame (the outputs are copied anyway; the word is
+ * cleared). */
 int rtg_frame_server_post(uint32_t *ctl, uint32_t seq, float *in, const float *body, const float *left_hand,
                           const float *right_hand, const float *dof, const float *local_rot, const float *body_rot,
                           float *dof_dst, float *local_rot_dst, float *body_rot_dst, uint32_t timeout_us);
@@ -272,15 +305,19 @@ int rtg_quat_op_f32(int op, const float *a, const float *b, const float *c, int6
                     rtg_stream_t stream);
 
 /* cal_joint_quat (transform3d.py:31-50): Kabsch fit of npts (1..8) point pairs.
- * Z (n,npts,3) zero-pose vectors, M (n,npts,3) motion vectors -> (n,4). */
+ * Z (n,npts,3) zero-pose vectors, M (n,npts,3) motion vectors -> (n,4).  A fit whose Kabsch matrix has a NaN
+ * entry (where torch.linalg.svd raises, rtg_frame_error) gets all four components = RTG_FRAME_NAN |
+ * RTG_FRAME_SVD_NONFINITE. */
 int rtg_cal_joint_quat_f32(const float *Z, const float *M, int32_t npts, int64_t n, float *out,
                            rtg_stream_t stream);
 
 /* quat_in_xyz_axis (transform3d.py:52-59): scipy Euler split (float64) into three
- * single-axis quaternions.  seq: 3 chars of xyz/XYZ (upper = intrinsic). q (n,4) -> (n,3,4). */
+ * single-axis quaternions.  seq: 3 chars of xyz/XYZ (upper = intrinsic). q (n,4) -> (n,3,4).  A quaternion scipy
+ * refuses (zero norm or NaN, rtg_frame_error) gets all twelve outputs = RTG_FRAME_NAN | RTG_FRAME_ZERO_NORM_QUAT. */
 int rtg_quat_in_xyz_axis_f32(const float *q, const char *seq, int64_t n, float *out, rtg_stream_t stream);
 /* scipy Rotation.from_quat(q).as_euler(seq, degrees) in float64 (rotation3d.py:658-661 quat_to_eular uses
- * 'xyz', degrees=True; degrees multiply by 180/pi like np.rad2deg).  q (n,4) f32 -> out (n,3) f64. */
+ * 'xyz', degrees=True; degrees multiply by 180/pi like np.rad2deg).  q (n,4) f32 -> out (n,3) f64.  A quaternion
+ * scipy refuses gets the three f64 NaNs 0x7FF8000000000000 | RTG_FRAME_ZERO_NORM_QUAT. */
 int rtg_quat_as_euler_f64(const float *q, const char *seq, int degrees, int64_t n, double *out, rtg_stream_t stream);
 
 /* ------------------------------------------------------------------------
@@ -309,6 +346,17 @@ int rtg_angular_velocity_f32(const float *r, int64_t nseq, int64_t L, int64_t J,
  * ---------------------------------------------------------------------- */
 int rtg_synth_full_body_f32(rtg_topology_t topo, uint64_t seed, int64_t frame_offset, int64_t B, int layout,
                             float *body, float *lh, float *rh, float *body_rot, rtg_stream_t stream);
+
+/* ------------------------------------------------------------------------
+ * Box probe (diagnostics, no reference counterpart): what the current GPU delivers right now, so throughput
+ * measured on one box can be set against another's.  Synchronous; allocates 2 GiB of scratch for its duration.
+ * out (host, >= RTG_PROBE_FIELDS doubles):
+ *   [0] shader clock under full VALU load, MHz (shader-cycle counter / 100 MHz wall clock, median workgroup)
+ *   [1] f32 FMA issue rate, T lane-ops/s      [2] HBM copy bandwidth (read + write), GB/s
+ *   [3] VALU kernel ms                        [4] copy kernel ms (1 GiB -> 1 GiB)     [5] compute units
+ * ---------------------------------------------------------------------- */
+#define RTG_PROBE_FIELDS 6
+int rtg_box_probe(double *out, int32_t n_out, rtg_stream_t stream);
 
 #ifdef __cplusplus
 }

@@ -414,3 +414,11 @@ def project_quat_to_axis(q, which):
 def quat_to_eular(q):
     """rotation3d.py:658-661: scipy as_euler('xyz', degrees=True) = radians * (180 / pi) (np.rad2deg)."""
     return as_euler(_c32(q).reshape(-1, 4), "xyz") * (180.0 / np.pi)
+
+
+def frame_status(dof) -> np.ndarray:
+    """The per-frame rtg_frame_error code (include/rtg.h) carried by a solver's dof rows: 0 for a frame the reference
+    solves, else the payload of dof[:, 0] (RTG_FRAME_NAN | code) -- 1 where torch.linalg.svd raises, 2 where
+    scipy's from_quat raises."""
+    d0 = np.ascontiguousarray(np.asarray(dof, np.float32)[:, 0]).view(np.uint32)
+    return np.where((d0 & 0xFFFFFFF0) == 0x7FC00000, d0 & 0xF, 0).astype(np.int8)

@@ -377,3 +377,74 @@ def test_overlay_extras_oracle_vs_reference():
     for got, ref in ulps:
         s = frame_stats(got, ref)
         assert s["max"] <= 2.5e-7 and s["exact_elems"] >= 0.88, s
+
+
+# ------------------------------------------------------------------ degenerate frames (tools/make_golden.py *_edge)
+# Frames on which the reference raises (rtg.h rtg_frame_error): torch.linalg.svd on a NaN Kabsch matrix
+# (transform3d.py:40, RuntimeError) or scipy from_quat on a zero / NaN quaternion (transform3d.py:53, ValueError).
+# The oracle marks them exactly where the reference raised; every other frame is compared like the goldens.
+EDGE_MESSAGES = {0: "", 1: "RuntimeError: RuntimeError: linalg.svd: (Batch element 0): The algorithm failed to "
+                 "converge because the input matrix contained non-finite values.",
+                 2: "ValueError: Found zero norm quaternions in `quat`."}
+
+
+def _edge_run(name, precise=True):
+    """(golden, oracle dof, oracle local_rot, reference status, reference dof) of one edge fixture."""
+    from rtg import assets
+    zp = golden("zero_pose")
+    d = golden(name)
+    if name == "full_body_pos_edge":
+        tag = "precise" if precise else "binary"
+        dof, lr, _ = orc.full_body_pos(zp["vtrdyn_full_local_t"], zp["vtrdyn_full_global_t"], d["body"], d["lh"],
+                                       d["rh"], precise)
+        return d, dof, lr, d[f"{tag}_status"], d[f"{tag}_dof"], d[f"{tag}_message"]
+    if name == "upper_body_edge":
+        dof, lr = orc.upper_body(zp["vtrdyn_local_t"], d["x"])
+    elif name == "full_body_rot_edge":
+        dof, lr = orc.full_body_rot(zp["vtrdyn_full_local_t"], d["body_rot"], d["body_pos"], d["lh"], d["rh"])
+    else:
+        dof, lr = orc.body_rot(assets.parents("vtrdyn"), d["global_rot"])
+    return d, dof, lr, d["status"], d["dof"], d["message"]
+
+
+EDGE_CASES = [("full_body_pos_edge", True), ("full_body_pos_edge", False), ("upper_body_edge", True),
+              ("full_body_rot_edge", True), ("body_rot_edge", True)]
+# frames at the elbow map's singularity (the forearm continues the upper arm to within rounding): the elbow angle is
+# acos of a dot product at 1 - O(ulp), so VML's rounding of acos moves it by up to 1.6 rad (test_edge_vml_attribution)
+EDGE_SINGULAR = {"rand4: straight left elbow", "rand8: straight left elbow"}
+
+
+@pytest.mark.parametrize("name,precise", EDGE_CASES)
+def test_edge_frames_raise_where_the_reference_raises(name, precise):
+    """Every frame the reference raised on is marked with the reference's exception (code in dof[f, 0]'s NaN
+    payload, the whole row NaN), and no other frame is; the others match the reference like the goldens."""
+    d, dof, lr, status, ref_dof, msgs = _edge_run(name, precise)
+    np.testing.assert_array_equal(orc.frame_status(dof), status)
+    assert {EDGE_MESSAGES[int(s)] for s in status} == set(msgs.tolist())
+    for s, m in zip(status, msgs):
+        assert m == EDGE_MESSAGES[int(s)]
+    raised = status != 0
+    assert raised.any() and (~raised).any()
+    assert np.isnan(dof[raised]).all() and np.isnan(lr[raised]).all()
+    ok = ~raised & ~np.isin(d["names"], list(EDGE_SINGULAR))
+    np.testing.assert_array_equal(np.isnan(dof[ok]), np.isnan(ref_dof[ok]))   # NaN where the reference has NaN
+    e = np.abs(np.nan_to_num(dof[ok].astype(np.float64)) - np.nan_to_num(ref_dof[ok]))
+    assert e.max() <= 2.2e-5, e.max()
+
+
+def test_edge_vml_attribution():
+    """The singular straight-elbow frames match too once torch's own VML acos / sin / cos are routed into the
+    oracle: their residual is VML's rounding at a singularity, not a different algorithm."""
+    import ctypes
+    fns = _torch_vml()
+    if fns is None or "avx512f" not in open("/proc/cpuinfo").read():
+        pytest.skip("torch's VML or an AVX-512 host (the goldens' ISA) is not available")
+    lib = orc.lib()
+    lib.oracle_set_vml(*fns, ctypes.c_longlong(0x140102))
+    try:
+        d, dof, _, status, ref_dof, _ = _edge_run("full_body_pos_edge", True)
+    finally:
+        lib.oracle_set_vml(None, None, None, ctypes.c_longlong(0))
+    sing = np.isin(d["names"], list(EDGE_SINGULAR))
+    assert sing.sum() == 2 and (status[sing] == 0).all()
+    assert np.abs(dof[sing].astype(np.float64) - ref_dof[sing]).max() <= 1e-5

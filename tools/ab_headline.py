@@ -22,7 +22,7 @@ from rtg.runtime import Solver, Topology
 zp = np.load(os.path.join(sys.argv[1], "tests", "golden", "zero_pose.npz"))
 S = Solver(_lib.SOLVER_FULL_BODY_POS, zp["vtrdyn_full_local_t"], zp["vtrdyn_full_global_t"], assets.parents("vtrdyn_full"), True)
 T = Topology(assets.parents("vtrdyn_full"), assets.local_translation("vtrdyn_full"), assets.tree_quat("vtrdyn_full"))
-B, out = 262144, {}
+B, out = 262144, {"box": ops.box_probe()}
 for layout in ("soa", "aos"):
     sets = [ops.synth_full_body(T, B, seed=1234, frame_offset=r * B, layout=layout) for r in range(3)]
     dof = torch.empty((B, 30), device="cuda")
@@ -62,10 +62,12 @@ def main():
     ref = res[builds[0][0]][0]
     summary = {}
     for name, runs in res.items():
-        summary[name] = {lay: {"kernel_us_min": min(r[lay]["kernel_us"] for r in runs),
+        summary[name] = {"sclk_mhz_under_load": [r["box"]["sclk_mhz_under_load"] for r in runs],
+                         "hbm_copy_GBs": [r["box"]["hbm_copy_GBs"] for r in runs]}
+        summary[name].update({lay: {"kernel_us_min": min(r[lay]["kernel_us"] for r in runs),
                                "kernel_us_med": sorted(r[lay]["kernel_us"] for r in runs)[len(runs) // 2],
                                "bits_match_first_build": all(r[lay]["dof_sha"] == ref[lay]["dof_sha"] for r in runs)}
-                         for lay in ("soa", "aos")}
+                         for lay in ("soa", "aos")})
     print(json.dumps({"summary": summary}), flush=True)
 
 
