@@ -579,27 +579,27 @@ __global__ __launch_bounds__(kFkTile) RTG_FK_WAVES void k_dof_fk(TopoView T, Dof
 }
 
 // ----------------------------------------------------------------------------
-// Row-staged FK (RTG_FK_ROWS, the production path).  Measured (profiles/r03/fk): the windowed streaming kernels
-// above move their bytes at ~3 TB/s whatever they compute -- a build that skips the chain and copies each window
-// straight out (RTG_EXP_FK_COPY) is only 4 % faster than the real FK.  Their stores write every frame's row in 96-
-// and 128-byte pieces at 16-byte (not line) alignment, one window at a time, so each wave keeps ~2 partly written
-// lines per frame open in L2 between windows and many leave L2 partial.  Here one wave owns a tile of F frames whose
-// input rows and output rows are each ONE contiguous span of global memory:
+// Row-staged FK, one quaternion component per lane (the production path).
+//
+// The windowed streaming kernels above move their bytes at ~3 TB/s whatever they compute (a build that skips the
+// chain and copies each window straight out, RTG_EXP_FK_COPY, is only 4 % faster): every frame's row leaves in 96- and
+// 128-byte pieces at 16-byte (not line) alignment, one window at a time, and lines left partly read or written
+// between windows are fetched again (PMC: FETCH 1.75x, WRITE 1.22x the algorithmic bytes).  Here a wave owns a tile
+// of kQuadFrames consecutive frames whose input rows and output rows are each ONE contiguous span of global memory:
 //   1. the tile's input rows land in LDS as one contiguous image (16-byte LDS-DMA, 1 KiB per wave-instruction);
-//   2. lane f composes frame f joint by joint, reading joint j's input from the image and writing its results over
-//      it in place (the rotation image) and into a position image -- a branch parent is simply read back from
-//      the images, so no parent slots are needed;
-//   3. the images go out as contiguous 1 KiB wave-stores: every line is written whole, by one instruction.
-// F is chosen per skeleton so the images fit ~32 KiB (5 waves per CU): F = 36 for the 31-joint Hu.  The per-joint
-// arithmetic is fk_stream_tile's, in the same order (the same bits: test_gpu_parity FK / inverse-FK tests).
+//   2. the tile is composed joint by joint in the image, in place (global rotations over the locals), positions into a
+//      second image -- a branch parent is read back from the images, so no parent slots;
+//   3. the images leave as contiguous 1 KiB wave-stores: every line is written whole, by one instruction.
+// The composition runs with FOUR lanes per frame, lane 4f + c holding component c (x, y, z, w) of frame f's
+// quaternions: a Hamilton product is one instruction stream in which each lane folds its own component's four
+// products in the reference's order (rtg_math.cuh qmul), its operands fetched across the quad by DPP quad_perm; the
+// normalisation's sum of squares is the same left fold in every lane of the quad.  So all 64 lanes are busy with 16
+// frames, a wave's dependent chain is a quarter of a one-lane-per-frame chain, and the images of a 16-frame tile
+// (J x 28 bytes per frame) leave ~11 waves per CU -- where the one-lane-per-frame row kernel (36 frames per wave,
+// 28 lanes idle, 5 waves per CU) was slower than the streaming one.  Every value is the scalar
+// device functions' own arithmetic: bit-identical (test_gpu_parity FK / inverse-FK / mixed tests).
 // ----------------------------------------------------------------------------
-constexpr int kRowsLdsBudget = RTG_FK_ROWS_LDS;   // bytes of row images per wave (32 KiB: 5 waves per CU)
-static inline int rows_frames(int J, int bytes_per_frame_joint, int extra_bytes_per_frame = 0)
-{
-    int F = kRowsLdsBudget / (J * bytes_per_frame_joint + extra_bytes_per_frame);
-    F = F > 64 ? 64 : F;
-    return F & ~3;   // F multiple of 4: every tile's position / DOF span starts 16-byte aligned
-}
+constexpr int kQuadFrames = 16;   // frames per tile = 64 lanes / 4 components
 
 // nbytes (a multiple of 4) from global src to LDS dst, both 16-byte aligned: 16-byte LDS-DMA (1 KiB per
 // wave-instruction, lane-linear), then the last 0-3 dwords by 4-byte LDS-DMA -- nothing past src + nbytes is read
@@ -637,72 +637,122 @@ RTG_DEV void rows_store(float *__restrict__ dst, const float *src, int nbytes)
             *reinterpret_cast<float4 *>(dst + (o >> 2) + 4 * lane) = *reinterpret_cast<const float4 *>(src + (o >> 2) + 4 * lane);
     for (int i = (n16 >> 2) + lane; i < (nbytes >> 2); i += 64) dst[i] = src[i];
 }
-
-// FK of a tile's nfr frames whose input rows are in the rotation image (kinematics.py:13-39; STATE:
-// skeleton3d.py:402-430): global rotations over the locals in place, translations into the position image
-template <bool STATE>
-RTG_DEV void fk_rows_compute(const TopoView &T, V root, int nfr, float *rot, float *pos)
-{
-    const int J = T.J, lane = threadIdx.x & 63;
-    if (lane >= nfr) return;
-    float *R = rot + lane * J * 4;
-    float *P = pos + lane * J * 3;
-    Q g = ld4(R);   // root: global = local, unnormalised (kinematics.py:27-29)
-    V t = root;
-    P[0] = t.x; P[1] = t.y; P[2] = t.z;
-    Q next = J > 1 ? ld4(R + 4) : g;   // joint j+1's input is read while joint j composes
-    for (int j = 1; j < J; ++j) {
-        Q lq = next;
-        if (j + 1 < J) next = ld4(R + 4 * (j + 1));
-        const int p = ld_const(T.parents + j);
-        if (p != j - 1) {   // a branch parent: read back from the images (launch-uniform branch)
-            g = ld4(R + 4 * p);
-            t = V{P[3 * p], P[3 * p + 1], P[3 * p + 2]};
-        }
-        if (STATE) lq = qmul_norm(ld_const(T.tree_quat + j), lq);   // skeleton3d.py:412-418
-        const V rv = qrotate(g, ld_const(T.local_t + j));
-        g = qmul_norm(g, lq);
-        t = V{rv.x + t.x, rv.y + t.y, rv.z + t.z};
-        st4(R + 4 * j, g);
-        P[3 * j] = t.x; P[3 * j + 1] = t.y; P[3 * j + 2] = t.z;
-    }
-}
-
-// inverse FK of a tile's nfr frames in the image (kinematics.py:41-63; STATE: skeleton3d.py:468-484).  Joints run
-// from the last to the first, in place: joint j needs g[p] (p < j, not yet overwritten) and g[j].
-template <bool STATE>
-RTG_DEV void local_rows_compute(const TopoView &T, int nfr, float *img)
-{
-    const int J = T.J, lane = threadIdx.x & 63;
-    if (lane >= nfr) return;
-    float *W = img + lane * J * 4;
-    for (int j = J - 1; j > 0; --j) {   // the root row is copied as it is (kinematics.py:49)
-        const int p = ld_const(T.parents + j);
-        Q q = qmul_norm(qconj(ld4(W + 4 * p)), ld4(W + 4 * j));
-        if (STATE) q = qmul_norm(qnormalize(qconj(ld_const(T.tree_quat + j))), q);   // skeleton3d.py:470-478
-        st4(W + 4 * j, q);
-    }
-}
-
-// Tiles of every segment (FK or inverse FK) in one persistent launch.  RF.f[s] frames per tile of segment s; the
-// input / rotation image sits at the start of the wave's LDS, the position image at RF.pos_off floats (past the
-// largest rotation image, so a next tile of another segment never overlaps it).  Each wave walks tiles
-// blockIdx.x, + gridDim.x, ...: it stores tile t's rotation image, then issues tile t+1's input DMA into that image
-// (the image's LDS reads are done), then stores t's positions -- the next input is in flight while the stores leave.
-struct RowsF {
-    int32_t f[RTG_MAX_SEGMENTS];
-    int32_t pos_off;
-};
 RTG_DEV void lds_reads_done()   // every LDS read this wave issued has returned (before an LDS-DMA overwrites it)
 {
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
 }
+
+// ---- component-per-lane quaternion algebra: lane c of a quad holds component c (0 x, 1 y, 2 z, 3 w)
+template <int P0, int P1, int P2, int P3>
+RTG_DEV float qperm(float v)   // the quad's lane P<c> value, in lane c (DPP quad_perm)
+{
+    return __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, v),
+                                                              P0 | (P1 << 2) | (P2 << 4) | (P3 << 6), 0xF, 0xF, false));
+}
+RTG_DEV float xorf(float v, uint32_t m) { return __builtin_bit_cast(float, __builtin_bit_cast(uint32_t, v) ^ m); }
+struct QLane {
+    int c;           // this lane's component
+    uint32_t wneg;   // sign bit in the w lane: its 2nd and 3rd products are subtracted (a - b == a + (-b), exactly)
+    uint32_t conj;   // sign bit in the x, y, z lanes (qconj)
+};
+RTG_DEV QLane qlane()
+{
+    const int c = threadIdx.x & 3;
+    return QLane{c, c == 3 ? 0x80000000u : 0u, c < 3 ? 0x80000000u : 0u};
+}
+RTG_DEV float qsel(const QLane &L, Q q) { return L.c == 0 ? q.x : (L.c == 1 ? q.y : (L.c == 2 ? q.z : q.w)); }
+// qmul (rotation3d.py:14-27): component c = ((t1 +- t2) +- t3) - t4, each product rounded, in the scalar order:
+//   x: ((aw bx + ax bw) + ay bz) - az by      y: ((aw by + ay bw) + az bx) - ax bz
+//   z: ((aw bz + az bw) + ax by) - ay bx      w: ((aw bw - ax bx) - ay by) - az bz
+RTG_DEV float qmul_l(const QLane &L, float a, float b)
+{
+    const float t1 = qperm<3, 3, 3, 3>(a) * b;
+    const float t2 = xorf(qperm<0, 1, 2, 0>(a), L.wneg) * qperm<3, 3, 3, 0>(b);
+    const float t3 = xorf(qperm<1, 2, 0, 1>(a), L.wneg) * qperm<2, 0, 1, 1>(b);
+    const float t4 = qperm<2, 0, 1, 2>(a) * qperm<1, 2, 0, 2>(b);
+    return ((t1 + t2) + t3) - t4;
+}
+// qnormalize (quat_unit(quat_pos(q)), rotation3d.py:30-56): w >= 0, then / max(|q|, 1e-9) -- the sum of squares is
+// the same left fold in every lane of the quad, and a lane's quotient is mulr's (equal to mulr_k's, rtg_math.cuh)
+RTG_DEV float qnormalize_l(float q)
+{
+    const float f = 1.0f - 2.0f * (qperm<3, 3, 3, 3>(q) < 0.0f ? 1.0f : 0.0f);
+    q = f * q;
+    const float q0 = qperm<0, 0, 0, 0>(q), q1 = qperm<1, 1, 1, 1>(q), q2 = qperm<2, 2, 2, 2>(q), q3 = qperm<3, 3, 3, 3>(q);
+    const Rcp r = sqrt_clamp_rcp(((q0 * q0 + q1 * q1) + q2 * q2) + q3 * q3, 1e-9f).r;
+    return mulr(q, r);
+}
+RTG_DEV float qmul_norm_l(const QLane &L, float a, float b) { return qnormalize_l(qmul_l(L, a, b)); }
+// qrotate (rotation3d.py:205-211): imag((q (v, 0)) conj(q)); lanes 0-2 hold x, y, z
+RTG_DEV float qrotate_l(const QLane &L, float q, V v)
+{
+    const float vb = L.c == 0 ? v.x : (L.c == 1 ? v.y : (L.c == 2 ? v.z : 0.0f));
+    return qmul_l(L, qmul_l(L, q, vb), xorf(q, L.conj));
+}
+
+// FK of a tile (nfr frames valid; the quads of the others compute on whatever the image holds and store nothing
+// that leaves LDS) whose input rows are in the rotation image (kinematics.py:13-39; STATE: skeleton3d.py:402-430):
+// global rotations over the locals in place, translations into the position image.  rootc: this lane's component
+// of its frame's root translation (lanes 0-2).
 template <bool STATE>
-__global__ __launch_bounds__(64) void k_kin_rows(FkMultiArgs A, RowsF RF, int64_t ntiles)
+RTG_DEV void fk_quad_compute(const TopoView &T, float rootc, float *rot, float *pos)
+{
+    const int J = T.J;
+    const QLane L = qlane();
+    const int fr = (threadIdx.x & 63) >> 2;
+    float *R = rot + fr * J * 4 + L.c;
+    float *P = pos + fr * J * 3 + (L.c < 3 ? L.c : 2);
+    float g = R[0];   // root: global = local, unnormalised (kinematics.py:27-29)
+    float t = rootc;
+    if (L.c < 3) P[0] = t;
+    float next = J > 1 ? R[4] : g;   // joint j+1's input is read while joint j composes
+    for (int j = 1; j < J; ++j) {
+        float lq = next;
+        if (j + 1 < J) next = R[4 * (j + 1)];
+        const int p = ld_const(T.parents + j);
+        if (p != j - 1) {   // a branch parent: read back from the images (launch-uniform branch)
+            g = R[4 * p];
+            t = P[3 * p];
+        }
+        if (STATE) lq = qmul_norm_l(L, qsel(L, ld_const(T.tree_quat + j)), lq);   // skeleton3d.py:412-418
+        const float rv = qrotate_l(L, g, ld_const(T.local_t + j));
+        g = qmul_norm_l(L, g, lq);
+        t = rv + t;
+        R[4 * j] = g;
+        if (L.c < 3) P[3 * j] = t;
+    }
+}
+
+// inverse FK of a tile in the image (kinematics.py:41-63; STATE: skeleton3d.py:468-484).  Joints run from the last
+// to the first, in place: joint j needs g[p] (p < j, not yet overwritten) and g[j].
+template <bool STATE>
+RTG_DEV void local_quad_compute(const TopoView &T, float *img)
+{
+    const int J = T.J;
+    const QLane L = qlane();
+    float *W = img + ((threadIdx.x & 63) >> 2) * J * 4 + L.c;
+    for (int j = J - 1; j > 0; --j) {   // the root row is copied as it is (kinematics.py:49)
+        const int p = ld_const(T.parents + j);
+        float q = qmul_norm_l(L, xorf(W[4 * p], L.conj), W[4 * j]);
+        if (STATE) {   // skeleton3d.py:470-478
+            const float tq = qnormalize_l(xorf(qsel(L, ld_const(T.tree_quat + j)), L.conj));
+            q = qmul_norm_l(L, tq, q);
+        }
+        W[4 * j] = q;
+    }
+}
+
+// Tiles of every segment (FK or inverse FK) in one persistent launch.  The rotation image sits at the start of the
+// wave's LDS, the position image at pos_off floats (past the largest rotation image, so a next tile of another
+// segment never overlaps it).  Each wave walks tiles blockIdx.x, + gridDim.x, ...: it stores tile t's rotation
+// image, then issues tile t+1's input DMA into that image (the image's LDS reads are done), then stores t's
+// positions -- the next input is in flight while the stores leave.
+template <bool STATE>
+__global__ __launch_bounds__(64) void k_kin_quad(FkMultiArgs A, int32_t pos_off, int64_t ntiles)
 {
     extern __shared__ __attribute__((aligned(16))) float fk_lds[];
     const int lane = threadIdx.x & 63;
-    float *img = fk_lds, *pos = fk_lds + RF.pos_off;
+    float *img = fk_lds, *pos = fk_lds + pos_off;
     struct Tile {
         int s, nfr;
         int64_t f0;
@@ -712,19 +762,19 @@ __global__ __launch_bounds__(64) void k_kin_rows(FkMultiArgs A, RowsF RF, int64_
 #pragma unroll
         for (int i = 1; i < RTG_MAX_SEGMENTS; ++i)
             if (i < A.n && t >= A.block_start[i]) s = i;
-        const int F = RF.f[s];
-        const int64_t f0 = (t - A.block_start[s]) * F, left = A.seg[s].B - f0;
-        return Tile{s, (int)(left < F ? left : F), f0};
+        const int64_t f0 = (t - A.block_start[s]) * kQuadFrames, left = A.seg[s].B - f0;
+        return Tile{s, (int)(left < kQuadFrames ? left : kQuadFrames), f0};
     };
-    auto issue = [&](const Tile &k, V &root) {   // the tile's input rows -> the image; its root translations
+    auto issue = [&](const Tile &k, float &rootc) {   // the tile's input rows -> the image; the root translations
         const FkSeg &S = A.seg[k.s];
         rows_load(S.local_rot + k.f0 * S.T.J * 4, img, k.nfr * S.T.J * 16);
-        if (S.op == 0 && lane < k.nfr) root = ld3(S.root_t + (k.f0 + lane) * 3);
+        const int fr = lane >> 2, c = lane & 3;
+        if (S.op == 0 && fr < k.nfr && c < 3) rootc = S.root_t[(k.f0 + fr) * 3 + c];
     };
     int64_t t = blockIdx.x;
     if (t >= ntiles) return;
     Tile k = decode(t);
-    V root{0.0f, 0.0f, 0.0f};
+    float root = 0.0f;
     issue(k, root);
     for (;;) {
         rows_load_wait();
@@ -733,9 +783,9 @@ __global__ __launch_bounds__(64) void k_kin_rows(FkMultiArgs A, RowsF RF, int64_
         const int64_t tn = t + gridDim.x;
         const bool more = tn < ntiles;
         const Tile kn = more ? decode(tn) : k;
-        V rootn{0.0f, 0.0f, 0.0f};
-        if (S.op == 0) fk_rows_compute<STATE>(S.T, root, k.nfr, img, pos);
-        else local_rows_compute<STATE>(S.T, k.nfr, img);
+        float rootn = 0.0f;
+        if (S.op == 0) fk_quad_compute<STATE>(S.T, root, img, pos);
+        else local_quad_compute<STATE>(S.T, img);
         wave_sync();
         rows_store(S.g_rot + k.f0 * J * 4, img, k.nfr * J * 16);
         lds_reads_done();
@@ -748,63 +798,6 @@ __global__ __launch_bounds__(64) void k_kin_rows(FkMultiArgs A, RowsF RF, int64_
         k = kn;
         root = rootn;
     }
-}
-
-// HuForwardModel.forward_kinematics (hu_forward_model.py:17-33) row-staged: the tile's DOF rows ((J-1) floats per
-// frame, one contiguous span) are staged with the rotation image's LDS-DMA; joint j's local rotation is built in-lane
-// from its angle exactly as k_dof_fk does.
-template <bool CLIP>
-__global__ __launch_bounds__(64) void k_dof_fk_rows(TopoView T, DofView D, const float *__restrict__ dof,
-                                                    const float *__restrict__ root_rot,
-                                                    const float *__restrict__ root_t, int64_t B, int F,
-                                                    float *__restrict__ g_rot, float *__restrict__ g_pos)
-{
-    extern __shared__ __attribute__((aligned(16))) float fk_lds[];
-    const int J = T.J, lane = threadIdx.x & 63, N = J - 1;
-    const int64_t f0 = (int64_t)blockIdx.x * F;
-    const int nfr = (int)((B - f0) < F ? (B - f0) : F);
-    float *rot = fk_lds, *pos = fk_lds + F * J * 4, *ang = pos + F * J * 3;   // ang: [F][J-1]
-    if (N > 0) rows_load(dof + f0 * N, ang, nfr * N * 4);
-    Q rroot = qident();
-    V troot{0.0f, 0.0f, 0.0f};
-    if (lane < nfr) {
-        rroot = ld4(root_rot + (f0 + lane) * 4);
-        troot = ld3(root_t + (f0 + lane) * 3);
-    }
-    rows_load_wait();
-    if (lane < nfr) {
-        float *R = rot + lane * J * 4;
-        float *P = pos + lane * J * 3;
-        const float *A = ang + lane * N;
-        Q g = rroot;   // root: global = the root rotation, unnormalised (:24, kinematics.py:27-29)
-        V t = troot;
-        st4(R, g);
-        P[0] = t.x; P[1] = t.y; P[2] = t.z;
-        for (int j = 1; j < J; ++j) {
-            const int p = ld_const(T.parents + j);
-            if (p != j - 1) {
-                g = ld4(R + 4 * p);
-                t = V{P[3 * p], P[3 * p + 1], P[3 * p + 2]};
-            }
-            float a = A[j - 1];
-            if (CLIP) {   // torch.clamp (min then max; NaN passes), then the straight-through sum
-                const float lo = ld_const(D.lower + (j - 1)), hi = ld_const(D.upper + (j - 1));
-                float c = a < lo ? lo : a;
-                c = c > hi ? hi : c;
-                a = (c - a) + a;
-            }
-            const int ax = ld_const(D.axis + (j - 1));
-            const Q lq = qfrom_angle_axis(a, V{ax == 0 ? 1.0f : 0.0f, ax == 1 ? 1.0f : 0.0f, ax == 2 ? 1.0f : 0.0f});
-            const V rv = qrotate(g, ld_const(T.local_t + j));
-            g = qmul_norm(g, lq);
-            t = V{rv.x + t.x, rv.y + t.y, rv.z + t.z};
-            st4(R + 4 * j, g);
-            P[3 * j] = t.x; P[3 * j + 1] = t.y; P[3 * j + 2] = t.z;
-        }
-    }
-    wave_sync();
-    rows_store(g_rot + f0 * J * 4, rot, nfr * J * 16);
-    rows_store(g_pos + f0 * J * 3, pos, nfr * J * 12);
 }
 
 static inline bool al16(const void *p) { return ((uintptr_t)p & 15u) == 0; }
@@ -829,34 +822,32 @@ __global__ __launch_bounds__(256) void k_fk_multi(FkMultiArgs A)
     for (int j = 1; j < S.T.J; ++j) st4(l + 4 * j, qmul_norm(qconj(ld4(g + 4 * S.T.parents[j])), ld4(g + 4 * j)));
 }
 
-// Launch k_kin_rows over A's segments (tile sizes, image offsets, a persistent grid of what fits the device).
-static bool rows_ok(const FkMultiArgs &A)
+// The quad kernel needs 16-byte aligned rows (LDS-DMA and dwordx4 stores)
+static bool quad_ok(const FkMultiArgs &A)
 {
-    if (!RTG_FK_ROWS) return false;
+    if (!RTG_FK_QUAD) return false;
     for (int i = 0; i < A.n; ++i) {
         const FkSeg &S = A.seg[i];
         if (!al16(S.local_rot) || !al16(S.g_rot) || (S.op == 0 && !al16(S.g_pos))) return false;
     }
     return true;
 }
-static hipError_t launch_rows(FkMultiArgs &A, bool state, hipStream_t s)
+// Launch k_kin_quad over A's segments: tile starts, image offsets, a persistent grid of what fits the device.
+static hipError_t launch_quad(FkMultiArgs &A, bool state, hipStream_t s)
 {
-    RowsF RF{};
     int64_t tiles = 0;
     int rot = 4, pos = 0;   // floats of the largest rotation / position image
     for (int i = 0; i < A.n; ++i) {
-        const int J = A.seg[i].T.J, fk = A.seg[i].op == 0;
-        RF.f[i] = rows_frames(J, fk ? 28 : 16);
+        const int J = A.seg[i].T.J;
         A.block_start[i] = tiles;
-        tiles += grid_for(A.seg[i].B, RF.f[i]);
-        rot = RF.f[i] * J * 4 > rot ? RF.f[i] * J * 4 : rot;
-        if (fk) pos = RF.f[i] * J * 3 > pos ? RF.f[i] * J * 3 : pos;
+        tiles += grid_for(A.seg[i].B, kQuadFrames);
+        rot = kQuadFrames * J * 4 > rot ? kQuadFrames * J * 4 : rot;
+        if (A.seg[i].op == 0) pos = kQuadFrames * J * 3 > pos ? kQuadFrames * J * 3 : pos;
     }
     for (int i = A.n; i < RTG_MAX_SEGMENTS; ++i) A.block_start[i] = tiles;
     if (tiles == 0) return hipSuccess;
-    RF.pos_off = rot;
     const size_t lds = sizeof(float) * (size_t)(rot + pos);
-    const void *fn = state ? (const void *)k_kin_rows<true> : (const void *)k_kin_rows<false>;
+    const void *fn = state ? (const void *)k_kin_quad<true> : (const void *)k_kin_quad<false>;
     int dev = 0, cus = 0, per_cu = 0;
     hipError_t e = hipGetDevice(&dev);
     if (e == hipSuccess) e = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
@@ -864,8 +855,8 @@ static hipError_t launch_rows(FkMultiArgs &A, bool state, hipStream_t s)
     if (e != hipSuccess) return e;
     const int64_t slots = (int64_t)(per_cu > 0 ? per_cu : 1) * (cus > 0 ? cus : 1);
     const unsigned grid = (unsigned)(tiles < slots ? tiles : slots);
-    if (state) hipLaunchKernelGGL(k_kin_rows<true>, dim3(grid), dim3(64), lds, s, A, RF, tiles);
-    else hipLaunchKernelGGL(k_kin_rows<false>, dim3(grid), dim3(64), lds, s, A, RF, tiles);
+    if (state) hipLaunchKernelGGL(k_kin_quad<true>, dim3(grid), dim3(64), lds, s, A, rot, tiles);
+    else hipLaunchKernelGGL(k_kin_quad<false>, dim3(grid), dim3(64), lds, s, A, rot, tiles);
     return hipGetLastError();
 }
 static FkMultiArgs one_segment(const TopoView &T, int op, const float *in, const float *rt, int64_t B, float *out,
@@ -881,7 +872,7 @@ hipError_t launch_fk(const TopoView &T, bool state, const float *lr, const float
                      hipStream_t s)
 {
     FkMultiArgs A = one_segment(T, 0, lr, rt, B, gr, gp);
-    if (rows_ok(A)) return launch_rows(A, state, s);
+    if (quad_ok(A)) return launch_quad(A, state, s);
     if (T.nslots <= kMaxFkSlots) {
         const dim3 g(grid_for(B, kFkTile)), b(kFkTile);
         const size_t lds = fk_stream_lds_bytes(T.nslots);
@@ -898,7 +889,7 @@ hipError_t launch_fk(const TopoView &T, bool state, const float *lr, const float
 hipError_t launch_local_rotation(const TopoView &T, bool state, const float *g, int64_t B, float *l, hipStream_t s)
 {
     FkMultiArgs A = one_segment(T, 1, g, nullptr, B, l, nullptr);
-    if (rows_ok(A)) return launch_rows(A, state, s);
+    if (quad_ok(A)) return launch_quad(A, state, s);
     if (T.nslots <= kMaxFkSlots) {
         const dim3 gd(grid_for(B, kFkTile)), b(kFkTile);
         const size_t lds = fk_stream_lds_bytes(T.nslots);
@@ -914,7 +905,7 @@ hipError_t launch_local_rotation(const TopoView &T, bool state, const float *g, 
 
 hipError_t launch_fk_multi(FkMultiArgs &A, hipStream_t s)
 {
-    if (rows_ok(A)) return launch_rows(A, false, s);
+    if (quad_ok(A)) return launch_quad(A, false, s);
     int maxS = 0;
     for (int i = 0; i < A.n; ++i) maxS = A.seg[i].T.nslots > maxS ? A.seg[i].T.nslots : maxS;
     const bool stream = maxS <= kMaxFkSlots;
@@ -936,14 +927,6 @@ hipError_t launch_fk_multi(FkMultiArgs &A, hipStream_t s)
 hipError_t launch_dof_fk(const TopoView &T, const DofView &D, bool clip, const float *dof, const float *root_rot,
                          const float *root_t, int64_t B, float *gr, float *gp, hipStream_t s)
 {
-    if (RTG_DOF_FK_ROWS && al16(dof) && al16(gr) && al16(gp)) {
-        const int F = rows_frames(T.J, 28, (T.J - 1) * 4);
-        const dim3 g(grid_for(B, F)), b(64);
-        const size_t lds = (size_t)F * (T.J * 28 + (T.J - 1) * 4);
-        if (clip) hipLaunchKernelGGL(k_dof_fk_rows<true>, g, b, lds, s, T, D, dof, root_rot, root_t, B, F, gr, gp);
-        else hipLaunchKernelGGL(k_dof_fk_rows<false>, g, b, lds, s, T, D, dof, root_rot, root_t, B, F, gr, gp);
-        return hipGetLastError();
-    }
     if (T.nslots > kMaxFkSlots) return hipErrorInvalidValue;   // rejected at rtg_dof_model_create
     const dim3 g(grid_for(B, kFkTile)), b(kFkTile);
     const size_t lds = dof_fk_lds_bytes(T.nslots);

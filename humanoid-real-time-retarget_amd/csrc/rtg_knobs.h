@@ -22,14 +22,8 @@
 #define RTG_EXP_SKIP_SIGNAL 0   // measurement knob: block 0's first R10 hand-over is never raised, so its partner wave
 #endif                          // times out (tests the RTG_DEVERR_HANDOVER_TIMEOUT report; wrong answers)
 // ---- used by rtg_fk.hip
-#ifndef RTG_FK_ROWS
-#define RTG_FK_ROWS 0   // 1: row-staged FK / inverse FK / DOF FK (whole tile rows through LDS, contiguous 1 KiB stores); 0: windowed streaming
-#endif
-#ifndef RTG_FK_ROWS_LDS
-#define RTG_FK_ROWS_LDS 32768   // bytes of row images per wave: sets the frames per tile (36 for the 31-joint Hu)
-#endif
-#ifndef RTG_DOF_FK_ROWS
-#define RTG_DOF_FK_ROWS 0   // HuForwardModel row-staged too (measured 2.5x slower: its sincos-heavy chain wants all 64 lanes)
+#ifndef RTG_FK_QUAD
+#define RTG_FK_QUAD 1   // FK / inverse FK / mixed launches: k_kin_quad (row-staged tiles, four lanes per frame); 0: windowed streaming
 #endif
 #ifndef RTG_FK_LDS_PAD
 #define RTG_FK_LDS_PAD 0   // extra LDS bytes per streaming-FK wave: fewer waves per CU (an L2-footprint experiment)

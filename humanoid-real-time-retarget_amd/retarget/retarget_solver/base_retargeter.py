@@ -23,7 +23,7 @@ class BaseHumanoidRetargeter(ABC):
     SOLVER_KIND: Optional[int] = None
 
     def __init__(self, source_zero_pose: RobotZeroPose, target_zero_pose: RobotZeroPose, precise_gripper=False, *,
-                 frame_server: Optional[bool] = None, idle_ms: int = 200):
+                 frame_server: Optional[bool] = None, idle_ms: int = 5):
         self.source_zero_pose = source_zero_pose
         self.target_zero_pose = target_zero_pose
         self._motion_local_rotation = []
@@ -33,17 +33,18 @@ class BaseHumanoidRetargeter(ABC):
         self._frame_runner = None
         self.configure_per_frame(frame_server, idle_ms)
 
-    def configure_per_frame(self, frame_server: Optional[bool] = None, idle_ms: int = 200):
+    def configure_per_frame(self, frame_server: Optional[bool] = None, idle_ms: int = 5):
         """How single host frames are served (an addition to the reference API).
 
-        frame_server=False (the default; RTG_FRAME_SERVER=1 flips it): one launch per frame over pinned memory, on a
-        private stream -- nothing stays resident, so a caller's device-wide synchronize never waits on it.
-        frame_server=True (FULL_BODY_POS): a resident workgroup serves frames with no launch per frame; it occupies
-        its stream until ``idle_ms`` pass without a frame or :meth:`close` runs, and a device-wide synchronize in
-        between waits for it."""
+        frame_server=True (the default for FULL_BODY_POS; RTG_FRAME_SERVER=0 turns it off): a resident workgroup
+        serves the frames with no launch per frame (rtg.realtime.FrameServer).  It ends after ``idle_ms`` without a
+        frame (default 5 ms: a device-wide synchronize between frames waits at most that long), on :meth:`close`,
+        or at interpreter exit, and relaunches itself on the next frame.  frame_server=False, and every other
+        solver kind: one launch per frame over pinned memory on a private stream (rtg.realtime.FrameGraph) --
+        nothing stays resident."""
         if frame_server is None:
             import os
-            frame_server = os.environ.get("RTG_FRAME_SERVER", "0") == "1"
+            frame_server = os.environ.get("RTG_FRAME_SERVER", "1") == "1"
         self.close()
         self.frame_server, self.idle_ms = bool(frame_server), int(idle_ms)
 

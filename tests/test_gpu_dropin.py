@@ -223,7 +223,7 @@ def test_per_frame_graph_matches_batched(gpu):
     from robot_kinematics_model import RobotZeroPose
     g = golden("full_body_pos_precise")
     hu = VtrdynFullBodyPosRetargeter(RobotZeroPose.from_asset("vtrdyn_full"), RobotZeroPose.from_asset("hu_v5"),
-                                     precise_gripper=True)
+                                     precise_gripper=True, frame_server=False)
     n = 40
     lr_b, dof_b, br_b = hu.retarget_batch(torch.from_numpy(g["body"][:n]), torch.from_numpy(g["lh"][:n]),
                                           torch.from_numpy(g["rh"][:n]), want_body_rot=True)
@@ -266,17 +266,18 @@ def test_frame_server_matches_batched(gpu):
 
 
 def test_per_frame_calls_do_not_stall_device_synchronize(gpu):
-    """the drop-in's default per-frame path leaves nothing resident, so a torch.cuda.synchronize()
-    between teleop frames returns at once; the opt-in frame server honours the retargeter's idle_ms and close();
-    one runner serves both retarget() (body_rot) and a caller that drops it."""
+    """a torch.cuda.synchronize() between teleop frames returns at once with the one-launch path
+    (frame_server=False, nothing resident) and within the server's idle_ms with the resident server -- the default,
+    5 ms; close() ends it at once; one runner serves both retarget() (body_rot) and a caller that drops it."""
     import time
 
     from retarget.retarget_solver import VtrdynFullBodyPosRetargeter
     from robot_kinematics_model import RobotZeroPose
     g = golden("full_body_pos_precise")
     zf, zh = RobotZeroPose.from_asset("vtrdyn_full"), RobotZeroPose.from_asset("hu_v5")
-    for server, idle_ms, bound_s in ((False, 200, 0.05), (True, 10, 0.15)):
-        hu = VtrdynFullBodyPosRetargeter(zf, zh, precise_gripper=True, frame_server=server, idle_ms=idle_ms)
+    for server, idle_ms, bound_s in ((False, 200, 0.05), (True, 10, 0.15), (None, None, 0.05)):
+        kw = {} if server is None else dict(frame_server=server, idle_ms=idle_ms)   # None: the defaults
+        hu = VtrdynFullBodyPosRetargeter(zf, zh, precise_gripper=True, **kw)
         worst = 0.0
         for i in range(6):
             _, dof, br = hu.retarget(g["body"][i], g["lh"][i], g["rh"][i])
