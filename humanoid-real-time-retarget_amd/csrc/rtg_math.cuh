@@ -37,15 +37,11 @@ RTG_DEV float ieee_sqrtf(float x) { return __builtin_sqrtf(x); }   // IEEE sqrt 
 // tools/check_fastmath.hip (run by tests/test_gpu_parity.py).
 RTG_DEV float cr_sqrt(float x)
 {
-#if RTG_FAST_EXACT
     const double d = (double)x;
     const double y = __builtin_amdgcn_sqrt(d);
     const double r = __builtin_fma(-y, y, d);
     const double y1 = __builtin_fma(r, 0.5 * __builtin_amdgcn_rcp(y), y);
     return (float)((r == 0.0 || r != r) ? y : y1);
-#else
-    return __builtin_sqrtf(x);
-#endif
 }
 RTG_DEV float cr_acos(float x) { return (float)::acos((double)x); }
 RTG_DEV float cr_sin(float x) { return (float)::sin((double)x); }
@@ -78,16 +74,12 @@ struct Rcp {
 };
 RTG_DEV Rcp rcp64(float n)
 {
-#if RTG_FAST_EXACT
     const double d = (double)n;
     const double r0 = __builtin_amdgcn_rcp(d);
     const double e0 = __builtin_fma(-d, r0, 1.0);
     const double r1 = __builtin_fma(r0, e0, r0);
     const double e1 = __builtin_fma(-d, r1, 1.0);
     return Rcp{e0 == e0 ? __builtin_fma(r1, e1, r1) : r0, n};
-#else
-    return Rcp{1.0 / (double)n, n};
-#endif
 }
 // RN(a/n) == (float)((double)a * 1/n) whenever the quotient is a normal f32: an f32 quotient is never within
 // 2^-50 (relative) of an f32 midpoint and the f64 product is within 2^-52.  A subnormal quotient (absolute
@@ -150,7 +142,6 @@ struct NormRcp {
 };
 RTG_DEV NormRcp sqrt_clamp_rcp(float s, float lo)
 {
-#if RTG_FAST_NORM
     // the fast path runs unconditionally (on s <= 0 / inf / NaN its values are discarded) and ONE rare-case branch
     // takes the cr_sqrt + rcp64 path when s is not a positive finite number or n needs the clamp
     const double d = (double)s;
@@ -173,10 +164,6 @@ RTG_DEV NormRcp sqrt_clamp_rcp(float s, float lo)
         out = NormRcp{nc, rcp64(nc)};
     }
     return out;
-#else
-    const float n = clamp_lo(cr_sqrt(s), lo);
-    return NormRcp{n, rcp64(n)};
-#endif
 }
 
 RTG_DEV float tsign(float v) { return v > 0.0f ? 1.0f : (v < 0.0f ? -1.0f : 0.0f); }
@@ -400,17 +387,17 @@ RTG_DEV float qexp_component(Q q, int k)
 // joint angles below 151 degrees -- R(w) is stored as a short move from a cheap f32 estimate P(w) =
 // 4 asin(sqrt((1 - w) / 2)) (v_sqrt_f32 and a degree-6 fma polynomial, within 3 ulps of R): the 3-bit code c in
 // 1..7 means R = P + (c - 4) ulps, 0 means "not tabulated" (exact path).  2^24 entries, 10 per 32-bit word, in
-// 6.7 MiB (RTG_ANG_TAB_BITS=4 packs 8 per word in 8 MiB; measured no faster), built on the device by the exact path
+// 6.7 MiB (4-bit codes, 8 per word in 8 MiB, measured no faster), built on the device by the exact path
 // itself (ang_tab_code, k_build_ang_tab) with the same P.  qexp_component_tab thus skips acos, sincos and
 // atan2f (290 of the 330 instructions of an exp-map); w outside the table or a code-0 entry takes the exact
 // path.  tools/check_fastmath.hip checks qexp_component_tab == qexp_component for every f32 w.
 constexpr uint32_t kAngTabLo = 0x3e800000u;                     // bits of 0.25f
 constexpr uint32_t kAngTabEntries = 0x3f800000u - kAngTabLo;    // up to 1.0f (exclusive): 2^24
-constexpr uint32_t kAngTabBits = RTG_ANG_TAB_BITS;              // 3: moves -3..3, 10 codes per word; 4: -7..7, 8
-constexpr uint32_t kAngTabPer = kAngTabBits == 3 ? 10u : 8u;
+constexpr uint32_t kAngTabBits = 3;                             // moves -3..3
+constexpr uint32_t kAngTabPer = 10u;                            // codes per 32-bit word
 constexpr uint32_t kAngTabWords = (kAngTabEntries + kAngTabPer - 1) / kAngTabPer;
 constexpr uint32_t kAngTabBias = 1u << (kAngTabBits - 1);      // code = move + bias; code 0 = not tabulated
-RTG_DEV uint32_t ang_tab_word(uint32_t i) { return kAngTabPer == 10u ? __umulhi(i, 0xCCCCCCCDu) >> 3 : i >> 3; }
+RTG_DEV uint32_t ang_tab_word(uint32_t i) { return __umulhi(i, 0xCCCCCCCDu) >> 3; }   // i / 10
 RTG_DEV float exp_angle_estimate(float w)
 {
     const float t2 = (1.0f - w) * 0.5f;
@@ -616,19 +603,11 @@ RTG_DEV Q axis_half_quat(int axis, float a)
 // roots are IEEE-exact (fdiv = one rcp64 + mulr, cr_sqrt).  Matrices are column-major: a[r + 3 c].
 RTG_DEV float fdiv(float a, float b)
 {
-#if RTG_SVD_DIV
-    return a / b;
-#else
-    return mulr(a, rcp64(b));
-#endif
+    return a / b;   // the compiler's IEEE f32 division sequence (measured 6 % faster here than rcp64 + mulr)
 }
 RTG_DEV float la_sqrt(float x)
 {
-#if RTG_SVD_SQRT
-    return __builtin_sqrtf(x);
-#else
     return cr_sqrt(x);
-#endif
 }
 RTG_DEV float la_sign(float a, float b) { return __builtin_copysignf(fabsf(a), b); }   // Fortran SIGN
 RTG_DEV float la_lapy2(float x, float y)                                                 // SLAPY2

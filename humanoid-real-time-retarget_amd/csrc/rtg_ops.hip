@@ -696,9 +696,7 @@ int probe_valu_iters() { return kProbeIters; }
 extern "C" const char *rtg_build_info(void)
 {
     return "{\"abi\":" RTG_STR(RTG_ABI_VERSION) ",\"arch\":\"gfx950\",\"knobs\":{"
-        RTG_KNOB(RTG_FAST_EXACT) RTG_KNOB(RTG_FAST_NORM) RTG_KNOB(RTG_SVD_DIV) RTG_KNOB(RTG_SVD_SQRT) RTG_KNOB(RTG_ANG_TAB_BITS)
-        RTG_KNOB(RTG_SIDES_WAVES) RTG_KNOB(RTG_LATENCY_MAX_B) RTG_KNOB(RTG_FK_QUAD) RTG_KNOB(RTG_FK_LDS_PAD) RTG_KNOB(RTG_FK_CHUNK) RTG_KNOB(RTG_FK_POS_REGS) RTG_KNOB(RTG_FK_POS_WIN16) RTG_KNOB(RTG_FK_MULTI_POS16) RTG_KNOB(RTG_FK_MIN_WAVES)
-        RTG_KNOB(RTG_FK_ALIGNED_STORE) RTG_KNOB(RTG_FK_REG_SLOTS) RTG_KNOB(RTG_FK_NT_STORE) RTG_KNOB(RTG_DOF_FK_POS_REGS)
+        RTG_KNOB(RTG_SIDES_WAVES) RTG_KNOB(RTG_LATENCY_MAX_B)
         RTG_KNOB(RTG_EXP_TIMESTAMPS) RTG_KNOB(RTG_EXP_SKIP_SIGNAL) RTG_KNOB(RTG_EXP_STUB_SVD) RTG_KNOB(RTG_EXP_NO_TABLE) RTG_KNOB(RTG_EXP_FK_COPY) RTG_KNOB(RTG_EXP_FK_NOPOS) RTG_KNOB(RTG_EXP_MULR_NOBRANCH)
         "\"RTG_EXP_HOT_INPUTS\":\"" RTG_STR(RTG_EXP_HOT_INPUTS) "\"},\"wrong_answer_knobs\":"
         RTG_STR(RTG_WRONG_ANSWER_KNOBS) "}";

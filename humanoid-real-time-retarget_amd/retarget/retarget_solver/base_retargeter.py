@@ -18,6 +18,9 @@ from rtg.bridge import as_tensor, back, home_device
 from rtg.runtime import Solver, dev_f32, frame_status, raise_frame_error
 
 
+_CPU = torch.device("cpu")
+
+
 class BaseHumanoidRetargeter(ABC):
     #: rtg_solver_kind of the subclass
     SOLVER_KIND: Optional[int] = None
@@ -66,14 +69,14 @@ class BaseHumanoidRetargeter(ABC):
         one-launch frame call over pinned memory (rtg.realtime.per_frame_runner).  A single frame the reference
         raises on raises the same exception here (rtg.h rtg_frame_error); a batch marks such frames instead."""
         dev = home_device(*inputs)
-        if not batched and dev.type == "cpu":
+        if not batched and dev == _CPU:
             if self._frame_runner is None:   # one runner per solver; FULL_BODY_POS always carries body_rot
                 from rtg.realtime import per_frame_runner
                 self._frame_runner = per_frame_runner(self.solver, self.SOLVER_KIND == _lib.SOLVER_FULL_BODY_POS,
                                                       server=self.frame_server, idle_ms=self.idle_ms)
             lr, dof, br = self._frame_runner(*inputs)
-            if dof[0] != dof[0]:   # NaN DOF 0: the frame is marked (the solvers never write DOF 0 otherwise)
-                raise_frame_error(frame_status(dof.reshape(1, 30))[0])
+            if self._frame_runner.status:   # the frame is marked (read off the host row, no torch op)
+                raise_frame_error(self._frame_runner.status)
             return lr, dof, (br if want_body_rot else None)
         tails = [tuple(as_tensor(x).shape[-2:]) for x in inputs]
         xs = [dev_f32(as_tensor(x).reshape(-1, *t)) for x, t in zip(inputs, tails)]

@@ -27,7 +27,7 @@ from typing import Sequence
 import numpy as np
 import torch
 
-from ._lib import RtgError, check, lib
+from ._lib import FRAME_NAN, RtgError, check, lib
 from .runtime import Solver, require_gpu, stream_handle
 
 from .runtime import IN_TAILS as _IN_TAILS
@@ -35,9 +35,14 @@ from .runtime import IN_TAILS as _IN_TAILS
 _SERVER_ENDED = 6   # rtg.h RTG_SERVER_ENDED
 
 
+_F32 = torch.float32
+
+
 def _host_f32_ptr(x, n: int, tail):
     """(address, owner) of n contiguous float32 values on the host: a CPU tensor or array as it is when it already
     is one, else a float32 copy."""
+    if type(x) is torch.Tensor and x.is_cpu and x.dtype is _F32 and x.is_contiguous() and x.numel() == n:
+        return x.data_ptr(), x   # the teleop loop's case, in five cheap attribute reads
     if isinstance(x, torch.Tensor):
         if x.device.type != "cpu":
             raise ValueError("per-frame inputs are host arrays")
@@ -54,6 +59,33 @@ def _host_f32_ptr(x, n: int, tail):
 
 def _addr(a: np.ndarray) -> int:
     return a.__array_interface__["data"][0]   # cheaper than a.ctypes.data
+
+
+def _marked(dof_row: np.ndarray) -> int:
+    """rtg_frame_error code of one frame's host dof row: 0 unless DOF 0 carries the NaN mark (rtg.h RTG_FRAME_NAN)."""
+    if dof_row[0] == dof_row[0]:
+        return 0
+    v = int(dof_row[:1].view(np.uint32)[0])
+    return v & 0xF if (v & ~0xF) == FRAME_NAN else 0
+
+
+class _OutRows:
+    """Per-frame output rows carved from blocks of ``n`` frames (one per output; 64 frames, so a view that is pickled drags at most ~100 KB along): a frame's addresses are
+    arithmetic and its tensors are views (a numpy index and torch.from_numpy each) -- about 3 us less per frame than
+    fresh arrays whose addresses Python has to look up.  A block lives while any frame's tensors do."""
+
+    def __init__(self, shapes, n: int = 64):
+        self.shapes, self.n, self.k = shapes, n, n
+        self.strides = [4 * int(np.prod(s)) if s else 0 for s in shapes]
+
+    def next(self):
+        if self.k == self.n:
+            self.blocks = [np.empty((self.n,) + s, np.float32) if s else None for s in self.shapes]
+            self.bases = [_addr(b) if b is not None else None for b in self.blocks]
+            self.k = 0
+        k = self.k
+        self.k = k + 1
+        return k
 
 
 class FrameGraph:
@@ -82,6 +114,7 @@ class FrameGraph:
         self.stream = torch.cuda.Stream(dev)
         self.done = torch.cuda.Event()   # no timing: recording and querying it stays cheap
         self.timeout_s = float(timeout_s)
+        self.status = 0   # rtg_frame_error code of the last frame
 
     def _launch(self):
         check(lib().rtg_retarget_f32(*self._args, stream_handle(self.stream)))
@@ -107,6 +140,7 @@ class FrameGraph:
         self._launch()
         self._wait()
         out = self.h_out.numpy()
+        self.status = _marked(out[124:154])   # read by the drop-in retargeters (raise like the reference)
         lr = torch.from_numpy(out[:124].reshape(31, 4).copy())
         dof = torch.from_numpy(out[124:154].copy())
         br = torch.from_numpy(out[154:].reshape(59, 4).copy()) if self.want_body_rot else None
@@ -147,8 +181,12 @@ class FrameServer:
         self.stream = torch.cuda.Stream(dev)
         self.timeout_s = float(timeout_s)
         self.seq = 0
+        self.status = 0   # rtg_frame_error code of the last frame
         self._running = False
         self._sizes = [int(np.prod(t)) for t in self.tails]
+        self._rows = _OutRows([(31, 4), (30,), (59, 4) if want_body_rot else None])
+        self._post = lib().rtg_frame_server_post
+        self._timeout_us = int(self.timeout_s * 1e6)
         self._ctl_ptr, self._in_ptr = self.h_ctl.data_ptr(), self.h_in.data_ptr()
         self._lr_ptr, self._dof_ptr = out, out + 4 * 124
         self._br_ptr = out + 4 * 154 if want_body_rot else None
@@ -163,31 +201,32 @@ class FrameServer:
         self._running = True
 
     def __call__(self, *inputs: Sequence):
-        """One frame: the copy in, the post, the wait and the copy out are ONE C call (rtg_frame_server_post)."""
-        if len(inputs) != len(self.tails):
-            raise ValueError(f"expected {len(self.tails)} inputs")
-        keep, ptrs = [], []
-        for x, n, t in zip(inputs, self._sizes, self.tails):
-            p, x = _host_f32_ptr(x, n, t)
-            keep.append(x)
-            ptrs.append(p)
-        lr = np.empty((31, 4), np.float32)
-        dof = np.empty(30, np.float32)
-        br = np.empty((59, 4), np.float32) if self.want_body_rot else None
+        """One frame: the copy in, the post, the wait and the copy out are ONE C call (rtg_frame_server_post).
+        Python's share is kept to attribute reads and integer arithmetic (tools/extra_bench.py latency)."""
+        if len(inputs) != 3:
+            raise ValueError("expected 3 inputs")
+        sz, tl = self._sizes, self.tails
+        p0, x0 = _host_f32_ptr(inputs[0], sz[0], tl[0])
+        p1, x1 = _host_f32_ptr(inputs[1], sz[1], tl[1])
+        p2, x2 = _host_f32_ptr(inputs[2], sz[2], tl[2])
+        R = self._rows
+        k = R.next()
+        (b_lr, b_dof, b_br), (s_lr, s_dof, s_br) = R.bases, R.strides
         if not self._running or (self._ctl[2] and self.stream.query()):
             self._launch()
         self.seq = self.seq + 1 if self.seq + 1 < int(self._quit) else 1
-        post = lib().rtg_frame_server_post
-        args = [self._ctl_ptr, self.seq, self._in_ptr, *ptrs, self._dof_ptr, self._lr_ptr, self._br_ptr,
-                _addr(dof), _addr(lr), _addr(br) if br is not None else None,
-                int(self.timeout_s * 1e6)]
-        rc = post(*args)
+        args = (self._ctl_ptr, self.seq, self._in_ptr, p0, p1, p2, self._dof_ptr, self._lr_ptr, self._br_ptr,
+                b_dof + k * s_dof, b_lr + k * s_lr, b_br + k * s_br if b_br is not None else None, self._timeout_us)
+        rc = self._post(*args)
         while rc == _SERVER_ENDED:   # it idled out before it took the frame: relaunch (the frame is still posted)
             self.stream.synchronize()
             self._launch()
-            rc = post(*args)
+            rc = self._post(*args)
         check(rc)
-        return torch.from_numpy(lr), torch.from_numpy(dof), (torch.from_numpy(br) if br is not None else None)
+        lr, dof, br = R.blocks
+        dof = dof[k]
+        self.status = _marked(dof)
+        return torch.from_numpy(lr[k]), torch.from_numpy(dof), (torch.from_numpy(br[k]) if br is not None else None)
 
     def close(self):
         if self._running:

@@ -4,9 +4,13 @@ Needs a build with -DRTG_EXP_TIMESTAMPS=1 (tools/build_variants.sh "ts:-DRTG_EXP
 RTG_LIB=humanoid-real-time-retarget_amd/variants/ts.so): lane 0 of each wave of every 8th block records the 100 MHz
 wall clock at the phase boundaries (rtg_solver.cuh, TS slots).  Prints, per wave side and per residency round, the
 median time of each phase (us) and the spread of block start / end times.
-Slots: 0 start, 1 first fit's points loaded + A formed, 2 its SVD + R done, 3 phase-1 done, 4 after barrier 1,
-5 phase-2 done (left: wrist fit; right: both arm chains), 6 after barrier 2, 7 Euler split + gripper done,
-8 exp-map read-out done, 9 after barrier 3, 12 DOF tile stored; 10 / 11 the left wave's second fit (A, SVD).
+Slots: 0 start, 1 first fit's points loaded + A formed, 2 its SVD + R done, 3 phase-1 done, 4 after the R10 hand-over
+(right wave: flag seen; left wave: flag raised), 5 phase-2 done (left: wrist fit; right: both arm chains), 6 after
+the left-chain hand-over, 7 Euler split + gripper done, 8 exp-map read-out done, 9 past the tile counter, 12 DOF tile
+stored; 10 / 11 the left wave's second fit (A, SVD).  The tile's two waves meet at an LDS counter: the first to
+arrive records 9 and 12 at once and exits (its "store" phase is 0), the second stores the tile's rows.  A slot a
+wave never recorded stays 0 and is masked out of the medians.
+Needs RTG_ALLOW_MEASUREMENT_BUILD=1 (RTG_EXP_TIMESTAMPS writes the clock into body_rot: a wrong-answer knob).
 """
 from __future__ import annotations
 
@@ -24,8 +28,8 @@ from rtg import _lib, assets, ops  # noqa: E402
 from rtg._lib import check, lib  # noqa: E402
 from rtg.runtime import Solver, Topology, ptr, stream_handle  # noqa: E402
 
-PH = [("loads_A", 0, 1), ("svd1", 1, 2), ("phase1_rest", 2, 3), ("barrier1", 3, 4), ("phase2", 4, 5),
-      ("barrier2", 5, 6), ("after_arm", 6, 7), ("finalize", 7, 8), ("barrier3", 8, 9), ("store", 9, 12)]
+PH = [("loads_A", 0, 1), ("svd1", 1, 2), ("phase1_rest", 2, 3), ("handover1", 3, 4), ("phase2", 4, 5),
+      ("handover2", 5, 6), ("after_arm", 6, 7), ("finalize", 7, 8), ("tile_counter", 8, 9), ("store", 9, 12)]
 
 
 def main(B=262144, layout="soa", reps=5):
@@ -50,11 +54,12 @@ def main(B=262144, layout="soa", reps=5):
             runs.append((t[0::2] | (t[1::2] << np.uint64(32))).astype(np.int64).reshape(ns, 4, 16))
     out = {"B": B, "layout": layout, "sampled_blocks": ns, "runs": len(runs)}
     per = []
-    for R in runs:
-        t0 = R[:, :, 0].min()
-        R = (R - t0) * 0.01          # us from the first wave's start
+    for raw in runs:
+        t0 = raw[:, :, 0].min()
+        R = (raw - t0) * 0.01          # us from the first wave's start
+        R = np.where(raw == 0, np.nan, R)   # slots a wave never recorded
         start = R[:, :, 0].min(1)
-        end = R[:, :, 12].max(1)
+        end = np.nanmax(R[:, :, 12], 1)
         order = np.argsort(start)
         # residency rounds: a block starts in round 2 once some earlier block has ended
         first_end = end.min()
@@ -69,11 +74,11 @@ def main(B=262144, layout="soa", reps=5):
                 continue
             for side, waves in (("left", [0, 2]), ("right", [1, 3])):
                 W = R[sel][:, waves].reshape(-1, 16)
-                res[f"round{rr}_{side}"] = {name: float(np.median(W[:, b] - W[:, a])) for name, a, b in PH}
+                res[f"round{rr}_{side}"] = {name: float(np.nanmedian(W[:, b] - W[:, a])) for name, a, b in PH}
                 if side == "left":
-                    res[f"round{rr}_{side}"]["fit2_loads_A"] = float(np.median(W[:, 10] - W[:, 4]))
-                    res[f"round{rr}_{side}"]["fit2_svd"] = float(np.median(W[:, 11] - W[:, 10]))
-                res[f"round{rr}_{side}"]["total"] = float(np.median(W[:, 12] - W[:, 0]))
+                    res[f"round{rr}_{side}"]["fit2_loads_A"] = float(np.nanmedian(W[:, 10] - W[:, 4]))
+                    res[f"round{rr}_{side}"]["fit2_svd"] = float(np.nanmedian(W[:, 11] - W[:, 10]))
+                res[f"round{rr}_{side}"]["total"] = float(np.nanmedian(W[:, 12] - W[:, 0]))
         per.append(res)
     out["per_run"] = per
     print(json.dumps(out, indent=1))
