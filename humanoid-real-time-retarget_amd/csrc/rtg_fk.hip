@@ -91,7 +91,7 @@ template <bool POS16>
 constexpr int pos_win() { return POS16 ? kFkTile * kPos16Pitch : 0; }
 
 // Branch-parent slots live in LDS: [slot][7][64] (q x y z w, t x y z per lane).  Every shipped skeleton needs <= 2.
-static inline size_t lds_slot_floats(int nslots) { return (size_t)nslots * 7 * kFkTile; }
+__host__ __device__ inline size_t lds_slot_floats(int nslots) { return (size_t)nslots * 7 * kFkTile; }
 static inline size_t fk_stream_lds_bytes(int nslots, bool pos16 = false)
 {
     const size_t pw = pos16 ? pos_win<true>() : pos_win<false>();
@@ -473,6 +473,251 @@ __global__ __launch_bounds__(kFkTile) void k_dof_fk(TopoView T, DofView D, const
     }
 }
 
+// ----------------------------------------------------------------------------
+// Line-synchronous streaming (RTG_FK_LINE).  A 64-frame tile's rows are 64 J records of 16 B, i.e. 8 J whole
+// 128-byte lines, and a frame's row starts (f J) mod 8 records into a line.  The windowed kernels above move, per
+// frame, joints [8k, 8k+8): a 128-B piece at 16-B alignment that straddles two lines, so every line is requested by
+// two windows ~15 us apart and the second request misses L2 (FETCH 1.75x the input on Hu FK).  Here, at step m,
+// every lane moves the records of ITS OWN m-th line instead: the pieces are whole lines (8 lanes x 16 B), each line
+// of the rows is requested once (a line two frames share, once by each for its own records), and the position
+// piece of rotation line L is bytes [96 L, 96 L + 96) of the position rows (32-B aligned).  The price: a lane's
+// joint index at a step differs across lanes, so the topology (local_t, schedule, tree quaternion) is read from an
+// LDS table instead of scalar registers, and J joints take ceil((J + 8 - gcd(J, 8)) / 8) steps of 8 (Hu: 5 x 8
+// for 31).  Per lane the joints are still composed in index order with the same operations, so the bits are the
+// windowed kernels'.
+// ----------------------------------------------------------------------------
+RTG_DEV int line_steps(int J)
+{
+    const int g = (J & 7) == 0 ? 8 : (J & 3) == 0 ? 4 : (J & 1) == 0 ? 2 : 1;   // gcd(J, 8)
+    return (J + 8 - g + 7) >> 3;
+}
+// LDS topology table: per joint {local_t.x, .y, .z, sched bits} and its tree quaternion
+static inline size_t line_topo_floats(int J) { return (size_t)J * 8; }
+static inline size_t fk_line_lds_bytes(int J, int nslots)
+{
+    return sizeof(float) * ((size_t)kFkTile * kRotPitch + lds_slot_floats(nslots) + line_topo_floats(J));
+}
+RTG_DEV void line_topo_fill(const TopoView &T, float *topo)
+{
+    for (int j = threadIdx.x; j < T.J; j += kFkTile) {
+        const V lt = ld_const(T.local_t + j);
+        const Q tq = ld_const(T.tree_quat + j);
+        st4(topo + 8 * j, Q{lt.x, lt.y, lt.z, __int_as_float(ld_const(T.sched + j))});
+        st4(topo + 8 * j + 4, tq);
+    }
+}
+// piece (it, lane) of step m: frame fr's sub-th record of its m-th line, ok when that record is the frame's own
+struct LinePiece {
+    int fr, sub, g;
+    bool ok;
+};
+RTG_DEV LinePiece line_piece(int it, int m, int J, int nfr)
+{
+    const int v = it * kFkTile + (int)threadIdx.x, fr = v >> 3, sub = v & 7;
+    const int g = 8 * (((fr * J) >> 3) + m) + sub;
+    return LinePiece{fr, sub, g, fr < nfr && g >= fr * J && g < fr * J + J};
+}
+RTG_DEV void line_load(ChunkRegs &r, const float *__restrict__ rows, int m, int J, int nfr)
+{
+#define RTG_LLD(I)                                                                         \
+    {                                                                                      \
+        const LinePiece P = line_piece(I, m, J, nfr);                                      \
+        r.v##I = ld4(rows + 4 * (P.ok ? P.g : 0));                                         \
+    }
+    RTG_REP8(RTG_LLD)
+#undef RTG_LLD
+}
+RTG_DEV void line_to_lds(const ChunkRegs &r, float *win, int m, int J, int nfr)
+{
+#define RTG_LST(I)                                                                         \
+    {                                                                                      \
+        const LinePiece P = line_piece(I, m, J, nfr);                                      \
+        st4(win + P.fr * kRotPitch + P.sub * 4, r.v##I);                                   \
+    }
+    RTG_REP8(RTG_LST)
+#undef RTG_LST
+}
+template <int W>
+RTG_DEV void line_store(float *__restrict__ rows, const float *win, int m, int J, int nfr)
+{
+#pragma unroll
+    for (int it = 0; it < 8; ++it) {
+        const LinePiece P = line_piece(it, m, J, nfr);
+        if (P.ok) {
+            float *gp = rows + (int64_t)W * P.g;
+            const float *lp = win + P.fr * kRotPitch + P.sub * W;
+            if (W == 4) {
+                *reinterpret_cast<float4 *>(gp) = *reinterpret_cast<const float4 *>(lp);
+            } else {
+#pragma unroll
+                for (int c = 0; c < W; ++c) gp[c] = lp[c];
+            }
+        }
+    }
+}
+// a branch parent's transform from its slot, for lanes whose schedule names one (per-lane slot index)
+RTG_DEV void slot_get_lane(const Slots &S, int nslots, int32_t sc, Q &q, V &t)
+{
+    const int si = sc & 0xFF;
+    if (nslots > 0) {
+        Q sq;
+        V st;
+        slot_get(S, si != kNoSlot ? si : 0, sq, st);
+        if (si != kNoSlot) {
+            q = sq;
+            t = st;
+        }
+    }
+}
+
+template <bool STATE>
+RTG_DEV void fk_line_tile(const TopoView &T, const float *__restrict__ local_rot, const float *__restrict__ root_t,
+                          int64_t B, int64_t f0, float *__restrict__ g_rot, float *__restrict__ g_pos, float *lds)
+{
+    const int J = T.J;
+    const int nfr = (int)((B - f0) < kFkTile ? (B - f0) : kFkTile);
+    float *win = lds;                                   // [64][kRotPitch]
+    Slots slots{lds + kFkTile * kRotPitch};
+    float *topo = slots.lds + lds_slot_floats(T.nslots);
+    const int lane = threadIdx.x;
+    const bool active = lane < nfr;
+    const int64_t r0 = f0 * J;   // the tile's first record
+    const float *in = local_rot + 4 * r0;
+    float *out_r = g_rot + 4 * r0, *out_p = g_pos + 3 * r0;
+    Q g = qident();
+    V t = V{0.0f, 0.0f, 0.0f};
+    V pk[8];
+    const V root = ld3(root_t + (f0 + (active ? lane : 0)) * 3);
+    line_topo_fill(T, topo);
+    ChunkRegs next;
+    line_load(next, in, 0, J, nfr);
+    const int M = line_steps(J);
+    for (int m = 0; m < M; ++m) {
+        line_to_lds(next, win, m, J, nfr);
+        wave_sync();
+        if (m + 1 < M) line_load(next, in, m + 1, J, nfr);   // the next lines load while this one is composed
+        const int b = 8 * (((lane * J) >> 3) + m) - lane * J;   // joint of this lane's record 0 of the step
+        float *R = win + lane * kRotPitch;
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+            const int j = b + k;
+            const bool ok = active && j >= 0 && j < J;
+            const int jj = j < 0 ? 0 : (j >= J ? J - 1 : j);
+            const float *tp = topo + 8 * jj;
+            const int32_t sc = __float_as_int(tp[3]);
+            Q lq = Q{R[4 * k], R[4 * k + 1], R[4 * k + 2], R[4 * k + 3]};
+            Q pg = g;
+            V pt = t;
+            slot_get_lane(slots, T.nslots, sc, pg, pt);
+            Q ng;
+            V nt;
+            if (j == 0) {   // root: global = local, unnormalised (kinematics.py:27-29)
+                ng = lq;
+                nt = root;
+            } else {
+                if (STATE) lq = qmul_norm(Q{tp[4], tp[5], tp[6], tp[7]}, lq);   // skeleton3d.py:412-418
+                const V rv = qrotate(pg, V{tp[0], tp[1], tp[2]});
+                ng = qmul_norm(pg, lq);
+                nt = V{rv.x + pt.x, rv.y + pt.y, rv.z + pt.z};
+            }
+            R[4 * k] = ng.x; R[4 * k + 1] = ng.y; R[4 * k + 2] = ng.z; R[4 * k + 3] = ng.w;
+            pk[k] = nt;
+            if (ok && ((sc >> 8) & 0xFF) != kNoSlot) slot_put(slots, (sc >> 8) & 0xFF, ng, nt);
+            if (ok) {
+                g = ng;
+                t = nt;
+            }
+        }
+        wave_sync();
+        line_store<4>(out_r, win, m, J, nfr);
+        wave_sync();   // the rotation lines are out: the window takes the positions
+#pragma unroll
+        for (int k = 0; k < 8; ++k) { R[3 * k] = pk[k].x; R[3 * k + 1] = pk[k].y; R[3 * k + 2] = pk[k].z; }
+        wave_sync();
+        line_store<3>(out_p, win, m, J, nfr);
+        wave_sync();
+    }
+}
+
+template <bool STATE>
+RTG_DEV void lrot_line_tile(const TopoView &T, const float *__restrict__ g_rot, int64_t B, int64_t f0,
+                            float *__restrict__ local_rot, float *lds)
+{
+    const int J = T.J;
+    const int nfr = (int)((B - f0) < kFkTile ? (B - f0) : kFkTile);
+    float *win = lds;
+    Slots slots{lds + kFkTile * kRotPitch};
+    float *topo = slots.lds + lds_slot_floats(T.nslots);
+    const int lane = threadIdx.x;
+    const bool active = lane < nfr;
+    const int64_t r0 = f0 * J;
+    const float *in = g_rot + 4 * r0;
+    float *out = local_rot + 4 * r0;
+    Q prev = qident();
+    line_topo_fill(T, topo);
+    ChunkRegs next;
+    line_load(next, in, 0, J, nfr);
+    const int M = line_steps(J);
+    for (int m = 0; m < M; ++m) {
+        line_to_lds(next, win, m, J, nfr);
+        wave_sync();
+        if (m + 1 < M) line_load(next, in, m + 1, J, nfr);
+        const int b = 8 * (((lane * J) >> 3) + m) - lane * J;
+        float *W = win + lane * kRotPitch;
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+            const int j = b + k;
+            const bool ok = active && j >= 0 && j < J;
+            const int jj = j < 0 ? 0 : (j >= J ? J - 1 : j);
+            const float *tp = topo + 8 * jj;
+            const int32_t sc = __float_as_int(tp[3]);
+            const Q gj = Q{W[4 * k], W[4 * k + 1], W[4 * k + 2], W[4 * k + 3]};
+            Q q = gj;   // root copied (kinematics.py:49)
+            if (j > 0) {
+                Q gp = prev;
+                V unused = V{0.0f, 0.0f, 0.0f};
+                slot_get_lane(slots, T.nslots, sc, gp, unused);
+                q = qmul_norm(qconj(gp), gj);
+                if (STATE) q = qmul_norm(qnormalize(qconj(Q{tp[4], tp[5], tp[6], tp[7]})), q);   // skeleton3d.py:470-478
+            }
+            if (ok && ((sc >> 8) & 0xFF) != kNoSlot) slot_put(slots, (sc >> 8) & 0xFF, gj, V{0.0f, 0.0f, 0.0f});
+            W[4 * k] = q.x; W[4 * k + 1] = q.y; W[4 * k + 2] = q.z; W[4 * k + 3] = q.w;
+            if (ok) prev = gj;
+        }
+        wave_sync();
+        line_store<4>(out, win, m, J, nfr);
+        wave_sync();
+    }
+}
+
+template <bool STATE>
+__global__ __launch_bounds__(kFkTile) void k_fk_line(TopoView T, const float *__restrict__ local_rot,
+                                                     const float *__restrict__ root_t, int64_t B,
+                                                     float *__restrict__ g_rot, float *__restrict__ g_pos)
+{
+    extern __shared__ __attribute__((aligned(16))) float fk_lds[];
+    fk_line_tile<STATE>(T, local_rot, root_t, B, (int64_t)blockIdx.x * kFkTile, g_rot, g_pos, fk_lds);
+}
+template <bool STATE>
+__global__ __launch_bounds__(kFkTile) void k_local_rotation_line(TopoView T, const float *__restrict__ g_rot,
+                                                                 int64_t B, float *__restrict__ local_rot)
+{
+    extern __shared__ __attribute__((aligned(16))) float fk_lds[];
+    lrot_line_tile<STATE>(T, g_rot, B, (int64_t)blockIdx.x * kFkTile, local_rot, fk_lds);
+}
+__global__ __launch_bounds__(kFkTile) void k_fk_multi_line(FkMultiArgs A)
+{
+    extern __shared__ __attribute__((aligned(16))) float fk_lds[];
+    int s = 0;
+#pragma unroll
+    for (int i = 1; i < RTG_MAX_SEGMENTS; ++i)
+        if (i < A.n && (int64_t)blockIdx.x >= A.block_start[i]) s = i;
+    const FkSeg &S = A.seg[s];
+    const int64_t f0 = ((int64_t)blockIdx.x - A.block_start[s]) * kFkTile;
+    if (S.op == 0) fk_line_tile<false>(S.T, S.local_rot, S.root_t, S.B, f0, S.g_rot, S.g_pos, fk_lds);
+    else lrot_line_tile<false>(S.T, S.local_rot, S.B, f0, S.g_rot, fk_lds);
+}
+
 __global__ __launch_bounds__(256) void k_fk_multi(FkMultiArgs A)
 {
     int s = 0;
@@ -498,6 +743,12 @@ hipError_t launch_fk(const TopoView &T, bool state, const float *lr, const float
 {
     if (T.nslots <= kMaxFkSlots) {
         const dim3 g(grid_for(B, kFkTile)), b(kFkTile);
+        if (RTG_FK_LINE) {
+            const size_t lds = fk_line_lds_bytes(T.J, T.nslots);
+            if (state) hipLaunchKernelGGL(k_fk_line<true>, g, b, lds, s, T, lr, rt, B, gr, gp);
+            else hipLaunchKernelGGL(k_fk_line<false>, g, b, lds, s, T, lr, rt, B, gr, gp);
+            return hipGetLastError();
+        }
         const size_t lds = fk_stream_lds_bytes(T.nslots);
         if (state) hipLaunchKernelGGL(k_fk_stream<true>, g, b, lds, s, T, lr, rt, B, gr, gp);
         else hipLaunchKernelGGL(k_fk_stream<false>, g, b, lds, s, T, lr, rt, B, gr, gp);
@@ -513,6 +764,12 @@ hipError_t launch_local_rotation(const TopoView &T, bool state, const float *g, 
 {
     if (T.nslots <= kMaxFkSlots) {
         const dim3 gd(grid_for(B, kFkTile)), b(kFkTile);
+        if (RTG_FK_LINE) {
+            const size_t lds = fk_line_lds_bytes(T.J, T.nslots);
+            if (state) hipLaunchKernelGGL(k_local_rotation_line<true>, gd, b, lds, s, T, g, B, l);
+            else hipLaunchKernelGGL(k_local_rotation_line<false>, gd, b, lds, s, T, g, B, l);
+            return hipGetLastError();
+        }
         const size_t lds = fk_stream_lds_bytes(T.nslots);
         if (state) hipLaunchKernelGGL(k_local_rotation_stream<true>, gd, b, lds, s, T, g, B, l);
         else hipLaunchKernelGGL(k_local_rotation_stream<false>, gd, b, lds, s, T, g, B, l);
@@ -537,7 +794,11 @@ hipError_t launch_fk_multi(FkMultiArgs &A, hipStream_t s)
     }
     for (int i = A.n; i < RTG_MAX_SEGMENTS; ++i) A.block_start[i] = blocks;
     if (blocks == 0) return hipSuccess;
-    if (stream)
+    int maxJ = 0;
+    for (int i = 0; i < A.n; ++i) maxJ = A.seg[i].T.J > maxJ ? A.seg[i].T.J : maxJ;
+    if (stream && RTG_FK_LINE)
+        hipLaunchKernelGGL(k_fk_multi_line, dim3((unsigned)blocks), dim3(kFkTile), fk_line_lds_bytes(maxJ, maxS), s, A);
+    else if (stream)
         hipLaunchKernelGGL(k_fk_multi_stream, dim3((unsigned)blocks), dim3(kFkTile), fk_stream_lds_bytes(maxS, true), s, A);
     else
         hipLaunchKernelGGL(k_fk_multi, dim3((unsigned)blocks), dim3(256), 0, s, A);

@@ -64,7 +64,11 @@ def main(B=262144, layout="soa", reps=5):
         # residency rounds: a block starts in round 2 once some earlier block has ended
         first_end = end.min()
         rnd = np.where(start < first_end, 1, 2)
+        pct = lambda v: {f"p{q}": round(float(np.percentile(v, q)), 2) for q in (0, 10, 50, 90, 99, 100)}
         res = {"kernel_us": float(end.max()), "round1_blocks": int((rnd == 1).sum()),
+               "start_us": {f"round{rr}": pct(start[rnd == rr]) for rr in (1, 2) if (rnd == rr).any()},
+               "end_us": {f"round{rr}": pct(end[rnd == rr]) for rr in (1, 2) if (rnd == rr).any()},
+               "block_us": {f"round{rr}": pct((end - start)[rnd == rr]) for rr in (1, 2) if (rnd == rr).any()},
                "round2_blocks": int((rnd == 2).sum()),
                "start_us_p50_round2": float(np.median(start[rnd == 2])) if (rnd == 2).any() else None,
                "end_us_p50_round1": float(np.median(end[rnd == 1]))}
