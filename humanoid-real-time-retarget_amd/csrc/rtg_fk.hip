@@ -302,77 +302,6 @@ __global__ __launch_bounds__(kFkTile) void k_fk_stream(TopoView T, const float *
     fk_stream_tile<STATE>(T, local_rot, root_t, B, (int64_t)blockIdx.x * kFkTile, g_rot, g_pos, fk_lds);
 }
 
-// inverse FK, streamed the same way: local[j] = normalise(conj(g[p]) * g[j]) (kinematics.py:41-63).
-// The previous joint's global rotation stays in registers; branch parents come from slots.
-template <bool STATE, bool POS16 = false>
-RTG_DEV void local_rotation_tile(const TopoView &T, const float *__restrict__ g_rot, int64_t B, int64_t f0,
-                                 float *__restrict__ local_rot, float *fk_lds)
-{
-    const int J = T.J;
-    const int nfr = (int)((B - f0) < kFkTile ? (B - f0) : kFkTile);
-    float *win = fk_lds;                                 // [64][kRotPitch]
-    Slots slots{fk_lds + kFkTile * kRotPitch + pos_win<POS16>()};   // the same LDS slot offset as fk_stream_tile
-    const int lane = threadIdx.x;
-    Q prev = qident();
-    V unused = V{0.0f, 0.0f, 0.0f};
-    ChunkRegs next;
-    chunk_load(next, g_rot, f0, nfr, J, 0, J < kFkChunk ? J : kFkChunk);
-    for (int c0 = 0; c0 < J; c0 += kFkChunk) {
-        const int nC = (J - c0) < kFkChunk ? (J - c0) : kFkChunk;
-        chunk_to_lds(next, win, nfr, nC);
-        wave_sync();
-        if (c0 + kFkChunk < J)
-            chunk_load(next, g_rot, f0, nfr, J, c0 + kFkChunk,
-                       (J - c0 - kFkChunk) < kFkChunk ? (J - c0 - kFkChunk) : kFkChunk);
-        if (lane < nfr) {
-            float *W = win + lane * kRotPitch;
-#pragma unroll
-            for (int k = 0; k < kFkChunk; ++k) {
-                if (k >= nC) break;
-                const int j = c0 + k;
-                const int32_t sc = ld_const(T.sched + j);
-                const Q gj = Q{W[4 * k], W[4 * k + 1], W[4 * k + 2], W[4 * k + 3]};
-                Q q = gj;   // root copied (kinematics.py:49)
-                if (j > 0) {
-                    Q gp = prev;
-                    if ((sc & 0xFF) != kNoSlot) slot_get(slots, sc & 0xFF, gp, unused);
-                    q = qmul_norm(qconj(gp), gj);
-                    if (STATE) q = qmul_norm(qnormalize(qconj(ld_const(T.tree_quat + j))), q);   // skeleton3d.py:470-478
-                }
-                if (((sc >> 8) & 0xFF) != kNoSlot) slot_put(slots, (sc >> 8) & 0xFF, gj, unused);
-                W[4 * k] = q.x; W[4 * k + 1] = q.y; W[4 * k + 2] = q.z; W[4 * k + 3] = q.w;
-                prev = gj;
-            }
-        }
-        wave_sync();
-        chunk_store<4>(local_rot, win, kRotPitch, f0, nfr, J, c0, nC);
-        wave_sync();
-    }
-}
-
-template <bool STATE>
-__global__ __launch_bounds__(kFkTile) void k_local_rotation_stream(TopoView T, const float *__restrict__ g_rot,
-                                                                   int64_t B, float *__restrict__ local_rot)
-{
-    extern __shared__ __attribute__((aligned(16))) float fk_lds[];
-    local_rotation_tile<STATE>(T, g_rot, B, (int64_t)blockIdx.x * kFkTile, local_rot, fk_lds);
-}
-
-// Mixed-target kinematics (BASELINE config 5): every 64-frame tile of every segment is one wave; a segment is FK
-// (op 0) or inverse FK (op 1), so FK and inverse FK of several skeletons share one launch.
-__global__ __launch_bounds__(kFkTile) void k_fk_multi_stream(FkMultiArgs A)
-{
-    extern __shared__ __attribute__((aligned(16))) float fk_lds[];
-    int s = 0;
-#pragma unroll
-    for (int i = 1; i < RTG_MAX_SEGMENTS; ++i)
-        if (i < A.n && (int64_t)blockIdx.x >= A.block_start[i]) s = i;
-    const FkSeg &S = A.seg[s];
-    const int64_t f0 = ((int64_t)blockIdx.x - A.block_start[s]) * kFkTile;
-    if (S.op == 0) fk_stream_tile<false, true>(S.T, S.local_rot, S.root_t, S.B, f0, S.g_rot, S.g_pos, fk_lds);
-    else local_rotation_tile<false, true>(S.T, S.local_rot, S.B, f0, S.g_rot, fk_lds);
-}
-
 // Joint-angle FK (HuForwardModel.forward_kinematics, hu_forward_model.py:17-33): the streaming tile of
 // k_fk_stream, but joint j's local rotation is built in-lane from its DOF --
 // quat_from_angle_axis(a', e_axis) with a' = (clamp(a) - a) + a when clipping -- so no (B,J,4) local-rotation
@@ -474,7 +403,7 @@ __global__ __launch_bounds__(kFkTile) void k_dof_fk(TopoView T, DofView D, const
 }
 
 // ----------------------------------------------------------------------------
-// Line-synchronous streaming (RTG_FK_LINE).  A 64-frame tile's rows are 64 J records of 16 B, i.e. 8 J whole
+// Inverse FK, line-synchronous (k_local_rotation_line; the inverse segments of k_fk_multi_stream).  A 64-frame tile's rows are 64 J records of 16 B, i.e. 8 J whole
 // 128-byte lines, and a frame's row starts (f J) mod 8 records into a line.  The windowed kernels above move, per
 // frame, joints [8k, 8k+8): a 128-B piece at 16-B alignment that straddles two lines, so every line is requested by
 // two windows ~15 us apart and the second request misses L2 (FETCH 1.75x the input on Hu FK).  Here, at step m,
@@ -484,7 +413,10 @@ __global__ __launch_bounds__(kFkTile) void k_dof_fk(TopoView T, DofView D, const
 // joint index at a step differs across lanes, so the topology (local_t, schedule, tree quaternion) is read from an
 // LDS table instead of scalar registers, and J joints take ceil((J + 8 - gcd(J, 8)) / 8) steps of 8 (Hu: 5 x 8
 // for 31).  Per lane the joints are still composed in index order with the same operations, so the bits are the
-// windowed kernels'.
+// windowed kernel's.  Measured (tools/fk_pattern_probe.hip, Hu, B = 262144): the bare copy pattern takes 104 us
+// against 115 us for the windows; inverse FK 75.7 vs 82.7 us with the windows, bit-exact.  Forward FK in this form
+// was SLOWER (123 vs 120 us; the mixed launch 147 vs 132 us): its heavier chain pays for the extra step slots and
+// the per-lane topology reads, so forward FK keeps the windows above (git history has the line form).
 // ----------------------------------------------------------------------------
 RTG_DEV int line_steps(int J)
 {
@@ -571,75 +503,6 @@ RTG_DEV void slot_get_lane(const Slots &S, int nslots, int32_t sc, Q &q, V &t)
 }
 
 template <bool STATE>
-RTG_DEV void fk_line_tile(const TopoView &T, const float *__restrict__ local_rot, const float *__restrict__ root_t,
-                          int64_t B, int64_t f0, float *__restrict__ g_rot, float *__restrict__ g_pos, float *lds)
-{
-    const int J = T.J;
-    const int nfr = (int)((B - f0) < kFkTile ? (B - f0) : kFkTile);
-    float *win = lds;                                   // [64][kRotPitch]
-    Slots slots{lds + kFkTile * kRotPitch};
-    float *topo = slots.lds + lds_slot_floats(T.nslots);
-    const int lane = threadIdx.x;
-    const bool active = lane < nfr;
-    const int64_t r0 = f0 * J;   // the tile's first record
-    const float *in = local_rot + 4 * r0;
-    float *out_r = g_rot + 4 * r0, *out_p = g_pos + 3 * r0;
-    Q g = qident();
-    V t = V{0.0f, 0.0f, 0.0f};
-    V pk[8];
-    const V root = ld3(root_t + (f0 + (active ? lane : 0)) * 3);
-    line_topo_fill(T, topo);
-    ChunkRegs next;
-    line_load(next, in, 0, J, nfr);
-    const int M = line_steps(J);
-    for (int m = 0; m < M; ++m) {
-        line_to_lds(next, win, m, J, nfr);
-        wave_sync();
-        if (m + 1 < M) line_load(next, in, m + 1, J, nfr);   // the next lines load while this one is composed
-        const int b = 8 * (((lane * J) >> 3) + m) - lane * J;   // joint of this lane's record 0 of the step
-        float *R = win + lane * kRotPitch;
-#pragma unroll
-        for (int k = 0; k < 8; ++k) {
-            const int j = b + k;
-            const bool ok = active && j >= 0 && j < J;
-            const int jj = j < 0 ? 0 : (j >= J ? J - 1 : j);
-            const float *tp = topo + 8 * jj;
-            const int32_t sc = __float_as_int(tp[3]);
-            Q lq = Q{R[4 * k], R[4 * k + 1], R[4 * k + 2], R[4 * k + 3]};
-            Q pg = g;
-            V pt = t;
-            slot_get_lane(slots, T.nslots, sc, pg, pt);
-            Q ng;
-            V nt;
-            if (j == 0) {   // root: global = local, unnormalised (kinematics.py:27-29)
-                ng = lq;
-                nt = root;
-            } else {
-                if (STATE) lq = qmul_norm(Q{tp[4], tp[5], tp[6], tp[7]}, lq);   // skeleton3d.py:412-418
-                const V rv = qrotate(pg, V{tp[0], tp[1], tp[2]});
-                ng = qmul_norm(pg, lq);
-                nt = V{rv.x + pt.x, rv.y + pt.y, rv.z + pt.z};
-            }
-            R[4 * k] = ng.x; R[4 * k + 1] = ng.y; R[4 * k + 2] = ng.z; R[4 * k + 3] = ng.w;
-            pk[k] = nt;
-            if (ok && ((sc >> 8) & 0xFF) != kNoSlot) slot_put(slots, (sc >> 8) & 0xFF, ng, nt);
-            if (ok) {
-                g = ng;
-                t = nt;
-            }
-        }
-        wave_sync();
-        line_store<4>(out_r, win, m, J, nfr);
-        wave_sync();   // the rotation lines are out: the window takes the positions
-#pragma unroll
-        for (int k = 0; k < 8; ++k) { R[3 * k] = pk[k].x; R[3 * k + 1] = pk[k].y; R[3 * k + 2] = pk[k].z; }
-        wave_sync();
-        line_store<3>(out_p, win, m, J, nfr);
-        wave_sync();
-    }
-}
-
-template <bool STATE>
 RTG_DEV void lrot_line_tile(const TopoView &T, const float *__restrict__ g_rot, int64_t B, int64_t f0,
                             float *__restrict__ local_rot, float *lds)
 {
@@ -691,21 +554,15 @@ RTG_DEV void lrot_line_tile(const TopoView &T, const float *__restrict__ g_rot, 
 }
 
 template <bool STATE>
-__global__ __launch_bounds__(kFkTile) void k_fk_line(TopoView T, const float *__restrict__ local_rot,
-                                                     const float *__restrict__ root_t, int64_t B,
-                                                     float *__restrict__ g_rot, float *__restrict__ g_pos)
-{
-    extern __shared__ __attribute__((aligned(16))) float fk_lds[];
-    fk_line_tile<STATE>(T, local_rot, root_t, B, (int64_t)blockIdx.x * kFkTile, g_rot, g_pos, fk_lds);
-}
-template <bool STATE>
 __global__ __launch_bounds__(kFkTile) void k_local_rotation_line(TopoView T, const float *__restrict__ g_rot,
                                                                  int64_t B, float *__restrict__ local_rot)
 {
     extern __shared__ __attribute__((aligned(16))) float fk_lds[];
     lrot_line_tile<STATE>(T, g_rot, B, (int64_t)blockIdx.x * kFkTile, local_rot, fk_lds);
 }
-__global__ __launch_bounds__(kFkTile) void k_fk_multi_line(FkMultiArgs A)
+// Mixed-target kinematics (BASELINE config 5): every 64-frame tile of every segment is one wave; a segment is FK
+// (op 0) or inverse FK (op 1), so FK and inverse FK of several skeletons share one launch.
+__global__ __launch_bounds__(kFkTile) void k_fk_multi_stream(FkMultiArgs A)
 {
     extern __shared__ __attribute__((aligned(16))) float fk_lds[];
     int s = 0;
@@ -714,7 +571,7 @@ __global__ __launch_bounds__(kFkTile) void k_fk_multi_line(FkMultiArgs A)
         if (i < A.n && (int64_t)blockIdx.x >= A.block_start[i]) s = i;
     const FkSeg &S = A.seg[s];
     const int64_t f0 = ((int64_t)blockIdx.x - A.block_start[s]) * kFkTile;
-    if (S.op == 0) fk_line_tile<false>(S.T, S.local_rot, S.root_t, S.B, f0, S.g_rot, S.g_pos, fk_lds);
+    if (S.op == 0) fk_stream_tile<false, true>(S.T, S.local_rot, S.root_t, S.B, f0, S.g_rot, S.g_pos, fk_lds);
     else lrot_line_tile<false>(S.T, S.local_rot, S.B, f0, S.g_rot, fk_lds);
 }
 
@@ -743,12 +600,6 @@ hipError_t launch_fk(const TopoView &T, bool state, const float *lr, const float
 {
     if (T.nslots <= kMaxFkSlots) {
         const dim3 g(grid_for(B, kFkTile)), b(kFkTile);
-        if (RTG_FK_LINE) {
-            const size_t lds = fk_line_lds_bytes(T.J, T.nslots);
-            if (state) hipLaunchKernelGGL(k_fk_line<true>, g, b, lds, s, T, lr, rt, B, gr, gp);
-            else hipLaunchKernelGGL(k_fk_line<false>, g, b, lds, s, T, lr, rt, B, gr, gp);
-            return hipGetLastError();
-        }
         const size_t lds = fk_stream_lds_bytes(T.nslots);
         if (state) hipLaunchKernelGGL(k_fk_stream<true>, g, b, lds, s, T, lr, rt, B, gr, gp);
         else hipLaunchKernelGGL(k_fk_stream<false>, g, b, lds, s, T, lr, rt, B, gr, gp);
@@ -764,15 +615,9 @@ hipError_t launch_local_rotation(const TopoView &T, bool state, const float *g, 
 {
     if (T.nslots <= kMaxFkSlots) {
         const dim3 gd(grid_for(B, kFkTile)), b(kFkTile);
-        if (RTG_FK_LINE) {
-            const size_t lds = fk_line_lds_bytes(T.J, T.nslots);
-            if (state) hipLaunchKernelGGL(k_local_rotation_line<true>, gd, b, lds, s, T, g, B, l);
-            else hipLaunchKernelGGL(k_local_rotation_line<false>, gd, b, lds, s, T, g, B, l);
-            return hipGetLastError();
-        }
-        const size_t lds = fk_stream_lds_bytes(T.nslots);
-        if (state) hipLaunchKernelGGL(k_local_rotation_stream<true>, gd, b, lds, s, T, g, B, l);
-        else hipLaunchKernelGGL(k_local_rotation_stream<false>, gd, b, lds, s, T, g, B, l);
+        const size_t lds = fk_line_lds_bytes(T.J, T.nslots);
+        if (state) hipLaunchKernelGGL(k_local_rotation_line<true>, gd, b, lds, s, T, g, B, l);
+        else hipLaunchKernelGGL(k_local_rotation_line<false>, gd, b, lds, s, T, g, B, l);
     } else if (state) {
         hipLaunchKernelGGL(k_local_rotation<true>, dim3(grid_for(B, 256)), dim3(256), 0, s, T, g, B, l);
     } else {
@@ -796,10 +641,10 @@ hipError_t launch_fk_multi(FkMultiArgs &A, hipStream_t s)
     if (blocks == 0) return hipSuccess;
     int maxJ = 0;
     for (int i = 0; i < A.n; ++i) maxJ = A.seg[i].T.J > maxJ ? A.seg[i].T.J : maxJ;
-    if (stream && RTG_FK_LINE)
-        hipLaunchKernelGGL(k_fk_multi_line, dim3((unsigned)blocks), dim3(kFkTile), fk_line_lds_bytes(maxJ, maxS), s, A);
-    else if (stream)
-        hipLaunchKernelGGL(k_fk_multi_stream, dim3((unsigned)blocks), dim3(kFkTile), fk_stream_lds_bytes(maxS, true), s, A);
+    if (stream) {   // FK segments use the windows (16-joint position window), inverse segments the line tile
+        const size_t lf = fk_stream_lds_bytes(maxS, true), ll = fk_line_lds_bytes(maxJ, maxS);
+        hipLaunchKernelGGL(k_fk_multi_stream, dim3((unsigned)blocks), dim3(kFkTile), lf > ll ? lf : ll, s, A);
+    }
     else
         hipLaunchKernelGGL(k_fk_multi, dim3((unsigned)blocks), dim3(256), 0, s, A);
     return hipGetLastError();

@@ -12,9 +12,6 @@
 #ifndef RTG_LATENCY_MAX_B
 #define RTG_LATENCY_MAX_B 49152   // 2 <= B <= this: k_fbp_latency5 (swept: faster up to 49152, slower at 65536)
 #endif
-#ifndef RTG_SOA_NT_LOADS
-#define RTG_SOA_NT_LOADS 0   // A/B in progress: SoA input planes loaded non-temporal
-#endif
 #ifndef RTG_EXP_HOT_INPUTS
 #define RTG_EXP_HOT_INPUTS 0   // measurement knob: every side-kernel tile reads the first block's rows (wrong answers)
 #endif
@@ -25,9 +22,6 @@
 #define RTG_EXP_SKIP_SIGNAL 0   // measurement knob: block 0's first R10 hand-over is never raised, so its partner wave
 #endif                          // times out (tests the RTG_DEVERR_HANDOVER_TIMEOUT report; wrong answers)
 // ---- used by rtg_fk.hip
-#ifndef RTG_FK_LINE
-#define RTG_FK_LINE 0   // A/B in progress: line-synchronous FK / inverse FK / mixed tiles (k_fk_line)
-#endif
 #ifndef RTG_EXP_FK_COPY
 #define RTG_EXP_FK_COPY 0   // measurement knob: k_fk_stream copies its windows out without the chain (wrong answers)
 #endif

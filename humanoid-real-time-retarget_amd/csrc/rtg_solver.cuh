@@ -180,11 +180,7 @@ template <>
 struct FV<true> {
     const float *__restrict__ p;
     int64_t s;
-#if RTG_SOA_NT_LOADS   // A/B knob: once-read SoA planes loaded non-temporal (the angle table keeps the L2)
-    RTG_DEV float e(int64_t i) const { return __builtin_nontemporal_load(p + i); }
-#else
     RTG_DEV float e(int64_t i) const { return p[i]; }
-#endif
     RTG_DEV V p3(int j) const { return V{e((3 * j) * s), e((3 * j + 1) * s), e((3 * j + 2) * s)}; }
     RTG_DEV Q q4(int j) const { return Q{e((4 * j) * s), e((4 * j + 1) * s), e((4 * j + 2) * s), e((4 * j + 3) * s)}; }
 };

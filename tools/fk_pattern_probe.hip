@@ -76,6 +76,38 @@ __global__ __launch_bounds__(64) void k_line(const float4 *__restrict__ in, floa
     }
 }
 
+// line, but each rotation line's 96-B position piece leaves as 6 lanes x 16 B (whole piece; a piece two frames
+// share is written whole by both, with the same bytes -- fine for a pattern probe, not for the product)
+__global__ __launch_bounds__(64) void k_line_p4(const float4 *__restrict__ in, float4 *__restrict__ rot,
+                                                float *__restrict__ pos, int64_t B)
+{
+    const int64_t f0 = (int64_t)blockIdx.x * kTile;
+    const int64_t R0 = f0 * J;
+    for (int m = 0; m < (J + 7) / 8 + 1; ++m) {
+#pragma unroll
+        for (int it = 0; it < 8; ++it) {
+            const int v = it * 64 + threadIdx.x, fr = v / 8, sub = v % 8;
+            const int first = (fr * J) / 8;
+            const int g = 8 * (first + m) + sub;
+            if (g >= fr * J && g < fr * J + J && f0 + fr < B) rot[R0 + g] = in[R0 + g];
+        }
+#pragma unroll
+        for (int it = 0; it < 6; ++it) {
+            const int v = it * 64 + threadIdx.x, fr = v / 6, c = v % 6;
+            const int first = (fr * J) / 8, last = (fr * J + J - 1) / 8;
+            const int L = first + m;
+            if (L <= last && f0 + fr < B) {
+                float o[4];
+                for (int e = 0; e < 4; ++e) {
+                    const int64_t fl = 24 * (int64_t)L + 4 * c + e;   // float in the tile's position rows
+                    o[e] = (float)(R0 + fl / 3 + fl % 3);
+                }
+                reinterpret_cast<float4 *>(pos + 3 * R0)[6 * (int64_t)L + c] = make_float4(o[0], o[1], o[2], o[3]);
+            }
+        }
+    }
+}
+
 __global__ __launch_bounds__(64) void k_linear(const float4 *__restrict__ in, float4 *__restrict__ rot,
                                                float *__restrict__ pos, int64_t B)
 {
@@ -104,7 +136,7 @@ int main(int argc, char **argv)
     CK(hipMemcpy(in, h.data(), nr * 16, hipMemcpyHostToDevice));
     const double bytes = (double)nr * (16 + 16 + 12);
     const unsigned grid = (unsigned)((B + kTile - 1) / kTile);
-    struct { const char *name; Kern k; } ks[] = {{"win", k_win}, {"line", k_line}, {"linear", k_linear}};
+    struct { const char *name; Kern k; } ks[] = {{"win", k_win}, {"line", k_line}, {"line_p4", k_line_p4}, {"linear", k_linear}};
     hipEvent_t a, b;
     CK(hipEventCreate(&a));
     CK(hipEventCreate(&b));
