@@ -12,15 +12,18 @@ cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
 out=gpurun_out/prof_$tag
 mkdir -p $out
 B="python bench.py --steps 10 --warmup 2 --no-cpu-baseline"
+# the PMC passes count bytes and instructions, which the clock does not change: no clock-settle phase there
+export RTG_BENCH_SETTLE_MS=0
 pmc() {   # pmc <name> <lib or -> <counters...>
   name=$1; lib=$2; shift 2
   if [ "$lib" = "-" ]; then env_lib=""; else env_lib="$lib"; fi
   RTG_ALLOW_MEASUREMENT_BUILD=1 RTG_LIB=${env_lib:-$PWD/humanoid-real-time-retarget_amd/librtg_hip.so} timeout -s KILL 120 \
     rocprofv3 --pmc "$@" -d $out/$name -o $name --output-format csv -- $B > $out/$name.log 2>&1
 }
-timeout -k 10 300 python bench.py > $out/bench.log 2>&1
-timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $out/trace -o trace --output-format csv \
+RTG_BENCH_SETTLE_MS=200 timeout -k 10 300 python bench.py > $out/bench.log 2>&1
+RTG_BENCH_SETTLE_MS=200 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $out/trace -o trace --output-format csv \
   -- python bench.py --steps 20 --no-cpu-baseline > $out/trace.log 2>&1
+python tools/trace_summary.py $out/trace/trace_kernel_trace.csv 12 10 > $out/trace_by_grid.txt 2>&1 || true
 pmc fetch - FETCH_SIZE
 pmc write - WRITE_SIZE
 pmc sq - SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_VALU_ADD_F64 SQ_INSTS_VALU_MUL_F64 SQ_INSTS_VALU_FMA_F64 \
