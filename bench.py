@@ -16,6 +16,7 @@ import argparse
 import hashlib
 import json
 import os
+import shutil
 import subprocess
 import sys
 import time
@@ -124,9 +125,13 @@ def barrier(world, backend=None):
 
 def rocm_smi_clocks(dev: int):
     """Current sclk / mclk as rocm-smi reports them for this device (None when rocm-smi is unavailable)."""
+    if "rocprof" in os.environ.get("LD_PRELOAD", ""):
+        return None   # under rocprofv3 a child process would initialise the GPU through the profiler's preload
     try:
-        r = subprocess.run(["rocm-smi", "-d", str(dev), "--showclocks", "--json"], capture_output=True, text=True,
-                           timeout=30)
+        # the script through this interpreter: no `#!/usr/bin/env` hop (an exec) in the child
+        smi = os.path.realpath(shutil.which("rocm-smi") or "/opt/rocm/bin/rocm-smi")
+        r = subprocess.run([sys.executable, smi, "-d", str(dev), "--showclocks", "--json"], capture_output=True,
+                           text=True, timeout=30)
         card = next(iter(json.loads(r.stdout).values()))
         return {k: v for k, v in card.items() if "sclk" in k or "mclk" in k}
     except Exception:  # noqa: BLE001
@@ -218,7 +223,7 @@ def cpu_baseline(body, lh, rh, zl, zg, seconds):
     return out
 
 
-PMC_JSON = os.path.join(REPO, "profiles", "pmc_r03.json")
+PMC_JSON = os.path.join(REPO, "profiles", "pmc_r04.json")
 PMC_KERNELS = {"soa": "rtg::k_solve_sides<0, true, true>", "aos": "rtg::k_solve_sides<0, true, false>"}
 VALU_PEAK_LANE_OPS = 256 * 4 * 32 * 2.4e9   # MI355X: CUs x SIMDs x lanes issued per cycle x 2.4 GHz (78.6 T/s)
 
