@@ -68,8 +68,9 @@ class BaseHumanoidRetargeter(ABC):
         A single frame of host inputs (the live teleop loop) goes to the resident frame server (FULL_BODY_POS) or a
         one-launch frame call over pinned memory (rtg.realtime.per_frame_runner).  A single frame the reference
         raises on raises the same exception here (rtg.h rtg_frame_error); a batch marks such frames instead."""
-        dev = home_device(*inputs)
-        if not batched and dev == _CPU:
+        x0 = inputs[0]
+        host = (x0.is_cpu if type(x0) is torch.Tensor else home_device(*inputs) == _CPU) if not batched else False
+        if host:
             if self._frame_runner is None:   # one runner per solver; FULL_BODY_POS always carries body_rot
                 from rtg.realtime import per_frame_runner
                 self._frame_runner = per_frame_runner(self.solver, self.SOLVER_KIND == _lib.SOLVER_FULL_BODY_POS,
@@ -78,6 +79,7 @@ class BaseHumanoidRetargeter(ABC):
             if self._frame_runner.status:   # the frame is marked (read off the host row, no torch op)
                 raise_frame_error(self._frame_runner.status)
             return lr, dof, (br if want_body_rot else None)
+        dev = home_device(*inputs)
         tails = [tuple(as_tensor(x).shape[-2:]) for x in inputs]
         xs = [dev_f32(as_tensor(x).reshape(-1, *t)) for x, t in zip(inputs, tails)]
         dof, lr, br = self.solver.retarget(xs, want_local_rot=True, want_body_rot=want_body_rot)

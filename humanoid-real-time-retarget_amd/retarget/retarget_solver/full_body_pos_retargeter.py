@@ -7,8 +7,11 @@ finger-spread gripper -- one frame per GPU lane (``RTG_SOLVER_FULL_BODY_POS``).
 """
 from __future__ import annotations
 
+import torch
+
 from rtg import _lib, ops
 from rtg.bridge import as_tensor, back, home_device
+from rtg.runtime import raise_frame_error
 
 from retarget.retarget_solver.base_retargeter import BaseHumanoidRetargeter
 
@@ -25,8 +28,14 @@ class VtrdynFullBodyPosRetargeter(BaseHumanoidRetargeter):
         """One frame: body (21,3), hands (20,3) -> (local_rot (31,4), dof (30,), body_global_rotation (59,4)).
         Raises where the reference raises: RuntimeError (torch.linalg.svd of a NaN Kabsch matrix, transform3d.py:40)
         or ValueError (scipy's zero-norm quaternion, transform3d.py:53); nothing is recorded then."""
-        lr, dof, br = self._solve([body_global_translation, left_hand_global_translation,
-                                   right_hand_global_translation], batched=False, want_body_rot=True)
+        fr, b = self._frame_runner, body_global_translation
+        if fr is not None and type(b) is torch.Tensor and b.is_cpu:   # the live loop's frame: straight to the runner
+            lr, dof, br = fr(b, left_hand_global_translation, right_hand_global_translation)
+            if fr.status:
+                raise_frame_error(fr.status)
+        else:
+            lr, dof, br = self._solve([body_global_translation, left_hand_global_translation,
+                                       right_hand_global_translation], batched=False, want_body_rot=True)
         self._record(lr, dof)
         return lr, dof, br
 

@@ -20,6 +20,7 @@ pattern instead, which an input carrying that pattern through a NaN path could m
 from __future__ import annotations
 
 import atexit
+import ctypes
 import time
 import weakref
 from typing import Sequence
@@ -33,6 +34,11 @@ from .runtime import Solver, require_gpu, stream_handle
 from .runtime import IN_TAILS as _IN_TAILS
 
 _SERVER_ENDED = 6   # rtg.h RTG_SERVER_ENDED
+
+try:   # the frame's host round trip with tensor arguments and results (rtg/_frame_post.cpp, rtg/build_ext.py)
+    from . import _frame_post as _fast_post
+except ImportError:   # not built: the ctypes path below does the same call
+    _fast_post = None
 
 
 _F32 = torch.float32
@@ -187,6 +193,8 @@ class FrameServer:
         self._rows = _OutRows([(31, 4), (30,), (59, 4) if want_body_rot else None])
         self._post = lib().rtg_frame_server_post
         self._timeout_us = int(self.timeout_s * 1e6)
+        self._fast = _fast_post.post if _fast_post is not None else None
+        self._post_addr = ctypes.cast(self._post, ctypes.c_void_p).value
         self._ctl_ptr, self._in_ptr = self.h_ctl.data_ptr(), self.h_in.data_ptr()
         self._lr_ptr, self._dof_ptr = out, out + 4 * 124
         self._br_ptr = out + 4 * 154 if want_body_rot else None
@@ -205,6 +213,22 @@ class FrameServer:
         Python's share is kept to attribute reads and integer arithmetic (tools/extra_bench.py latency)."""
         if len(inputs) != 3:
             raise ValueError("expected 3 inputs")
+        b, lh, rh = inputs
+        if self._fast is not None and type(b) is torch.Tensor and type(lh) is torch.Tensor and type(rh) is torch.Tensor:
+            if not self._running or (self._ctl[2] and self.stream.query()):
+                self._launch()
+            self.seq = self.seq + 1 if self.seq + 1 < int(self._quit) else 1
+            args = (self._post_addr, self._ctl_ptr, self.seq, self._in_ptr, b, lh, rh, self._dof_ptr, self._lr_ptr,
+                    self._br_ptr or 0, self._timeout_us)
+            rc, code, lr, dof, br = self._fast(*args)
+            while rc == _SERVER_ENDED:   # idled out before it took the frame: relaunch (the frame is still posted)
+                self.stream.synchronize()
+                self._launch()
+                rc, code, lr, dof, br = self._fast(*args)
+            if rc != _fast_post.NOT_HOST_F32:   # else: inputs to convert, the ctypes path below
+                check(rc)
+                self.status = code
+                return lr, dof, br
         sz, tl = self._sizes, self.tails
         p0, x0 = _host_f32_ptr(inputs[0], sz[0], tl[0])
         p1, x1 = _host_f32_ptr(inputs[1], sz[1], tl[1])

@@ -334,3 +334,18 @@ def test_frame_server_post_protocol_on_the_host():
     assert lib.rtg_frame_server_post(None, 1, *([None] * 10), 10) == 1
     assert lib.rtg_frame_server_post(vp(ctl.ctypes.data), _lib.SERVER_QUIT, *([vp(inb.ctypes.data)] * 5),
                                      *([None] * 5), 10) == 1
+
+
+def test_frame_post_extension_refuses_what_it_cannot_post():
+    """rtg/_frame_post (the server's per-frame round trip with tensor arguments) checks its inputs before it posts:
+    a non-float32, non-contiguous or wrongly sized frame returns NOT_HOST_F32 without calling the C function (the
+    null function address here would crash if it were called), so FrameServer converts and takes the ctypes path."""
+    import torch
+    fp = pytest.importorskip("rtg._frame_post")
+    good = (torch.zeros(21, 3), torch.zeros(20, 3), torch.zeros(20, 3))
+    bad = [(good[0].double(), good[1], good[2]), (good[0], torch.zeros(3, 20).t(), good[2]),
+           (good[0], good[1], torch.zeros(21, 3))]
+    for b, l, r in bad:
+        rc, code, *_ = fp.post(0, 0, 1, 0, b, l, r, 0, 0, 0, 1000)
+        assert rc == fp.NOT_HOST_F32 and code == 0
+    assert fp.SERVER_ENDED == 6

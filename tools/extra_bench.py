@@ -81,7 +81,9 @@ def latency():
     from rtg.realtime import FrameServer
     fg = FrameGraph(S, want_body_rot=False)
     fsrv = FrameServer(S, want_body_rot=False)
+    fsrv_br = FrameServer(S, want_body_rot=True)
     for name, fn in (("dropin_retarget_per_frame", lambda: hu.retarget(fb, fl, fr)),
+                     ("frame_server_dof_local_rot_body_rot", lambda: fsrv_br(fb, fl, fr)),
                      ("dropin_batch_of_one_no_graph",
                       lambda: hu.retarget_batch(fb[None], fl[None], fr[None], want_body_rot=True)),
                      ("frame_graph_dof_local_rot", lambda: fg(fb, fl, fr)),
@@ -97,6 +99,8 @@ def latency():
     a, b = fg(fb, fl, fr), fsrv(fb, fl, fr)
     out["frame_server_bits_equal_frame_graph"] = bool(torch.equal(a[0], b[0]) and torch.equal(a[1], b[1]))
     fsrv.close()
+    fsrv_br.close()
+    hu.close()
     return out
 
 
