@@ -383,6 +383,7 @@ def golden_errors(dof, gold_dof):
 class DeviceBackend:
     """The product path of one rank: librtg_hip.so on this rank's GPU (RCCL for the collectives)."""
     DIST_BACKEND = "nccl"
+    DEVICE = True
 
     @staticmethod
     def bind_device(local):
@@ -614,10 +615,10 @@ def main():
         sys.exit(2)
     backend_cls = load_backend()
     world, rank, local = dist_setup(backend_cls)
-    if backend_cls is not DeviceBackend:
+    if not getattr(backend_cls, "DEVICE", False):   # (a subclass may come from `import bench`, not __main__)
         return host_main(args, backend_cls(local), world, rank)
     B = args.batch
-    backend = DeviceBackend(local, args.layout)
+    backend = backend_cls(local, args.layout)
     bytes_per_set = B * (63 + 60 + 60 + 30) * 4
     ring = args.ring or max(2, int(np.ceil(2 * 256 * 2**20 / bytes_per_set)))
     res = rank_flow(world, rank, backend, B, args.steps, args.warmup, ring)

@@ -146,6 +146,8 @@ def gather_shards(shard: torch.Tensor, counts: Sequence[int], dst: int = 0) -> O
     if len(counts) != world or shard.shape[0] != counts[rank]:
         raise ValueError("counts must list every rank's shard length")
     m = max(counts) if counts else 0
+    if shard.is_cuda and dist.get_backend() == "gloo":   # gloo gathers host tensors only
+        shard = shard.cpu()
     padded = shard
     if shard.shape[0] < m:
         padded = torch.cat([shard, shard.new_zeros((m - shard.shape[0],) + tuple(shard.shape[1:]))])

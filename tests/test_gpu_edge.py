@@ -253,3 +253,26 @@ def test_handover_timeout_is_reported_not_silent(gpu):
                        text=True, timeout=120)
     assert r.returncode == 0 and "REPORTED" in r.stdout and "hand-over timed out" in r.stdout, r.stdout + r.stderr
     assert "CLEARED" in r.stdout
+
+
+@pytest.mark.gpu
+def test_bench_device_path_two_ranks_on_one_gpu():
+    """bench.py's N>1 DEVICE flow rehearsed on the one-GPU box: two rank processes on cuda:0 (gloo collectives,
+    tests/bench_shared_gpu_backend.py), each with its two streams, clock settle and single-launch kernel time.  Rank 0
+    prints the line with n_gpus 2, both ranks pass their golden check, and the gathered DOFs hold both shards."""
+    import json
+    import subprocess
+    import sys
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_PORT")}
+    env.update(RTG_BENCH_BACKEND="bench_shared_gpu_backend:SharedGpuGlooBackend", RTG_BENCH_SETTLE_MS="20",
+               PYTHONPATH=os.pathsep.join([os.path.dirname(os.path.abspath(__file__)), repo, env.get("PYTHONPATH", "")]))
+    r = subprocess.run([sys.executable, os.path.join(repo, "bench.py"), "--gpus", "2", "--steps", "6", "--warmup", "2",
+                        "--batch", "65536", "--no-cpu-baseline"], env=env, capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0, r.stderr[-3000:]
+    line = json.loads([x for x in r.stdout.splitlines() if x.startswith("{")][-1])
+    assert line["n_gpus"] == 2 and line["config"]["parallelism"] == "dp2"
+    assert line["value"] > 0 and line["roofline"]["kernel_ms"] > 0 and line["settle"]["blocks_of_K_steps"] >= 1
+    assert [g["rank"] for g in line["golden_per_rank"]] == [0, 1]
+    assert all(g["max_abs_err"] < 1e-4 for g in line["golden_per_rank"])
+    assert "gather_ms" in line
