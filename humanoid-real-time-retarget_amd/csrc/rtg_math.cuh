@@ -600,7 +600,7 @@ RTG_DEV Q axis_half_quat(int axis, float a)
 // routine follows the published LAPACK algorithm; the FMA placement inside MKL's BLAS kernels was measured stage
 // by stage against MKL's own entry points (tools/mkl_sgesdd_probe.py) and matches bit for bit.  The
 // oracle (oracle/rtg_oracle.c, la_gesdd3) restates the same routines independently.  All divisions / square
-// roots are IEEE-exact (fdiv = one rcp64 + mulr, cr_sqrt).  Matrices are column-major: a[r + 3 c].
+// roots are IEEE-exact (fdiv = the compiler's IEEE f32 division; shared denominators rcp64 + mulr_k; cr_sqrt).  Matrices are column-major: a[r + 3 c].
 RTG_DEV float fdiv(float a, float b)
 {
     return a / b;   // the compiler's IEEE f32 division sequence (measured 6 % faster here than rcp64 + mulr)

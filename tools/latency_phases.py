@@ -1,7 +1,7 @@
 """Where the per-frame (teleop) latency goes.
 
   phases    -- needs a build with -DRTG_EXP_TIMESTAMPS=1 (RTG_LIB=...): block 0's lane 0 of each wave of
-               the latency kernel (k_fbp_latency5, or k_fbp_latency in an RTG_LATENCY_WAVES=3 build) records the
+               the five-wave latency kernel (k_fbp_latency5; B = 1 runs k_fbp_frame1, which records no stages, so use B >= 2) records the
                100 MHz wall clock at its stage boundaries; prints the median stage times (us) per wave at B=1 and
                B=4096
   zerocopy  -- the B=1 call with the inputs and outputs in pinned host memory that the kernel reads / writes
@@ -43,7 +43,7 @@ def inputs(B, pinned=False, device=True):
     return [torch.from_numpy(a).pin_memory() if pinned else torch.from_numpy(a) for a in hs]
 
 
-# k_fbp_latency5 timestamp slots per wave (RTG_LATENCY_WAVES=5): 0 start, 1 own stage done, 2 next stage
+# k_fbp_latency5 timestamp slots per wave: 0 start, 1 own stage done, 2 next stage
 # (w0: fixed links; w1/2: gripper; w3/4: R10 received), 3 (w1/2: arm chain received; w3/4: arm done), 4 (w1/2:
 # Euler done; w3/4: arm exp-maps done), 5 pre-barrier, 6 post-barrier, 7 stored; 8/9 A formed / SVD done (fits)
 LAT5 = {0: {1: "torso_fit", 2: "fixed_links"},
