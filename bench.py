@@ -644,6 +644,9 @@ def main():
                          "kernel": f"k_solve_sides<FULL_BODY_POS, {args.layout.upper()}>", "kernel_ms": kern_ms,
                          "kernel_ms_source": "event pair around 10 single-stream launches right after the timed region",
                          "gpu_ms_per_step": res["gpu_step_ms"],
+                         # the same bytes over the timed region's per-step GPU time (steps overlap on two streams)
+                         "achieved_per_step": BYTES_PER_FRAME * B / (res["gpu_step_ms"] * 1e-3) / 1e9,
+                         "frac_per_step": BYTES_PER_FRAME * B / (res["gpu_step_ms"] * 1e-3) / 1e9 / HBM_PEAK_GBS,
                          "bytes_per_frame": BYTES_PER_FRAME,
                          "traffic_unit": "bytes/launch (rocprofv3 FETCH_SIZE x calibration + WRITE_SIZE)",
                          "traffic_detail": {k: rec[k] for k in ("fetch_size_raw", "fetch_correction", "fetch_bytes",
