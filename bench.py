@@ -404,8 +404,8 @@ class DeviceBackend:
         self.stream = torch.cuda.current_stream()
         # RTG_BENCH_STREAMS=2 (default): step i runs on stream i % 2, so the next batch's tiles take the CUs that the
         # previous batch's last tiles leave idle (tools/overlap_probe.py); every step is still one full batched solve
-        self.nstreams = int(os.environ.get("RTG_BENCH_STREAMS", "2"))
-        self.side = torch.cuda.Stream(self.dev) if self.nstreams > 1 else None
+        self.nstreams = max(1, int(os.environ.get("RTG_BENCH_STREAMS", "2")))
+        self.streams = [self.stream] + [torch.cuda.Stream(self.dev) for _ in range(self.nstreams - 1)]
 
     def golden_check(self, solver):
         """This rank's own solver on the reference's golden frames (AoS rows, as the teleop callers hand them)."""
@@ -488,14 +488,14 @@ class DeviceBackend:
             self.graph.replay()
             return
         torch = self.torch
-        if self.side is not None:
-            self.side.wait_stream(self.stream)   # nothing on the side stream starts before the timed region does
+        for s in self.streams[1:]:
+            s.wait_stream(self.stream)   # nothing on a side stream starts before the timed region does
         for i in range(steps):
             b, l, r_, d = sets[i % len(sets)]
-            with torch.cuda.stream(self.stream if (self.side is None or i % 2 == 0) else self.side):
+            with torch.cuda.stream(self.streams[i % self.nstreams]):
                 self.solve(solver, b, l, r_, d)
-        if self.side is not None:
-            self.stream.wait_stream(self.side)   # the stop event covers both streams' steps
+        for s in self.streams[1:]:
+            self.stream.wait_stream(s)   # the stop event covers every stream's steps
 
     def launch_ms(self, solver, sets, n=10):
         """One launch's own duration: an event pair around n back-to-back launches on ONE stream, right after the
