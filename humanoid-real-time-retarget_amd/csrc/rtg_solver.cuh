@@ -77,12 +77,12 @@ struct Emit {
     }
 };
 
-RTG_DEV void emit_fixed_links(const Emit &E)
+RTG_DEV void emit_fixed_links(const Emit &E, bool write_lr = true)
 {
 #pragma unroll
     for (int k = 0; k < 11; ++k) E.row[k] = 0.0f;
     E.row[29] = 0.0f;
-    if (E.lr) {
+    if (E.lr && write_lr) {
 #pragma unroll
         for (int j = 0; j < 12; ++j) st4(E.lr + 4 * j, qident());
         st4(E.lr + 4 * 19, qident());
@@ -301,12 +301,17 @@ RTG_DEV void fbp_gripper(const SolverConsts &C, float a, float *row_d0)
 }
 // body_global_rotation rows (:116, :172-173) of one side: the left side also writes row 10 and the identities
 template <int SIDE>
-RTG_DEV void fbp_body_rows(float *__restrict__ brow, Q R10, Q W)
+RTG_DEV void fbp_body_rows(float *__restrict__ brow, Q R10, Q W, bool const_rows = true)
 {
     st4(brow + 4 * (SIDE ? 39 : 14), W);
-    if (!SIDE)
-        for (int j = 0; j < 59; ++j)
-            if (j != 14 && j != 39) st4(brow + 4 * j, j == 10 ? R10 : qident());
+    if (!SIDE) {
+        if (const_rows) {
+            for (int j = 0; j < 59; ++j)
+                if (j != 14 && j != 39) st4(brow + 4 * j, j == 10 ? R10 : qident());
+        } else {
+            st4(brow + 4 * 10, R10);
+        }
+    }
 }
 // the Euler split of the wrist (:128-136), the gripper (:142-158 / :165-175) and the body_rot rows; true where
 // scipy refuses the wrist's local quaternion
@@ -864,9 +869,12 @@ RTG_DEV void finalize_lanes(const Emit &E, int s0, int n)
 
 // The frame whose rows (body 63 | left hand 60 | right hand 60 floats) are in `rows` (LDS); dof / local_rot /
 // body_rot point at the frame's output rows
+// const_rows false (the frame server, once its output buffers hold them): the rows that are the same for every
+// frame -- the 17 fixed links of local_rot and the 56 identity rows of body_rot -- are not rewritten; they are still
+// in the server's own pinned output rows from an earlier frame.  Returns the frame's status bits (block-uniform).
 template <bool PRECISE>
-RTG_DEV void fbp_frame1_tile(const SolverConsts &C, const float *rows, float *__restrict__ dof,
-                             float *__restrict__ local_rot, float *__restrict__ body_rot)
+RTG_DEV uint32_t fbp_frame1_tile(const SolverConsts &C, const float *rows, float *__restrict__ dof,
+                                 float *__restrict__ local_rot, float *__restrict__ body_rot, bool const_rows = true)
 {
     __shared__ float sdof[kDofStride];
     __shared__ float4 sfit, schain[2];
@@ -888,7 +896,7 @@ RTG_DEV void fbp_frame1_tile(const SolverConsts &C, const float *rows, float *__
             st = nan ? kStTorsoSvd : 0u;
         }
         lds_signal(&sflag[0]);
-        if (w0) emit_fixed_links(E);
+        if (w0) emit_fixed_links(E, const_rows);
     } else if (w >= 3) {
         const int side = w - 3;
         const ArmPts ap = side ? load_arm<1>(b) : load_arm<0>(b);
@@ -921,7 +929,7 @@ RTG_DEV void fbp_frame1_tile(const SolverConsts &C, const float *rows, float *__
             fbp_gripper<PRECISE>(C, a, E.row + (side ? 27 : 18));
             if (body_rot) {
                 if (side) fbp_body_rows<1>(body_rot, R10, W);
-                else fbp_body_rows<0>(body_rot, R10, W);
+                else fbp_body_rows<0>(body_rot, R10, W, const_rows);
             }
         }
         const Q loc = qmul_norm(qconj(qmul_norm(R10, chain)), W);
@@ -937,6 +945,7 @@ RTG_DEV void fbp_frame1_tile(const SolverConsts &C, const float *rows, float *__
         __syncthreads();
     }
     if (threadIdx.x < 30) dof[threadIdx.x] = sdof[threadIdx.x];
+    return bits;
 }
 // The frame's 183 input floats cross into LDS once, all loads in flight together (one round trip even from host
 // memory).  At B = 1 the SoA planes (P, C, 1) are the AoS rows, so one kernel serves both layouts.
@@ -972,6 +981,7 @@ __global__ __launch_bounds__(320) void k_frame_server(SolverConsts C, const floa
     __shared__ uint32_t scmd;
     __shared__ float sframe[184];
     uint32_t last = 0;
+    bool const_ok = false;   // the output rows that never change are in place (written by an unpoisoned frame)
     if (threadIdx.x == 0) last = __hip_atomic_load(ctl + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     for (int frame = 0; frame < (1 << 30); ++frame) {
         if (threadIdx.x == 0) {
@@ -996,7 +1006,8 @@ __global__ __launch_bounds__(320) void k_frame_server(SolverConsts C, const floa
         // loads (tips after the wrist fit, arm points after R10) then read LDS instead of host memory
         if (threadIdx.x < 183) sframe[threadIdx.x] = in[threadIdx.x];
         __syncthreads();
-        fbp_frame1_tile<PRECISE>(C, sframe, dof, local_rot, body_rot);
+        const uint32_t bits = fbp_frame1_tile<PRECISE>(C, sframe, dof, local_rot, body_rot, !const_ok);
+        const_ok = bits == 0u;   // a poisoned frame overwrote every row with NaN: the next one rewrites them
         __syncthreads();   // every lane of every wave has issued its output stores (a convergent point) ...
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");   // ... so this wave's release covers all of them
         __syncthreads();

@@ -126,7 +126,7 @@ def test_dropin_retarget_raises_like_the_reference(poses, server):
     import oracle as orc
     from retarget.retarget_solver import VtrdynFullBodyPosRetargeter
     d = golden("full_body_pos_edge")
-    odof, _, _ = _oracle(0, d, True)
+    odof, olr, obr = _oracle(0, d, True)
     s = VtrdynFullBodyPosRetargeter(poses["vtrdyn_full"], poses["hu_v5"], precise_gripper=True, frame_server=server,
                                     idle_ms=50)
     try:
@@ -139,9 +139,11 @@ def test_dropin_retarget_raises_like_the_reference(poses, server):
                 with pytest.raises(exc, match=msg):
                     s.retarget(*args)
                 assert s.motion_length == before
-            else:
-                _, dof, _ = s.retarget(*args)
+            else:   # every output, including the rows the server writes only once (a raising frame before
+                lr, dof, br = s.retarget(*args)   # overwrote them with NaN: they must be back)
                 np.testing.assert_array_equal(_bits(dof), _bits(odof[i]))
+                np.testing.assert_array_equal(_bits(lr), _bits(olr[i]))
+                np.testing.assert_array_equal(_bits(br), _bits(obr[i]))
                 assert s.motion_length == before + 1
         assert s.motion_length == int(d["precise_recorded"])   # the reference recorded exactly these frames
         assert orc.frame_status(odof).tolist() == status.tolist()
