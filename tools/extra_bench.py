@@ -166,6 +166,33 @@ def solvers():
     return res
 
 
+def aux():
+    """The §8(f) kernels around the solver: VTRDyn ingest (23/20/20-point broadcast frames -> solver rows and the
+    has-data flag, both layouts) and the SkeletonMotion velocity stencils (gradient + gaussian smoothing), at
+    262144 frames.  Algorithmic bytes: ingest 189 floats in + 183 floats + 1 flag out per frame; velocities the
+    input and output rows once each (the smoothing's intermediate pass is the kernels' own traffic)."""
+    from rtg import ingest
+    B = 262144
+    res = {}
+    g = torch.Generator().manual_seed(5)
+    b23 = torch.randn(B, 23, 3, generator=g).cuda()
+    l20 = torch.randn(B, 20, 3, generator=g).cuda()
+    r20 = torch.randn(B, 20, 3, generator=g).cuda()
+    nbytes = B * ((23 + 20 + 20) * 3 * 4 + (21 + 20 + 20) * 3 * 4 + 1)
+    for layout in ("aos", "soa"):
+        ms = time_events(lambda: ingest.reindex_frames(b23, l20, r20, layout=layout))
+        res[f"ingest_{layout}_262144"] = {"ms": ms, "frames_per_s": B / (ms * 1e-3),
+                                           "GBs_algorithmic": nbytes / (ms * 1e-3) / 1e9}
+    nseq, L, J = 64, 4096, 31   # 64 motions of 4096 frames, Hu links
+    p = torch.randn(nseq, L, J, 3, generator=g).cuda()
+    q = torch.nn.functional.normalize(torch.randn(nseq, L, J, 4, generator=g), dim=-1).cuda()
+    for name, fn, nb in (("linear_velocity", lambda: ops.motion_velocity(p, 1.0 / 30), nseq * L * J * 24),
+                         ("angular_velocity", lambda: ops.motion_angular_velocity(q, 1.0 / 30), nseq * L * J * 28)):
+        ms = time_events(fn)
+        res[f"{name}_64x4096"] = {"ms": ms, "frames_per_s": nseq * L / (ms * 1e-3), "GBs_algorithmic": nb / (ms * 1e-3) / 1e9}
+    return res
+
+
 def sweep():
     """FULL_BODY_POS kernel time across batch sizes (RTG_LATENCY_MAX_B picks the latency kernel below it): run with
     the default library and with an RTG_LATENCY_MAX_B=0 build (RTG_LIB=...) to find the crossover."""
