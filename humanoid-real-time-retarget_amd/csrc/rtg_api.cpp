@@ -511,7 +511,7 @@ int rtg_retarget_f32(rtg_solver_t s, const float *in0, const float *in1, const f
         return fail(RTG_ERR_INVALID_ARGUMENT, "rtg_retarget_f32: body_rot is only produced by FULL_BODY_POS");
     RTG_TRY(launch_retarget(s->kind, s->precise, s->consts, in0, in1, in2, in3, B, layout, dof, local_rot, body_rot,
                             as_stream(stream)),
-            "k_retarget");
+            "rtg_retarget_f32 launch");
     return RTG_OK;
 }
 
