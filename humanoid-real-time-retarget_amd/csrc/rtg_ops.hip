@@ -160,32 +160,60 @@ RTG_DEV int64_t lay_idx(bool soa, int64_t f, int j, int c, int P, int C, int64_t
     return soa ? ((int64_t)(j * C + c)) * B + f : f * (P * C) + C * j + c;
 }
 
+// VTRDyn ingest (sim_full_body_teleop.py:92,109-112: body 23 -> 21 points, hands reordered, the "frame carries data"
+// flag): one 256-thread block per 64-frame tile.  Each input's tile rows are ONE contiguous span (64 x 69 / 60 / 60
+// floats), staged into LDS by coalesced loads; the outputs leave coalesced too -- AoS rows (the tile's 64 x 63 / 60
+// floats are again one span) or SoA planes (64 consecutive frames per plane).  Round 3 moved each frame on one
+// thread: 12-byte pieces 276 / 240 bytes apart per lane, 64 lines per wave instruction (1.3 TB/s).
+constexpr int kIngTile = 64;
+template <int R, int O>
+RTG_DEV void ingest_rows_out(const float *srow, float *__restrict__ out, const int8_t *map, int64_t f0, int nfr,
+                             int64_t B, bool soa)
+{
+    if (!soa) {
+        const int n = nfr * O;
+        float *dst = out + f0 * O;
+        for (int e = threadIdx.x; e < n; e += 256) {
+            const int fr = e / O, k = e - fr * O, j = k / 3, c = k - 3 * j;
+            dst[e] = srow[fr * R + 3 * map[j] + c];
+        }
+    } else {
+        for (int e = threadIdx.x; e < O * kIngTile; e += 256) {
+            const int plane = e / kIngTile, fr = e - plane * kIngTile, j = plane / 3, c = plane - 3 * j;
+            if (fr < nfr) out[(int64_t)plane * B + f0 + fr] = srow[fr * R + 3 * map[j] + c];
+        }
+    }
+}
 __global__ __launch_bounds__(256) void k_ingest_vtrdyn(const float *__restrict__ bp, const float *__restrict__ lhp,
                                                        const float *__restrict__ rhp, int64_t B,
                                                        float *__restrict__ body, float *__restrict__ lh,
                                                        float *__restrict__ rh, uint8_t *__restrict__ valid, bool soa)
 {
-    const int64_t f = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (f >= B) return;
-    const float *b = bp + f * 69;
-    bool close = true;   // np.allclose(body_pos, 0): |x| <= 1e-8 everywhere (a NaN is never close)
-    for (int i = 0; i < 69; ++i) close = close && (fabsf(b[i]) <= 1e-8f);
-    valid[f] = close ? 0 : 1;
-    if (!soa) {
-        for (int j = 0; j < 21; ++j) st3(body + f * 63 + 3 * j, ld3(b + 3 * c_body23_to_21[j]));
-        for (int j = 0; j < 20; ++j) {
-            st3(lh + f * 60 + 3 * j, ld3(lhp + f * 60 + 3 * c_hand_order[j]));
-            st3(rh + f * 60 + 3 * j, ld3(rhp + f * 60 + 3 * c_hand_order[j]));
-        }
-        return;
+    __shared__ float srow[kIngTile * 69];
+    __shared__ int sdata[kIngTile];   // the frame carries data: not np.allclose(body_pos, 0)
+    const int64_t f0 = (int64_t)blockIdx.x * kIngTile;
+    const int nfr = (int)((B - f0) < kIngTile ? (B - f0) : kIngTile);
+    const int tid = threadIdx.x;
+    if (tid < kIngTile) sdata[tid] = 0;
+    {   // body (23 points): the flag over all 69 values (|x| <= 1e-8 everywhere; a NaN is never close), then 21 points
+        const int n = nfr * 69;
+        const float *src = bp + f0 * 69;
+        for (int e = tid; e < n; e += 256) srow[e] = src[e];
+        __syncthreads();
+        for (int e = tid; e < n; e += 256)
+            if (!(fabsf(srow[e]) <= 1e-8f)) sdata[e / 69] = 1;   // every writer stores 1
+        ingest_rows_out<69, 63>(srow, body, c_body23_to_21, f0, nfr, B, soa);
+        __syncthreads();
+        if (tid < nfr) valid[f0 + tid] = sdata[tid] ? 1 : 0;
     }
-    for (int j = 0; j < 21; ++j)   // SoA planes: each store instruction writes 256 contiguous bytes per wave
-        for (int c = 0; c < 3; ++c) body[lay_idx(true, f, j, c, 21, 3, B)] = b[3 * c_body23_to_21[j] + c];
-    for (int j = 0; j < 20; ++j)
-        for (int c = 0; c < 3; ++c) {
-            lh[lay_idx(true, f, j, c, 20, 3, B)] = lhp[f * 60 + 3 * c_hand_order[j] + c];
-            rh[lay_idx(true, f, j, c, 20, 3, B)] = rhp[f * 60 + 3 * c_hand_order[j] + c];
-        }
+    for (int h = 0; h < 2; ++h) {   // hands (20 points each), reordered
+        const int n = nfr * 60;
+        const float *src = (h ? rhp : lhp) + f0 * 60;
+        for (int e = tid; e < n; e += 256) srow[e] = src[e];
+        __syncthreads();
+        ingest_rows_out<60, 60>(srow, h ? rh : lh, c_hand_order, f0, nfr, B, soa);
+        __syncthreads();
+    }
 }
 
 int32_t fk_schedule(const int32_t *parents, int32_t J, int32_t *sched)
@@ -365,33 +393,57 @@ __global__ __launch_bounds__(256) void k_quat_in_xyz_axis(const float *__restric
 }
 
 // ----------------------------------------------------------------------------
-// motion velocities: thread per (sequence, frame, channel), channel fastest
-// (coalesced over the J*C channels of a frame).
+// motion velocities (skeleton3d.py:1126-1146).  The data are rows of C channels (one row per (sequence, frame),
+// rows = nseq * L, the frame fastest within a sequence).  A 256-thread block covers 256 / Cp consecutive rows, Cp =
+// C rounded up to a power of two, so a thread's (row, channel) is a shift and a mask, and its frame t = row % L is
+// one 32-bit remainder per thread (round 3 divided the flat 64-bit index by C and L per thread: 64-bit division
+// dominated the kernels).  Rows wider than 256 channels take one row per block and gridDim.y 256-channel slices.
+// Launches cover at most 2^30 rows each (row0 offsets the chunks).
 // ----------------------------------------------------------------------------
-// np.gradient along frames (edge_order 1, unit spacing) then / dt, all float32
-__global__ __launch_bounds__(256) void k_gradient_dt(const float *__restrict__ p, int64_t nseq, int64_t L, int64_t S,
-                                                     float dt, float *__restrict__ v)
+struct RowTile {
+    int64_t row0;       // first row of this launch
+    uint32_t rows;      // rows in this launch
+    uint32_t L;         // frames per sequence
+    int32_t C, cp_log2; // channels per row, log2(Cp)
+};
+RTG_DEV bool row_tile(const RowTile &rt, int64_t &row, int &ch, uint32_t &t)
 {
-    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= nseq * L * S) return;
-    const int64_t s = i % S, t = (i / S) % L, base = i - s - t * S;
+    const uint32_t r = (blockIdx.x << (8 - rt.cp_log2)) + (threadIdx.x >> rt.cp_log2);
+    ch = (int)(threadIdx.x & ((1u << rt.cp_log2) - 1u)) + (int)(blockIdx.y << 8);   // y: 256-channel slices
+    if (r >= rt.rows || ch >= rt.C) return false;
+    row = rt.row0 + r;
+    t = (uint32_t)(row % (int64_t)rt.L);
+    return true;
+}
+// np.gradient along frames (edge_order 1, unit spacing) then / dt, all float32
+__global__ __launch_bounds__(256) void k_gradient_dt(const float *__restrict__ p, RowTile rt, float dt,
+                                                     float *__restrict__ v)
+{
+    int64_t row;
+    int ch;
+    uint32_t t;
+    if (!row_tile(rt, row, ch, t)) return;
+    const int64_t S = rt.C, i = row * S + ch;
+    const uint32_t L = rt.L;
     float g;
     if (L == 1) g = 0.0f;   // numpy raises for < 2 frames; rtg_* rejects L < 2 before launch
-    else if (t == 0) g = (p[base + S + s] - p[base + s]) / 1.0f;
-    else if (t == L - 1) g = (p[base + t * S + s] - p[base + (t - 1) * S + s]) / 1.0f;
-    else g = (p[base + (t + 1) * S + s] - p[base + (t - 1) * S + s]) / 2.0f;
+    else if (t == 0) g = (p[i + S] - p[i]) / 1.0f;
+    else if (t == L - 1) g = (p[i] - p[i - S]) / 1.0f;
+    else g = (p[i + S] - p[i - S]) / 2.0f;
     v[i] = g / dt;
 }
 
 // quat_mul_norm(r[t+1], quat_inverse(r[t])) -> quat_angle_axis -> axis * angle / dt (last frame: identity -> 0)
-__global__ __launch_bounds__(256) void k_angular_raw(const float *__restrict__ r, int64_t nseq, int64_t L, int64_t J,
-                                                     float dt, float *__restrict__ v)
+__global__ __launch_bounds__(256) void k_angular_raw(const float *__restrict__ r, RowTile rt, float dt,
+                                                     float *__restrict__ v)
 {
-    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= nseq * L * J) return;
-    const int64_t t = (i / J) % L;
+    int64_t row;
+    int ch;
+    uint32_t t;
+    if (!row_tile(rt, row, ch, t)) return;
+    const int64_t J = rt.C, i = row * J + ch;
     Q d = qident();
-    if (t < L - 1) d = qmul_norm(ld4(r + 4 * (i + J)), qconj(ld4(r + 4 * i)));
+    if (t < rt.L - 1) d = qmul_norm(ld4(r + 4 * (i + J)), qconj(ld4(r + 4 * i)));
     const Q aa = qangle_axis_abs(d);
     v[3 * i + 0] = (aa.y * aa.x) / dt;
     v[3 * i + 1] = (aa.z * aa.x) / dt;
@@ -400,39 +452,260 @@ __global__ __launch_bounds__(256) void k_angular_raw(const float *__restrict__ r
 
 // scipy.ndimage.gaussian_filter1d(mode='nearest') along frames: symmetric correlate1d,
 // float64 accumulation from the outermost tap pair inwards, rounded to float32 once
-__global__ __launch_bounds__(256) void k_gauss_nearest(const float *__restrict__ v, int64_t nseq, int64_t L, int64_t S,
+__global__ __launch_bounds__(256) void k_gauss_nearest(const float *__restrict__ v, RowTile rt, GaussTaps taps,
+                                                       float *__restrict__ out)
+{
+    int64_t row;
+    int ch;
+    uint32_t t;
+    if (!row_tile(rt, row, ch, t)) return;
+    const int64_t S = rt.C, i = row * S + ch, base = i - (int64_t)t * S;
+    const int R = taps.radius;
+    const int64_t L = rt.L;
+    auto at = [&](int64_t tt) { tt = tt < 0 ? 0 : (tt > L - 1 ? L - 1 : tt); return (double)v[base + tt * S]; };
+    double acc = at(t) * taps.w[R];
+    for (int jj = -R; jj < 0; ++jj) acc += (at((int64_t)t + jj) + at((int64_t)t - jj)) * taps.w[R + jj];
+    out[i] = (float)acc;
+}
+
+// Smoothed velocities in one pass (the path the reference takes: SkeletonMotion always smooths).  A block owns
+// frames [t0, t0 + T) of one sequence: it computes the raw velocity of frames [t0 - R, t0 + T + R) (clamped to
+// the sequence, the 'nearest' edge) straight from the input rows into LDS, then the smoothed rows from LDS, so the
+// intermediate never touches HBM and the input and output rows stream once each (the halo re-reads, 2R of T rows,
+// hit L2).  Rows of a sequence are contiguous, so both passes walk contiguous memory with consecutive lanes.
+// Arithmetic is the per-element kernels' above, operation for operation.
+struct VelTile {
+    int64_t seq0;       // first sequence of this launch
+    uint32_t L, T;      // frames per sequence, frames per block
+    uint32_t tiles;     // blocks per sequence
+    uint32_t nblocks;   // blocks in this launch
+    int32_t C, J;       // output channels per row; joints (angular) or input channels (linear)
+};
+// (row, channel) of flat element e = row * C + ch, advanced by 256 elements per step without a division
+struct RowWalk {
+    uint32_t rr, ch, dq, dr;
+    RTG_DEV RowWalk(uint32_t e0, uint32_t C) : rr(e0 / C), ch(e0 - (e0 / C) * C), dq(256u / C), dr(256u - (256u / C) * C) {}
+    RTG_DEV void next(uint32_t C)
+    {
+        rr += dq;
+        ch += dr;
+        if (ch >= C) { ch -= C; ++rr; }
+    }
+};
+
+// LDS row stride (floats) of one channel's raw values in a tile: T + 2R rows, odd so that lanes on consecutive
+// channels hit distinct banks
+__host__ __device__ inline uint32_t vel_lds_stride(uint32_t T, int R) { return (T + 2u * (uint32_t)R) | 1u; }
+
+// W consecutive smoothed outputs of one channel from its raw values x[0 .. W + 2R) in LDS (x[k]: frame t - R + k,
+// edges already replicated), the k_gauss_nearest sum operation for operation; each raw value is widened to double
+// once for the W outputs that read it
+template <int RC, int W>
+RTG_DEV void gauss_rows(const float *x, const GaussTaps &taps, double (&acc)[W])
+{
+    constexpr int N = W + 2 * RC;
+    double v[N];
+#pragma unroll
+    for (int k = 0; k < N; ++k) v[k] = (double)x[k];
+#pragma unroll
+    for (int r = 0; r < W; ++r) {
+        double a = v[r + RC] * taps.w[RC];
+#pragma unroll
+        for (int jj = -RC; jj < 0; ++jj) a += (v[r + RC + jj] + v[r + RC - jj]) * taps.w[RC + jj];
+        acc[r] = a;
+    }
+}
+RTG_DEV double gauss_row_any(const float *x, const GaussTaps &taps)
+{
+    const int R = taps.radius;
+    double a = (double)x[R] * taps.w[R];
+    for (int jj = -R; jj < 0; ++jj) a += ((double)x[R + jj] + (double)x[R - jj]) * taps.w[R + jj];
+    return a;
+}
+
+// Phase 1 computes the raw velocity of frames t0 - R .. t1 - 1 + R, each clamped into the sequence (the 'nearest'
+// edge: a frame outside repeats the edge frame's raw value), into LDS channel-major; phase 2 runs the filter over
+// LDS without a clamp.  RC >= 0: the filter radius as a constant (4 outputs per thread from a sliding window).
+template <bool ANGULAR, int RC>
+__global__ __launch_bounds__(256) void k_velocity_tile(const float *__restrict__ src, VelTile vt, float dt,
                                                        GaussTaps taps, float *__restrict__ out)
 {
-    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= nseq * L * S) return;
-    const int64_t s = i % S, t = (i / S) % L, base = i - s - t * S;
-    const int R = taps.radius;
-    auto at = [&](int64_t tt) { tt = tt < 0 ? 0 : (tt > L - 1 ? L - 1 : tt); return (double)v[base + tt * S + s]; };
-    double acc = at(t) * taps.w[R];
-    for (int jj = -R; jj < 0; ++jj) acc += (at(t + jj) + at(t - jj)) * taps.w[R + jj];
-    out[i] = (float)acc;
+    extern __shared__ float sg[];   // [C][stride] raw values of frames t0 - R ..
+    // XCD-aware order: the 8 XCDs take blocks round-robin, so give each XCD a contiguous run of tiles (their
+    // halo rows are then in that XCD's L2)
+    uint32_t b = blockIdx.x;
+    if ((vt.nblocks & 7u) == 0u) b = (b & 7u) * (vt.nblocks >> 3) + (b >> 3);
+    const uint32_t tile = b % vt.tiles;
+    const int64_t seq = vt.seq0 + b / vt.tiles;
+    const int R = RC >= 0 ? RC : taps.radius;
+    const int C = vt.C;
+    const int L = (int)vt.L;
+    const uint32_t NS = vel_lds_stride(vt.T, R);
+    const int t0 = (int)(tile * vt.T);
+    const int t1 = min(t0 + (int)vt.T, L);
+    const uint32_t nx = (uint32_t)(t1 - t0 + 2 * R);   // raw rows this tile reads
+    // every thread issues the loads of NB elements before it uses any (latency, not bandwidth, bounds a
+    // load-then-use loop at this occupancy)
+    if (!ANGULAR) {
+        constexpr int NB = 8;
+        const float *p = src + seq * L * C;
+        const uint32_t n = nx * (uint32_t)C;
+        RowWalk w(threadIdx.x, (uint32_t)C);
+        for (uint32_t e0 = threadIdx.x; e0 < n; e0 += 256 * NB) {
+            float hi[NB], lo[NB], hf[NB];
+            uint32_t at[NB];
+#pragma unroll
+            for (int k = 0; k < NB; ++k) {
+                const uint32_t e = e0 + 256u * k;
+                const int x = t0 - R + (int)w.rr;
+                const int t = x < 0 ? 0 : (x > L - 1 ? L - 1 : x);
+                const int64_t i = (int64_t)t * C + w.ch;
+                // np.gradient: (p[t+1] - p[t-1]) / 2 inside, one-sided differences / 1 at the ends (x / 2 and
+                // x * 0.5 are the same correctly rounded value)
+                const int64_t ih = t == L - 1 ? i : i + C, il = t == 0 ? i : i - C;
+                hf[k] = (t == 0 || t == L - 1) ? 1.0f : 0.5f;
+                at[k] = w.ch * NS + w.rr;
+                if (e < n) { hi[k] = p[ih]; lo[k] = p[il]; }
+                w.next((uint32_t)C);
+            }
+#pragma unroll
+            for (int k = 0; k < NB; ++k)
+                if (e0 + 256u * k < n) sg[at[k]] = ((hi[k] - lo[k]) * hf[k]) / dt;
+        }
+    } else {
+        constexpr int NB = 4;
+        const int J = vt.J;
+        const float *r = src + seq * L * J * 4;
+        const uint32_t n = nx * (uint32_t)J;
+        RowWalk w(threadIdx.x, (uint32_t)J);
+        for (uint32_t e0 = threadIdx.x; e0 < n; e0 += 256 * NB) {
+            Q qa[NB], qb[NB];
+            bool last[NB];
+            uint32_t at[NB];
+#pragma unroll
+            for (int k = 0; k < NB; ++k) {
+                const uint32_t e = e0 + 256u * k;
+                const int x = t0 - R + (int)w.rr;
+                const int t = x < 0 ? 0 : (x > L - 1 ? L - 1 : x);
+                const int64_t i = (int64_t)t * J + w.ch;
+                last[k] = t >= L - 1;
+                at[k] = 3u * w.ch * NS + w.rr;
+                if (e < n && !last[k]) { qa[k] = ld4(r + 4 * (i + J)); qb[k] = ld4(r + 4 * i); }
+                w.next((uint32_t)J);
+            }
+#pragma unroll
+            for (int k = 0; k < NB; ++k) {
+                if (e0 + 256u * k >= n) continue;
+                Q d = qident();
+                if (!last[k]) d = qmul_norm(qa[k], qconj(qb[k]));
+                const Q aa = qangle_axis_abs(d);
+                sg[at[k]] = (aa.y * aa.x) / dt;
+                sg[at[k] + NS] = (aa.z * aa.x) / dt;
+                sg[at[k] + 2 * NS] = (aa.w * aa.x) / dt;
+            }
+        }
+    }
+    __syncthreads();
+    float *o = out + (seq * L + t0) * C;
+    const uint32_t rows = (uint32_t)(t1 - t0);
+    if constexpr (RC >= 0) {
+        constexpr int W = 4;
+        const uint32_t n = ((rows + W - 1) / W) * (uint32_t)C;   // (row group, channel) items
+        RowWalk w(threadIdx.x, (uint32_t)C);
+        for (uint32_t e = threadIdx.x; e < n; e += 256) {
+            const uint32_t r0 = w.rr * W;
+            double acc[W];
+            gauss_rows<RC, W>(sg + w.ch * NS + r0, taps, acc);
+#pragma unroll
+            for (int r = 0; r < W; ++r)
+                if (r0 + r < rows) o[(int64_t)(r0 + r) * C + w.ch] = (float)acc[r];
+            w.next((uint32_t)C);
+        }
+    } else {
+        const uint32_t n = rows * (uint32_t)C;
+        RowWalk w(threadIdx.x, (uint32_t)C);
+        for (uint32_t e = threadIdx.x; e < n; e += 256) {
+            o[e] = (float)gauss_row_any(sg + w.ch * NS + w.rr, taps);
+            w.next((uint32_t)C);
+        }
+    }
+}
+
+// frames per block for the one-pass kernel: 64 while the raw rows fit 48 KB of LDS, fewer for wide rows; 0 when even
+// 16 frames do not fit (the two-pass kernels then run)
+static uint32_t vel_tile_frames(int64_t C, int R)
+{
+    for (uint32_t T = 64; T >= 16; T /= 2)
+        if ((int64_t)vel_lds_stride(T, R) * C * 4 <= 48 * 1024) return T;
+    return 0;
+}
+
+template <bool ANGULAR>
+static hipError_t launch_velocity_tile(const float *src, int64_t nseq, int64_t L, int64_t J, int64_t C, uint32_t T,
+                                       float dt, const GaussTaps &taps, float *out, hipStream_t s)
+{
+    const uint32_t tiles = (uint32_t)((L + T - 1) / T);
+    const int64_t per = ((int64_t)1 << 30) / tiles;   // sequences per launch
+    const size_t lds = (size_t)vel_lds_stride(T, taps.radius) * C * sizeof(float);
+    for (int64_t q0 = 0; q0 < nseq; q0 += per) {
+        const int64_t nq = nseq - q0 < per ? nseq - q0 : per;
+        const VelTile vt{q0, (uint32_t)L, T, tiles, (uint32_t)(nq * tiles), (int32_t)C, (int32_t)J};
+        if (taps.radius == 8)   // sigma 2, truncate 4: the reference's filter
+            hipLaunchKernelGGL((k_velocity_tile<ANGULAR, 8>), dim3(vt.nblocks), dim3(256), lds, s, src, vt, dt, taps, out);
+        else
+            hipLaunchKernelGGL((k_velocity_tile<ANGULAR, -1>), dim3(vt.nblocks), dim3(256), lds, s, src, vt, dt, taps,
+                               out);
+    }
+    return hipGetLastError();
+}
+
+// the launches of one kernel over all rows, in chunks of <= 2^30 rows
+template <typename F>
+static hipError_t over_rows(int64_t nrows, int64_t L, int64_t C, F launch)
+{
+    int cl = 0;
+    while (cl < 8 && (1 << cl) < C) ++cl;
+    const unsigned slices = (unsigned)((C + 255) / 256);
+    const int64_t chunk = (int64_t)1 << 30;
+    for (int64_t r0 = 0; r0 < nrows; r0 += chunk) {
+        const int64_t n = nrows - r0 < chunk ? nrows - r0 : chunk;
+        const RowTile rt{r0, (uint32_t)n, (uint32_t)L, (int32_t)C, cl};
+        const int64_t rpb = (int64_t)256 >> cl;
+        launch(rt, dim3((unsigned)((n + rpb - 1) / rpb), slices > 0 ? slices : 1u));
+    }
+    return hipGetLastError();
 }
 
 hipError_t launch_linear_velocity(const float *p, int64_t nseq, int64_t L, int64_t S, float dt, const GaussTaps *taps,
                                   float *tmp, float *out, hipStream_t s)
 {
-    const int64_t n = nseq * L * S;
-    const unsigned g = (unsigned)((n + 255) / 256);
-    hipLaunchKernelGGL(k_gradient_dt, dim3(g), dim3(256), 0, s, p, nseq, L, S, dt, taps ? tmp : out);
-    if (taps) hipLaunchKernelGGL(k_gauss_nearest, dim3(g), dim3(256), 0, s, tmp, nseq, L, S, *taps, out);
-    return hipGetLastError();
+    if (nseq == 0) return hipSuccess;
+    const uint32_t T = taps && L < (1 << 30) ? vel_tile_frames(S, taps->radius) : 0;
+    if (T) return launch_velocity_tile<false>(p, nseq, L, S, S, T, dt, *taps, out, s);
+    float *g = taps ? tmp : out;
+    hipError_t e = over_rows(nseq * L, L, S, [&](const RowTile &rt, dim3 grid) {
+        hipLaunchKernelGGL(k_gradient_dt, grid, dim3(256), 0, s, p, rt, dt, g);
+    });
+    if (e != hipSuccess || !taps) return e;
+    return over_rows(nseq * L, L, S, [&](const RowTile &rt, dim3 grid) {
+        hipLaunchKernelGGL(k_gauss_nearest, grid, dim3(256), 0, s, tmp, rt, *taps, out);
+    });
 }
 
 hipError_t launch_angular_velocity(const float *r, int64_t nseq, int64_t L, int64_t J, float dt,
                                    const GaussTaps *taps, float *tmp, float *out, hipStream_t s)
 {
-    const int64_t n = nseq * L * J;
-    hipLaunchKernelGGL(k_angular_raw, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, r, nseq, L, J, dt,
-                       taps ? tmp : out);
-    if (taps)
-        hipLaunchKernelGGL(k_gauss_nearest, dim3((unsigned)((3 * n + 255) / 256)), dim3(256), 0, s, tmp, nseq, L,
-                           3 * J, *taps, out);
-    return hipGetLastError();
+    if (nseq == 0) return hipSuccess;
+    const uint32_t T = taps && L < (1 << 30) ? vel_tile_frames(3 * J, taps->radius) : 0;
+    if (T) return launch_velocity_tile<true>(r, nseq, L, J, 3 * J, T, dt, *taps, out, s);
+    float *raw = taps ? tmp : out;
+    hipError_t e = over_rows(nseq * L, L, J, [&](const RowTile &rt, dim3 grid) {
+        hipLaunchKernelGGL(k_angular_raw, grid, dim3(256), 0, s, r, rt, dt, raw);
+    });
+    if (e != hipSuccess || !taps) return e;
+    return over_rows(nseq * L, L, 3 * J, [&](const RowTile &rt, dim3 grid) {
+        hipLaunchKernelGGL(k_gauss_nearest, grid, dim3(256), 0, s, tmp, rt, *taps, out);
+    });
 }
 
 // ----------------------------------------------------------------------------
@@ -576,8 +849,8 @@ hipError_t launch_rebuild_vtrdyn(const TopoView &T, const float *motion, int64_t
 hipError_t launch_ingest_vtrdyn(const float *bp, const float *lhp, const float *rhp, int64_t B, int layout,
                                 float *body, float *lh, float *rh, uint8_t *valid, hipStream_t s)
 {
-    hipLaunchKernelGGL(k_ingest_vtrdyn, dim3(grid_for(B, 256)), dim3(256), 0, s, bp, lhp, rhp, B, body, lh, rh, valid,
-                       layout == RTG_LAYOUT_SOA);
+    hipLaunchKernelGGL(k_ingest_vtrdyn, dim3(grid_for(B, kIngTile)), dim3(256), 0, s, bp, lhp, rhp, B, body, lh, rh,
+                       valid, layout == RTG_LAYOUT_SOA);
     return hipGetLastError();
 }
 

@@ -7,6 +7,7 @@ per op; all arithmetic happens in librtg_hip.so.
 from __future__ import annotations
 
 import ctypes
+import functools
 from typing import Sequence
 
 import torch
@@ -369,8 +370,10 @@ def kinematics_multi(fk_segments: Sequence[tuple], inv_segments: Sequence[tuple]
     return fouts, iouts
 
 
+@functools.lru_cache(maxsize=8)
 def gaussian_taps(sigma: float = 2.0, truncate: float = 4.0):
-    """scipy.ndimage.gaussian_filter1d's taps (float64), as the reference applies them (sigma 2)."""
+    """scipy.ndimage.gaussian_filter1d's taps (float64), as the reference applies them (sigma 2).  Cached (the
+    velocity calls take them every time); the array is read-only."""
     import numpy as np
     radius = int(truncate * float(sigma) + 0.5)
     try:
@@ -380,7 +383,9 @@ def gaussian_taps(sigma: float = 2.0, truncate: float = 4.0):
         x = np.arange(-radius, radius + 1)
         w = np.exp(-0.5 / (sigma * sigma) * x ** 2)
         w = (w / w.sum())[::-1]
-    return np.ascontiguousarray(w, dtype=np.float64), radius
+    w = np.ascontiguousarray(w, dtype=np.float64)
+    w.flags.writeable = False
+    return w, radius
 
 
 def _time_axis_view(x, tail):
@@ -392,26 +397,28 @@ def _time_axis_view(x, tail):
     return x, nseq, L
 
 
-def motion_velocity(p, dt: float, smooth: bool = True):
-    """SkeletonMotion._compute_velocity (skeleton3d.py:1126-1135): p (..., L, J, 3) -> (..., L, J, 3)."""
+def motion_velocity(p, dt: float, smooth: bool = True, sigma: float = 2.0):
+    """SkeletonMotion._compute_velocity (skeleton3d.py:1126-1135): p (..., L, J, 3) -> (..., L, J, 3).  ``sigma``:
+    the smoothing filter's (the reference's is 2; radius 4 sigma, at most 16)."""
     x, nseq, L = _time_axis_view(p, 2)
     S = int(x.shape[-2] * x.shape[-1])
     out = torch.empty_like(x)
     tmp = torch.empty_like(x) if smooth else None
-    w, r = gaussian_taps() if smooth else (None, 0)
+    w, r = gaussian_taps(sigma) if smooth else (None, 0)
     check(lib().rtg_linear_velocity_f32(ptr(x), nseq, L, S, ctypes.c_float(dt),
                                         w.ctypes.data_as(ctypes.c_void_p) if smooth else None, r, ptr(tmp), ptr(out),
                                         stream_handle()))
     return out
 
 
-def motion_angular_velocity(r, dt: float, smooth: bool = True):
-    """SkeletonMotion._compute_angular_velocity (skeleton3d.py:1137-1146): r (..., L, J, 4) -> (..., L, J, 3)."""
+def motion_angular_velocity(r, dt: float, smooth: bool = True, sigma: float = 2.0):
+    """SkeletonMotion._compute_angular_velocity (skeleton3d.py:1137-1146): r (..., L, J, 4) -> (..., L, J, 3).
+    ``sigma`` as in motion_velocity."""
     x, nseq, L = _time_axis_view(r, 2)
     J = int(x.shape[-2])
     out = torch.empty(tuple(x.shape[:-1]) + (3,), device=x.device, dtype=torch.float32)
     tmp = torch.empty_like(out) if smooth else None
-    w, rad = gaussian_taps() if smooth else (None, 0)
+    w, rad = gaussian_taps(sigma) if smooth else (None, 0)
     check(lib().rtg_angular_velocity_f32(ptr(x), nseq, L, J, ctypes.c_float(dt),
                                          w.ctypes.data_as(ctypes.c_void_p) if smooth else None, rad, ptr(tmp),
                                          ptr(out), stream_handle()))

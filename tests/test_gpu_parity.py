@@ -514,14 +514,19 @@ def test_solver_rejects_bad_out_dof_and_device(gpu):
 def test_ingest_soa_matches_aos(gpu):
     from rtg import ingest
     rng = np.random.default_rng(3)
-    B = 1000
+    B = 65536 + 37   # a ragged last 64-frame tile
     b23 = rng.standard_normal((B, 23, 3)).astype(np.float32)
+    b23[[5, 64, B - 1]] = 0.0   # frames without data in the first, second and last tiles
     l20, r20 = (rng.standard_normal((B, 20, 3)).astype(np.float32) for _ in range(2))
     a = ingest.reindex_frames(b23, l20, r20)
     s = ingest.reindex_frames(b23, l20, r20, layout="soa")
     for x, y in zip(a[:3], s[:3]):
         assert torch.equal(x.permute(1, 2, 0), y)
     assert torch.equal(a[3], s[3])
+    np.testing.assert_array_equal(a[0].cpu().numpy(), b23[:, ingest.BODY23_TO_21])
+    np.testing.assert_array_equal(a[1].cpu().numpy(), l20[:, ingest.HAND_ORDER])
+    np.testing.assert_array_equal(a[2].cpu().numpy(), r20[:, ingest.HAND_ORDER])
+    np.testing.assert_array_equal(a[3].cpu().numpy(), ~np.array([np.allclose(x, 0) for x in b23]))
 
 
 @pytest.mark.parametrize("layout", ["aos", "soa"])
@@ -567,3 +572,44 @@ def test_motion_velocities_vs_oracle(gpu):
     # unsmoothed variant and batched sequences
     lv = _np(ops.motion_velocity(np.stack([m["global_pos"]] * 3), 1 / 30, smooth=False))
     np.testing.assert_array_equal(lv[1], orc.linear_velocity(m["global_pos"], 1 / 30, None))
+
+
+@pytest.mark.parametrize("nseq,L,J", [(1, 2, 1), (5, 37, 3), (3, 41, 31), (2, 19, 100), (7, 300, 24), (8, 130, 31),
+                                     (2, 40, 200)])
+def test_motion_velocities_row_tiles(gpu, nseq, L, J):
+    """The velocity kernels across tile shapes -- bit-exact against the oracle, smoothed and raw.  Smoothed: the
+    one-pass frame-tile kernel with 64-frame tiles, 16-frame tiles (J=100: 300 channels per row), block counts
+    that are and are not multiples of 8 (the XCD order), sequences shorter than the filter radius (L=2) and the
+    two-pass fallback for rows too wide for LDS (J=200).  Raw: the row-tiled kernels, rows that do not fill a
+    block, channel counts that are not powers of two, rows wider than 256 channels (gridDim.y slices)."""
+    import oracle as orc
+    from rtg import ops
+    g = np.random.default_rng(nseq * 1000 + L + J)
+    p = g.standard_normal((nseq, L, J, 3)).astype(np.float32)
+    q = g.standard_normal((nseq, L, J, 4)).astype(np.float32)
+    q /= np.linalg.norm(q, axis=-1, keepdims=True)
+    w, _ = ops.gaussian_taps()
+    np.testing.assert_array_equal(_np(ops.motion_velocity(p, 1 / 30)), orc.linear_velocity(p, 1 / 30, w))
+    np.testing.assert_array_equal(_np(ops.motion_velocity(p, 1 / 30, smooth=False)),
+                                  orc.linear_velocity(p, 1 / 30, None))
+    np.testing.assert_array_equal(_np(ops.motion_angular_velocity(q, 1 / 30)), orc.angular_velocity(q, 1 / 30, w))
+    np.testing.assert_array_equal(_np(ops.motion_angular_velocity(q, 1 / 30, smooth=False)),
+                                  orc.angular_velocity(q, 1 / 30, None))
+
+
+@pytest.mark.parametrize("sigma", [0.1, 0.2, 1.0, 3.5])
+def test_motion_velocities_other_filter_radii(gpu, sigma):
+    """Filters other than the reference's sigma 2 (radius 0, 1, 4, 14) take the one-pass kernel's generic-radius
+    branch: bit-exact against the oracle with the same taps."""
+    import oracle as orc
+    from rtg import ops
+    g = np.random.default_rng(int(sigma * 10))
+    p = g.standard_normal((3, 150, 31, 3)).astype(np.float32)
+    q = g.standard_normal((3, 150, 31, 4)).astype(np.float32)
+    q /= np.linalg.norm(q, axis=-1, keepdims=True)
+    w, radius = ops.gaussian_taps(sigma)
+    assert radius == int(4 * sigma + 0.5)
+    np.testing.assert_array_equal(_np(ops.motion_velocity(p, 1 / 30, sigma=sigma)), orc.linear_velocity(p, 1 / 30, w))
+    np.testing.assert_array_equal(_np(ops.motion_angular_velocity(q, 1 / 30, sigma=sigma)),
+                                  orc.angular_velocity(q, 1 / 30, w))
+
