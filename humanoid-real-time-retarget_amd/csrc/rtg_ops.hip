@@ -569,7 +569,7 @@ __global__ __launch_bounds__(256) void k_velocity_tile(const float *__restrict__
     // every thread issues the loads of NB elements before it uses any (latency, not bandwidth, bounds a
     // load-then-use loop at this occupancy)
     if (!ANGULAR) {
-        constexpr int NB = 8;
+        constexpr int NB = 8;    // measured: 16 and 32 slower (profiles/r04/aux/nb_ab.log)
         const float *p = src + seq * L * C;
         const uint32_t n = nx * (uint32_t)C;
         RowWalk w(threadIdx.x, (uint32_t)C);
@@ -595,7 +595,7 @@ __global__ __launch_bounds__(256) void k_velocity_tile(const float *__restrict__
                 if (e0 + 256u * k < n) sg[at[k]] = ((hi[k] - lo[k]) * hf[k]) / dt;
         }
     } else {
-        constexpr int NB = 4;
+        constexpr int NB = 2;    // measured: 2 > 4 > 8 (78 VGPRs, 6 waves/SIMD at 2)
         const int J = vt.J;
         const float *r = src + seq * L * J * 4;
         const uint32_t n = nx * (uint32_t)J;
