@@ -326,7 +326,9 @@ int rtg_quat_as_euler_f64(const float *q, const char *seq, int degrees, int64_t 
  * Time is the middle axis: nseq independent sequences of L frames of S channels.
  * weights: the 2*radius+1 Gaussian taps (scipy _gaussian_kernel1d, sigma=2 ->
  * radius 8, applied with mode='nearest' and float64 accumulation); NULL = no
- * smoothing.  tmp: caller-owned scratch of the output's size.
+ * smoothing.  tmp: caller-owned scratch of the output's size (required with
+ * weights; the one-pass kernel, used while a 16-frame tile's raw rows fit
+ * 48 KB of LDS, leaves it untouched; wider rows filter through it).
  * ---------------------------------------------------------------------- */
 #define RTG_MAX_FILTER_RADIUS 16
 /* p (nseq,L,S) -> out (nseq,L,S): np.gradient over frames / dt, then smoothing. */
