@@ -161,15 +161,18 @@ RTG_DEV int64_t lay_idx(bool soa, int64_t f, int j, int c, int P, int C, int64_t
 }
 
 // VTRDyn ingest (sim_full_body_teleop.py:92,109-112: body 23 -> 21 points, hands reordered, the "frame carries data"
-// flag): one 256-thread block per 64-frame tile.  Each input's tile rows are ONE contiguous span (64 x 69 / 60 / 60
-// floats); every thread issues all its loads of the three spans before it stores any into LDS (a load-then-store
-// loop leaves the tile latency-bound), and the outputs leave coalesced too -- AoS rows (the tile's 64 x 63 / 60
-// floats are again one span) or SoA planes (64 consecutive frames per plane).  LDS rows are padded to an odd
+// flag): one 256-thread block per tile of TILE frames.  Each input's tile rows are ONE contiguous span (TILE x 69 / 60 /
+// 60 floats); every thread issues all its loads of the three spans before it stores any into LDS (a load-then-store
+// loop leaves the tile latency-bound), and the outputs leave coalesced too -- AoS rows (the tile's TILE x 63 / 60
+// floats are again one span) or SoA planes (TILE consecutive frames per plane).  LDS rows are padded to an odd
 // stride so the SoA pass (lanes on consecutive frames) reads distinct banks.  Round 3 moved each frame on one
 // thread: 12-byte pieces 276 / 240 bytes apart per lane, 64 lines per wave instruction (1.3 TB/s).
-constexpr int kIngTile = 64;
+// frames per block, measured at B = 262144 (profiles/r04/aux/ingest_tiles.log): AoS out 64 / 32 / 16 frames 89 / 82 /
+// 80 us; SoA out 128 / 64 / 32 / 16 frames 200 / 111 / 90 / 104 us (smaller tiles: more blocks per CU; SoA below
+// 32 frames writes half lines per plane)
+constexpr int kIngAosTile = 16, kIngSoaTile = 32;
 constexpr int kIngBodyS = 69, kIngHandS = 61;   // LDS row strides (floats)
-template <int R, int RS, int O>
+template <int TILE, int R, int RS, int O>
 RTG_DEV void ingest_rows_out(const float *srow, float *__restrict__ out, const int8_t *map, int64_t f0, int nfr,
                              int64_t B, bool soa)
 {
@@ -181,61 +184,62 @@ RTG_DEV void ingest_rows_out(const float *srow, float *__restrict__ out, const i
             dst[e] = srow[fr * RS + 3 * map[j] + c];
         }
     } else {
-        for (int e = threadIdx.x; e < O * kIngTile; e += 256) {
-            const int plane = e / kIngTile, fr = e - plane * kIngTile, j = plane / 3, c = plane - 3 * j;
+        for (int e = threadIdx.x; e < O * TILE; e += 256) {
+            const int plane = e / TILE, fr = e - plane * TILE, j = plane / 3, c = plane - 3 * j;
             if (fr < nfr) out[(int64_t)plane * B + f0 + fr] = srow[fr * RS + 3 * map[j] + c];
         }
     }
 }
 // the tile's span of R-float rows (n floats) into registers: element tid + 256 k
-template <int R>
-RTG_DEV void ingest_load(const float *src, int n, float (&v)[(kIngTile * R + 255) / 256])
+template <int TILE, int R>
+RTG_DEV void ingest_load(const float *src, int n, float (&v)[(TILE * R + 255) / 256])
 {
 #pragma unroll
-    for (int k = 0; k < (kIngTile * R + 255) / 256; ++k) {
+    for (int k = 0; k < (TILE * R + 255) / 256; ++k) {
         const int e = (int)threadIdx.x + 256 * k;
         v[k] = e < n ? src[e] : 0.0f;
     }
 }
-template <int R, int RS>
-RTG_DEV void ingest_to_lds(const float (&v)[(kIngTile * R + 255) / 256], int n, float *srow)
+template <int TILE, int R, int RS>
+RTG_DEV void ingest_to_lds(const float (&v)[(TILE * R + 255) / 256], int n, float *srow)
 {
 #pragma unroll
-    for (int k = 0; k < (kIngTile * R + 255) / 256; ++k) {
+    for (int k = 0; k < (TILE * R + 255) / 256; ++k) {
         const int e = (int)threadIdx.x + 256 * k;
         if (e < n) srow[(e / R) * RS + e % R] = v[k];
     }
 }
+template <int TILE>
 __global__ __launch_bounds__(256) void k_ingest_vtrdyn(const float *__restrict__ bp, const float *__restrict__ lhp,
                                                        const float *__restrict__ rhp, int64_t B,
                                                        float *__restrict__ body, float *__restrict__ lh,
                                                        float *__restrict__ rh, uint8_t *__restrict__ valid, bool soa)
 {
-    __shared__ float sbody[kIngTile * kIngBodyS], slh[kIngTile * kIngHandS], srh[kIngTile * kIngHandS];
-    __shared__ int sdata[kIngTile];   // the frame carries data: not np.allclose(body_pos, 0)
-    const int64_t f0 = (int64_t)blockIdx.x * kIngTile;
-    const int nfr = (int)((B - f0) < kIngTile ? (B - f0) : kIngTile);
+    __shared__ float sbody[TILE * kIngBodyS], slh[TILE * kIngHandS], srh[TILE * kIngHandS];
+    __shared__ int sdata[TILE];   // the frame carries data: not np.allclose(body_pos, 0)
+    const int64_t f0 = (int64_t)blockIdx.x * TILE;
+    const int nfr = (int)((B - f0) < TILE ? (B - f0) : TILE);
     const int tid = threadIdx.x;
-    float vb[(kIngTile * 69 + 255) / 256], vl[(kIngTile * 60 + 255) / 256], vr[(kIngTile * 60 + 255) / 256];
-    ingest_load<69>(bp + f0 * 69, nfr * 69, vb);
-    ingest_load<60>(lhp + f0 * 60, nfr * 60, vl);
-    ingest_load<60>(rhp + f0 * 60, nfr * 60, vr);
-    if (tid < kIngTile) sdata[tid] = 0;
+    float vb[(TILE * 69 + 255) / 256], vl[(TILE * 60 + 255) / 256], vr[(TILE * 60 + 255) / 256];
+    ingest_load<TILE, 69>(bp + f0 * 69, nfr * 69, vb);
+    ingest_load<TILE, 60>(lhp + f0 * 60, nfr * 60, vl);
+    ingest_load<TILE, 60>(rhp + f0 * 60, nfr * 60, vr);
+    for (int e = tid; e < TILE; e += 256) sdata[e] = 0;
     __syncthreads();
     // the flag over all 69 body values (|x| <= 1e-8 everywhere; a NaN is never close): every writer stores 1
 #pragma unroll
-    for (int k = 0; k < (kIngTile * 69 + 255) / 256; ++k) {
+    for (int k = 0; k < (TILE * 69 + 255) / 256; ++k) {
         const int e = tid + 256 * k;
         if (e < nfr * 69 && !(fabsf(vb[k]) <= 1e-8f)) sdata[e / 69] = 1;
     }
-    ingest_to_lds<69, kIngBodyS>(vb, nfr * 69, sbody);
-    ingest_to_lds<60, kIngHandS>(vl, nfr * 60, slh);
-    ingest_to_lds<60, kIngHandS>(vr, nfr * 60, srh);
+    ingest_to_lds<TILE, 69, kIngBodyS>(vb, nfr * 69, sbody);
+    ingest_to_lds<TILE, 60, kIngHandS>(vl, nfr * 60, slh);
+    ingest_to_lds<TILE, 60, kIngHandS>(vr, nfr * 60, srh);
     __syncthreads();
-    ingest_rows_out<69, kIngBodyS, 63>(sbody, body, c_body23_to_21, f0, nfr, B, soa);
-    ingest_rows_out<60, kIngHandS, 60>(slh, lh, c_hand_order, f0, nfr, B, soa);
-    ingest_rows_out<60, kIngHandS, 60>(srh, rh, c_hand_order, f0, nfr, B, soa);
-    if (tid < nfr) valid[f0 + tid] = sdata[tid] ? 1 : 0;
+    ingest_rows_out<TILE, 69, kIngBodyS, 63>(sbody, body, c_body23_to_21, f0, nfr, B, soa);
+    ingest_rows_out<TILE, 60, kIngHandS, 60>(slh, lh, c_hand_order, f0, nfr, B, soa);
+    ingest_rows_out<TILE, 60, kIngHandS, 60>(srh, rh, c_hand_order, f0, nfr, B, soa);
+    for (int e = tid; e < nfr; e += 256) valid[f0 + e] = sdata[e] ? 1 : 0;
 }
 
 int32_t fk_schedule(const int32_t *parents, int32_t J, int32_t *sched)
@@ -871,8 +875,12 @@ hipError_t launch_rebuild_vtrdyn(const TopoView &T, const float *motion, int64_t
 hipError_t launch_ingest_vtrdyn(const float *bp, const float *lhp, const float *rhp, int64_t B, int layout,
                                 float *body, float *lh, float *rh, uint8_t *valid, hipStream_t s)
 {
-    hipLaunchKernelGGL(k_ingest_vtrdyn, dim3(grid_for(B, kIngTile)), dim3(256), 0, s, bp, lhp, rhp, B, body, lh, rh,
-                       valid, layout == RTG_LAYOUT_SOA);
+    if (layout == RTG_LAYOUT_SOA)
+        hipLaunchKernelGGL(k_ingest_vtrdyn<kIngSoaTile>, dim3(grid_for(B, kIngSoaTile)), dim3(256), 0, s, bp,
+                           lhp, rhp, B, body, lh, rh, valid, true);
+    else
+        hipLaunchKernelGGL(k_ingest_vtrdyn<kIngAosTile>, dim3(grid_for(B, kIngAosTile)), dim3(256), 0, s, bp,
+                           lhp, rhp, B, body, lh, rh, valid, false);
     return hipGetLastError();
 }
 
