@@ -661,6 +661,8 @@ __global__ __launch_bounds__(256) void k_velocity_tile(const float *__restrict__
 // 16 frames do not fit (the two-pass kernels then run)
 static uint32_t vel_tile_frames(int64_t C, int R)
 {
+    // measured at 64 x 4096 x 31 (profiles/r04/aux/vel_tiles.log): 64 / 32 / 16 frames linear 79 / 90 / 108 us,
+    // angular 125 / 140 / 169 us (the halo's share grows faster than the extra blocks per CU help)
     for (uint32_t T = 64; T >= 16; T /= 2)
         if ((int64_t)vel_lds_stride(T, R) * C * 4 <= 48 * 1024) return T;
     return 0;
