@@ -514,7 +514,7 @@ def test_solver_rejects_bad_out_dof_and_device(gpu):
 def test_ingest_soa_matches_aos(gpu):
     from rtg import ingest
     rng = np.random.default_rng(3)
-    B = 65536 + 37   # a ragged last 64-frame tile
+    B = 65536 + 37   # ragged last tiles (16-frame AoS, 32-frame SoA)
     b23 = rng.standard_normal((B, 23, 3)).astype(np.float32)
     b23[[5, 64, B - 1]] = 0.0   # frames without data in the first, second and last tiles
     l20, r20 = (rng.standard_normal((B, 20, 3)).astype(np.float32) for _ in range(2))
