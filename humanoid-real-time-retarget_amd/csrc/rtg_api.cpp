@@ -647,7 +647,8 @@ int rtg_linear_velocity_f32(const float *p, int64_t nseq, int64_t L, int64_t S, 
     GaussTaps taps{};
     int rc = make_taps(w, radius, &taps, "rtg_linear_velocity_f32");
     if (rc != RTG_OK) return rc;
-    RTG_TRY(launch_linear_velocity(p, nseq, L, S, dt, w ? &taps : nullptr, tmp, out, as_stream(stream)), "rtg_linear_velocity_f32 launch");
+    RTG_TRY(launch_linear_velocity(p, nseq, L, S, dt, w ? &taps : nullptr, tmp, out, as_stream(stream)),
+            "rtg_linear_velocity_f32 launch");
     return RTG_OK;
 }
 
@@ -660,7 +661,8 @@ int rtg_angular_velocity_f32(const float *r, int64_t nseq, int64_t L, int64_t J,
     GaussTaps taps{};
     int rc = make_taps(w, radius, &taps, "rtg_angular_velocity_f32");
     if (rc != RTG_OK) return rc;
-    RTG_TRY(launch_angular_velocity(r, nseq, L, J, dt, w ? &taps : nullptr, tmp, out, as_stream(stream)), "rtg_angular_velocity_f32 launch");
+    RTG_TRY(launch_angular_velocity(r, nseq, L, J, dt, w ? &taps : nullptr, tmp, out, as_stream(stream)),
+            "rtg_angular_velocity_f32 launch");
     return RTG_OK;
 }
 
