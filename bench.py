@@ -514,6 +514,12 @@ class DeviceBackend:
     def sync(self):
         self.torch.cuda.synchronize()
 
+    def identity(self):
+        """This rank's GPU: PCI address, UUID, name (rank_flow gathers them and refuses two ranks on one device)."""
+        p = self.torch.cuda.get_device_properties(self.dev)
+        return {"local_rank": self.dev.index, "name": p.name, "arch": p.gcnArchName,
+                "pci": f"{p.pci_domain_id:04x}:{p.pci_bus_id:02x}:{p.pci_device_id:02x}", "uuid": str(p.uuid)}
+
     def probe(self):
         """rtg_box_probe: the shader clock under load, f32 FMA rate and HBM copy bandwidth of this GPU right now,
         plus the clocks rocm-smi reports (kept in the line so numbers from different boxes can be compared)."""
@@ -537,6 +543,42 @@ class DeviceBackend:
         return self._e0.elapsed_time(self._e1)
 
 
+def rank_devices(world, rank, backend):
+    """Every rank's device identity (backend.identity(): PCI address, UUID, name), gathered to all ranks before the
+    timed region.  With one GPU per rank (the device backend) the identities must be distinct: two ranks on one
+    device would report twice the work of one GPU, so EVERY rank raises (none is left waiting in a collective).
+    Backends that share a device on purpose (the one-GPU rehearsal) set SHARES_DEVICE."""
+    ident = getattr(backend, "identity", None)
+    if ident is None:
+        return None
+    me = dict(ident(), rank=rank)
+    if world == 1:
+        return [me]
+    import torch.distributed as dist
+    devices = [None] * world
+    dist.all_gather_object(devices, me)
+    keys = [(d["pci"], d.get("uuid")) for d in devices]
+    if len(set(keys)) != world and not getattr(backend, "SHARES_DEVICE", False):
+        raise RuntimeError(f"bench.py: {world} ranks on {len(set(keys))} distinct devices: {devices}")
+    return devices
+
+
+def comm_info(world, backend):
+    """The collective library the ranks ran over: torch.distributed's backend and, on the device path, RCCL's
+    version (torch's "nccl" backend is RCCL on ROCm)."""
+    info = {"world": world, "backend": None, "rccl_version": None}
+    if world > 1:
+        import torch.distributed as dist
+        info["backend"] = dist.get_backend()
+    if getattr(backend, "DEVICE", False):
+        try:
+            import torch
+            info["rccl_version"] = ".".join(str(v) for v in torch.cuda.nccl.version())
+        except Exception as e:  # noqa: BLE001 -- reported, never fatal
+            info["rccl_version"] = repr(e)
+    return info
+
+
 def rank_flow(world, rank, backend, B, steps, warmup, ring):
     """One rank of the bench: setup broadcast -> own shard of B frames generated locally (seed
     1234 + rank) -> K timed solves between barriers -> max over ranks -> untimed DOF gather to rank 0."""
@@ -550,6 +592,7 @@ def rank_flow(world, rank, backend, B, steps, warmup, ring):
     else:
         parents, lt, tq, zg = setup
     topo, solver = backend.build(parents, lt, tq, zg)
+    devices = rank_devices(world, rank, backend)
     sets = []
     for r in range(ring):
         b, l, r_ = backend.synth(topo, B, 1234 + rank, r * B)
@@ -594,7 +637,8 @@ def rank_flow(world, rank, backend, B, steps, warmup, ring):
     if box is not None:
         box["after"] = probe()
     out = {"wall": wall, "kern_ms": kern_ms, "gpu_step_ms": gpu_step_ms, "frames": world * B * steps, "sets": sets, "topo": topo,
-           "solver": solver, "zl": lt, "zg": zg, "parents": parents, "golden_per_rank": per_rank, "box": box}
+           "solver": solver, "zl": lt, "zg": zg, "parents": parents, "golden_per_rank": per_rank, "box": box,
+           "devices": devices, "comm": comm_info(world, backend)}
     if world > 1:   # final DOF gather to rank 0 (untimed region, reported separately)
         d = sets[(steps - 1) % ring][3]
         backend.sync()
@@ -656,6 +700,8 @@ def main():
         }
         line["settle"] = getattr(backend, "settle", None)
         line["golden_per_rank"] = res["golden_per_rank"]
+        line["devices"] = res["devices"]   # one entry per rank: distinct PCI addresses (checked in rank_flow)
+        line["comm"] = res["comm"]
         line["box"] = res["box"]
         if "gather_ms" in res:
             line["gather_ms"] = res["gather_ms"]
@@ -695,7 +741,8 @@ def host_main(args, backend, world, rank):
     if rank == 0:
         line = {"metric": METRIC, "value": res["frames"] / res["wall"], "unit": "frames/s", "n_gpus": world,
                 "steps": args.steps, "warmup": args.warmup, "backend": type(backend).__name__,
-                "kern_ms": res["kern_ms"], "golden_per_rank": res["golden_per_rank"]}
+                "kern_ms": res["kern_ms"], "golden_per_rank": res["golden_per_rank"], "devices": res["devices"],
+                "comm": res["comm"]}
         if "gathered" in res:
             line["gathered_sha1"] = hashlib.sha1(res["gathered"].numpy().tobytes()).hexdigest()
         print(json.dumps(line), flush=True)

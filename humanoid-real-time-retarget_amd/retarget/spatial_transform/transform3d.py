@@ -38,9 +38,12 @@ def coord_transform(p, order: list = None, dir=None):
 
 def _raise_if_marked(t: torch.Tensor, code: int) -> None:
     """The reference raises for the whole call when one element is refused (rtg.h rtg_frame_error); the kernels
-    mark such elements with RTG_FRAME_NAN | code."""
-    if t.numel() and bool((t.reshape(-1).view(torch.int32) == (_lib.FRAME_NAN | code)).any()):
-        raise_frame_error(code)
+    mark such elements with RTG_FRAME_NAN | code.  The message names the first marked element, as torch's does."""
+    if not t.numel():
+        return
+    rows = (t.reshape(t.shape[0] if t.dim() > 1 else 1, -1).view(torch.int32) == (_lib.FRAME_NAN | code)).any(1)
+    if bool(rows.any()):
+        raise_frame_error(code, int(torch.nonzero(rows)[0, 0]))
 
 
 def cal_joint_quat(zero_pose_local_translation, motion_local_translation):

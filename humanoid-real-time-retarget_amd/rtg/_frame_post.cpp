@@ -41,11 +41,18 @@ std::tuple<int, int, at::Tensor, at::Tensor, c10::optional<at::Tensor>> post(
     at::Tensor lr = at::empty({31, 4}, opt), dof = at::empty({30}, opt);
     c10::optional<at::Tensor> br;
     if (br_src) br = at::empty({59, 4}, opt);
-    const int rc = reinterpret_cast<PostFn>(fn)(
-        reinterpret_cast<uint32_t *>(ctl), (uint32_t)seq, reinterpret_cast<float *>(in), body.data_ptr<float>(),
-        lh.data_ptr<float>(), rh.data_ptr<float>(), reinterpret_cast<const float *>(dof_src),
-        reinterpret_cast<const float *>(lr_src), reinterpret_cast<const float *>(br_src), dof.data_ptr<float>(),
-        lr.data_ptr<float>(), br ? br->data_ptr<float>() : nullptr, (uint32_t)timeout_us);
+    float *const br_dst = br ? br->data_ptr<float>() : nullptr;
+    int rc;
+    {
+        // the post spins until the frame is back (up to timeout_us when the server is late or relaunching): other
+        // Python threads -- the teleop loop's mocap receiver -- run meanwhile, as they did under ctypes
+        pybind11::gil_scoped_release nogil;
+        rc = reinterpret_cast<PostFn>(fn)(
+            reinterpret_cast<uint32_t *>(ctl), (uint32_t)seq, reinterpret_cast<float *>(in), body.data_ptr<float>(),
+            lh.data_ptr<float>(), rh.data_ptr<float>(), reinterpret_cast<const float *>(dof_src),
+            reinterpret_cast<const float *>(lr_src), reinterpret_cast<const float *>(br_src), dof.data_ptr<float>(),
+            lr.data_ptr<float>(), br_dst, (uint32_t)timeout_us);
+    }
     int code = 0;
     if (rc == 0) {
         uint32_t d0;

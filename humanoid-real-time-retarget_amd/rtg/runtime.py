@@ -131,8 +131,11 @@ class DofModel:
 # Frames the reference raises on (rtg.h rtg_frame_error): the batched solve marks them -- every dof of the row NaN,
 # dof[f, 0] = RTG_FRAME_NAN | code -- and the per-frame calls raise what the reference raises.
 FRAME_ERRORS = {
-    _lib.FRAME_SVD_NONFINITE: (RuntimeError, "linalg.svd: (Batch element 0): The algorithm failed to converge because "
-                                             "the input matrix contained non-finite values."),   # transform3d.py:40
+    # transform3d.py:40: eager torch.linalg.svd raises torch.linalg.LinAlgError naming the batch element; through the
+    # reference's @torch.jit.script cal_joint_quat it surfaces as a plain RuntimeError.  LinAlgError subclasses
+    # RuntimeError, so callers catching either form see it
+    _lib.FRAME_SVD_NONFINITE: (torch.linalg.LinAlgError, "linalg.svd: (Batch element {i}): The algorithm failed to "
+                                                         "converge because the input matrix contained non-finite values."),
     _lib.FRAME_ZERO_NORM_QUAT: (ValueError, "Found zero norm quaternions in `quat`."),           # transform3d.py:53
 }
 
@@ -145,12 +148,14 @@ def frame_status(dof: torch.Tensor) -> torch.Tensor:
     return torch.where(marked, d0 & 0xF, torch.zeros_like(d0)).to(torch.int8)
 
 
-def raise_frame_error(code: int) -> None:
-    """Raise the exception the reference raises on a frame with this rtg_frame_error code (no-op for 0)."""
+def raise_frame_error(code: int, index: int = 0) -> None:
+    """Raise the exception the reference raises on a frame with this rtg_frame_error code (no-op for 0).  index is
+    the batch element torch names in the SVD message: 0 for the reference's per-frame (1, 3, 3) call, the first
+    marked element for a batched primitive call."""
     code = int(code)
     if code:
         exc, msg = FRAME_ERRORS.get(code, (RuntimeError, f"rtg frame error {code}"))
-        raise exc(msg)
+        raise exc(msg.format(i=int(index)))
 
 
 # per-frame input rows of each solver kind (rtg.h rtg_solver_kind): (points, components)

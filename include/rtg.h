@@ -237,7 +237,11 @@ int rtg_retarget_f32(rtg_solver_t solver, const float *in0, const float *in1, co
  * iteration through VtrdynFullBodyPosRetargeter.retarget, full_body_pos_retargeter.py:60-176): launches ONE
  * resident workgroup that serves FULL_BODY_POS frames from host-mapped (pinned) memory without a launch per frame.
  *   in        183 floats: body (21,3) | left hand (20,3) | right hand (20,3), rows as rtg_retarget_f32's AoS inputs
- *   dof (30), local_rot (31,4, may be NULL), body_rot (59,4, may be NULL): written per frame
+ *   dof (30), local_rot (31,4, may be NULL), body_rot (59,4, may be NULL): the server OWNS these buffers while it
+ *             runs.  The dof row and the frame-dependent local_rot / body_rot rows are written per frame; the 73
+ *             rows that never change (local_rot's fixed links, body_rot's identity rows) are written once per
+ *             launch and again after a frame the reference raises on.  A client that clears or edits these
+ *             buffers between frames must copy the rows out instead (rtg_frame_server_post does) or relaunch.
  *   ctl       4 x uint32: [0] frame sequence number, written by the host after the frame's inputs;
  *             [1] the last sequence number served, written by the device after that frame's outputs;
  *             [2] set to 1 by the device when the server has ended;
@@ -245,7 +249,8 @@ int rtg_retarget_f32(rtg_solver_t solver, const float *in0, const float *in1, co
  *             Zero ctl[1..3] before the launch.
  * Writing RTG_SERVER_QUIT into ctl[0] ends the server; so does idle_ms (1..60000) without a new frame.  All
  * buffers must be device-accessible host memory (hipHostMalloc / pinned).  The stream is occupied until the
- * server ends.  Outputs are bit-identical to rtg_retarget_f32 at B = 1. */
+ * server ends.  The values in the buffers after a frame is served (ctl[1]) are bit-identical to rtg_retarget_f32's at
+ * B = 1. */
 #define RTG_SERVER_QUIT 0xFFFFFFFFu
 int rtg_frame_server_launch(rtg_solver_t solver, const float *in, float *dof, float *local_rot, float *body_rot,
                             uint32_t *ctl, uint32_t idle_ms, rtg_stream_t stream);

@@ -58,6 +58,13 @@ class HostBackend:
     def sync(self):
         pass
 
+    def identity(self):
+        """A stand-in device identity: this rank's process (RTG_TEST_SAME_DEVICE=1 makes every rank report the
+        same one, to test that rank_flow refuses it)."""
+        if os.environ.get("RTG_TEST_SAME_DEVICE") == "1":
+            return {"name": "host", "pci": "host-0", "uuid": None}
+        return {"name": "host", "pci": f"host-pid-{os.getpid()}", "uuid": None}
+
     def start(self):
         pass
 

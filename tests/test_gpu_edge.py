@@ -205,8 +205,14 @@ def test_dropin_primitives_raise_like_the_reference(gpu):
     q_ok = t3.cal_joint_quat(Z, M)
     assert q_ok.shape == (4, 4) and torch.isfinite(q_ok).all()
     M[2, 1, 0] = float("nan")
-    with pytest.raises(EXC[1][0], match=EXC[1][1]):
+    M[3, 0, 2] = float("nan")
+    # torch's own error: LinAlgError (a RuntimeError) naming the FIRST non-finite batch element, as eager
+    # torch.linalg.svd does on this batch; the per-frame calls name element 0 like the reference
+    with pytest.raises(torch.linalg.LinAlgError, match=EXC[1][1].replace("element 0", "element 2")):
         t3.cal_joint_quat(Z, M)
+    A = torch.einsum("bij,bjk->bik", M.permute(0, 2, 1), Z)
+    with pytest.raises(torch.linalg.LinAlgError, match="Batch element 2"):
+        torch.linalg.svd(A)
     q = torch.nn.functional.normalize(torch.randn(3, 4), dim=-1)
     t3.quat_in_xyz_axis(q, "XYZ")
     q[1] = 0.0
@@ -278,3 +284,7 @@ def test_bench_device_path_two_ranks_on_one_gpu():
     assert [g["rank"] for g in line["golden_per_rank"]] == [0, 1]
     assert all(g["max_abs_err"] < 1e-4 for g in line["golden_per_rank"])
     assert "gather_ms" in line
+    # both ranks report the device they ran on (the same card here: the rehearsal backend sets SHARES_DEVICE) and the
+    # line names the collective backend and the RCCL build torch carries
+    assert [d["rank"] for d in line["devices"]] == [0, 1] and all(d["pci"] for d in line["devices"])
+    assert line["comm"]["backend"] == "gloo" and line["comm"]["rccl_version"]

@@ -220,6 +220,20 @@ def test_bench_gpus_flag_spawns_ranks_world2():
         want.append(orc.full_body_pos(assets.local_translation("vtrdyn_full"), zp["vtrdyn_full_global_t"], b, l, rr,
                                       True, want_rot=False)[0])
     assert line["gathered_sha1"] == hashlib.sha1(np.ascontiguousarray(np.concatenate(want)).tobytes()).hexdigest()
+    # the line proves its N: one device identity per rank, all distinct, and the collective backend used
+    assert [d["rank"] for d in line["devices"]] == [0, 1]
+    assert len({d["pci"] for d in line["devices"]}) == 2
+    assert line["comm"]["backend"] == "gloo" and line["comm"]["world"] == 2
+
+
+def test_bench_refuses_two_ranks_on_one_device():
+    """Two ranks reporting the same device identity: every rank raises before the timed region (none hangs in a
+    collective) and no line is printed."""
+    r = _bench_cmd("--gpus", "2", "--steps", "2", "--warmup", "1", "--batch", "8", "--ring", "2",
+                   env_extra={"RTG_TEST_SAME_DEVICE": "1"})
+    assert r.returncode != 0
+    assert not [l for l in r.stdout.splitlines() if l.startswith("{")]
+    assert "2 ranks on 1 distinct devices" in r.stderr
 
 
 def test_bench_gpus_flag_must_match_launcher_world():
