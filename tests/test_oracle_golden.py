@@ -138,37 +138,76 @@ def test_kabsch_sgesdd_vs_polar_factor():
 
 
 def _torch_vml():
-    """MKL VML entry points torch itself calls for acos / sin / cos (VML_HA), or None."""
+    """MKL VML entry points torch itself calls for acos / sin / cos / sqrt (VML_HA), or None."""
     import ctypes
     try:
         import torch
         L = ctypes.CDLL(os.path.join(os.path.dirname(torch.__file__), "lib", "libtorch_cpu.so"))
-        return [ctypes.cast(getattr(L, f), ctypes.c_void_p) for f in ("vmsAcos", "vmsSin", "vmsCos")]
+        return [ctypes.cast(getattr(L, f), ctypes.c_void_p) for f in ("vmsAcos", "vmsSin", "vmsCos", "vmsSqrt")]
     except (OSError, AttributeError, ImportError):
         return None
 
 
 def test_vml_attribution():
-    """Attribution of the remaining residual: with torch's own VML acos/sin/cos routed into the oracle (a
-    test-only hook), every solver moves to (near) bit-equality with the reference -- what is left after the
-    sgesdd restatement is MKL VML's rounding, which no restatement of the published algorithm can reproduce.
-    VML's bits depend on the host CPU's dispatch; the numbers were measured on the build container's AVX-512
-    Xeon, where the goldens were made."""
+    """Attribution of the remaining residual: with torch's own VML acos / sin / cos / sqrt routed into the oracle's
+    eight VML call sites (a test-only hook), every solver golden is reproduced BIT FOR BIT -- the oracle is the
+    reference's arithmetic exactly, except that it rounds those four functions correctly where MKL VML does not.
+    tools/vml_attrib.py attributes each over-1e-5 frame to the single VML call that causes it
+    (profiles/r05/vml_attrib.md).  VML's bits depend on the host CPU's dispatch; the goldens were made on the build
+    container's AVX-512 Xeon."""
     import ctypes
     fns = _torch_vml()
     if fns is None or "avx512f" not in open("/proc/cpuinfo").read():
         pytest.skip("torch's VML or an AVX-512 host (the goldens' ISA) is not available")
     lib = orc.lib()
-    lib.oracle_set_vml(*fns, ctypes.c_longlong(0x140102))   # VML_HA | VML_FTZDAZ_OFF | VML_ERRMODE_IGNORE
+    lib.oracle_set_vml(*fns[:3], ctypes.c_longlong(0x140102))   # VML_HA | VML_FTZDAZ_OFF | VML_ERRMODE_IGNORE
+    lib.oracle_set_vml_sqrt(fns[3])
     try:
-        stats = {}
-        for name in BOUNDS:
-            dof, d = _run(name)
-            stats[name] = frame_stats(dof, d["dof"])
+        got = {name: _run(name) for name in BOUNDS}
     finally:
         lib.oracle_set_vml(None, None, None, ctypes.c_longlong(0))
-    for name, s in stats.items():
-        assert s["exact_elems"] >= 0.98 and s["frac_frames_gt_1e5"] <= 0.008 and s["p99_frame"] <= 2e-6, (name, s)
+        lib.oracle_set_vml_sqrt(None)
+    for name, (dof, d) in got.items():
+        np.testing.assert_array_equal(dof, d["dof"], err_msg=name)
+
+
+def test_vml_attribution_one_call_per_frame():
+    """Every solver-golden frame over 1e-5 is moved there by ONE VML call: with VML's value at that call alone (and
+    correctly rounded everywhere else) the frame is within 1e-5 (tools/vml_attrib.py, profiles/r05/vml_attrib.json).
+    The calls sit at five different sites, on inputs spread over their whole domains -- no narrow-domain table can
+    restate them."""
+    import ctypes
+    import json
+    fns = _torch_vml()
+    if fns is None or "avx512f" not in open("/proc/cpuinfo").read():
+        pytest.skip("torch's VML or an AVX-512 host (the goldens' ISA) is not available")
+    rep = json.load(open(os.path.join(REPO, "profiles", "r05", "vml_attrib.json")))
+    lib = orc.lib()
+    lib.oracle_set_threads(1)
+    lib.oracle_set_vml(*fns[:3], ctypes.c_longlong(0x140102))
+    lib.oracle_set_vml_sqrt(fns[3])
+    lib.oracle_set_vml_sites(ctypes.c_uint32(0))
+    checked = 0
+    try:
+        for name, sol in rep["solvers"].items():
+            d = golden(name)
+            for fr in sol["over_tol"]:
+                f = fr["frame"]
+                one = min(fr["calls_by_effect"], key=lambda c: c["frame_err_with_this_call_vml_alone"])
+                lib.oracle_set_vml_call(ctypes.c_int(one["call"]))
+                dof = _run_frames(name, np.array([f]))
+                lib.oracle_set_vml_call(ctypes.c_int(-1))
+                assert np.abs(dof[0].astype(np.float64) - d["dof"][f]).max() <= 1e-5, (name, f, one)
+                lib.oracle_set_vml_sites(ctypes.c_uint32(0))
+                assert np.abs(_run_frames(name, np.array([f]))[0].astype(np.float64) - d["dof"][f]).max() > 1e-5
+                checked += 1
+    finally:
+        lib.oracle_set_vml_call(ctypes.c_int(-1))
+        lib.oracle_set_vml_sites(ctypes.c_uint32(0xFFFFFFFF))
+        lib.oracle_set_vml(None, None, None, ctypes.c_longlong(0))
+        lib.oracle_set_vml_sqrt(None)
+        lib.oracle_set_threads(os.cpu_count() or 1)
+    assert checked == 14
 
 
 BOUNDS = {  # the measured residual, rounded up in the third digit (DESIGN.md §2.2): max, p99 of per-frame max,
@@ -194,6 +233,23 @@ def _run(name):
     if name == "full_body_rot":
         return orc.full_body_rot(zp["vtrdyn_full_local_t"], d["body_rot"], d["body_pos"], d["lh"], d["rh"])[0], d
     return orc.body_rot(assets.parents("vtrdyn"), d["global_rot"])[0], d
+
+
+def _run_frames(name, idx):
+    """The oracle's DOFs of the golden frames idx (oracle_vml_log / oracle_set_vml_call count calls from here)."""
+    from rtg import assets
+    zp = golden("zero_pose")
+    d = golden(name)
+    orc.lib().oracle_vml_log(None, 0)   # restarts the call count
+    if name.startswith("full_body_pos"):
+        return orc.full_body_pos(zp["vtrdyn_full_local_t"], zp["vtrdyn_full_global_t"], d["body"][idx], d["lh"][idx],
+                                 d["rh"][idx], bool(d["precise_gripper"]), want_rot=False)[0]
+    if name == "upper_body":
+        return orc.upper_body(zp["vtrdyn_local_t"], d["x"][idx])[0]
+    if name == "full_body_rot":
+        return orc.full_body_rot(zp["vtrdyn_full_local_t"], d["body_rot"][idx], d["body_pos"][idx], d["lh"][idx],
+                                 d["rh"][idx])[0]
+    return orc.body_rot(assets.parents("vtrdyn"), d["global_rot"][idx])[0]
 
 
 @pytest.mark.parametrize("name", list(BOUNDS))

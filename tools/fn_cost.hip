@@ -12,6 +12,8 @@
 //         -fno-fast-math -I include -I humanoid-real-time-retarget_amd/csrc tools/fn_cost.hip -o tools/fn_cost
 #include <cstdio>
 
+#include <cstdlib>
+
 #include "rtg_math.cuh"
 
 using namespace rtg;
@@ -30,15 +32,18 @@ __device__ __forceinline__ V rv(uint32_t i, uint32_t k) { return V{sn(i, k), sn(
 
 enum {
     F_EMPTY, F_EXP, F_ACOS, F_SINCOS, F_ATAN2, F_NORMANG, F_RADB, F_FAA, F_QNORM, F_ROTMAT, F_KAB3, F_KAB5,
-    F_EULER, F_QXYZ, F_SHPR, F_ELPY, F_QROT, F_DIV, F_COUNT
+    F_EULER, F_QXYZ, F_SHPR, F_ELPY, F_QROT, F_DIV, F_EXPTAB, F_QMULNORM, F_HANDX, F_SQRTCR, F_SCRCP, F_RCP64,
+    F_COUNT
 };
 static const char *kNames[F_COUNT] = {"empty", "qexp_component", "cr_acos", "cr_sincos", "f_atan2f",
                                       "normalize_angle", "radians_between", "qfrom_angle_axis", "qnormalize",
                                       "qfrom_rotmat", "cal_joint_quat<3>", "cal_joint_quat<5>", "scipy_as_euler",
-                                      "quat_in_xyz_axis", "shoulder_pr", "elbow_py", "qrotate", "f32 div"};
+                                      "quat_in_xyz_axis", "shoulder_pr", "elbow_py", "qrotate", "f32 div",
+                                      "exp_dof (table)", "qmul_norm", "hand_x_mean", "cr_sqrt", "sqrt_clamp_rcp",
+                                      "rcp64+mulr_q"};
 
 template <int F>
-__global__ __launch_bounds__(256) void kcost(float *out)
+__global__ __launch_bounds__(256) void kcost(float *out, const uint32_t *__restrict__ tab)
 {
     const uint32_t i = blockIdx.x * 256u + threadIdx.x;
     float r = 0.0f;
@@ -117,20 +122,42 @@ __global__ __launch_bounds__(256) void kcost(float *out)
     } else if (F == F_DIV) {
         const Q q = rq(i);
         r = q.x / q.w;
+    } else if (F == F_EXPTAB) {   // one exp-map DOF read-out through the angle table (all entries tabulated)
+        const Q q = rq(i);
+        r = exp_dof_finish(exp_dof_table_part(q.w, tab), q.y);
+    } else if (F == F_QMULNORM) {
+        const Q q = qmul_norm(rq(i), rq(i + 7));
+        r = q.x + q.w;
+    } else if (F == F_HANDX) {
+        const V tip[5] = {rv(i, 3), rv(i, 6), rv(i, 9), rv(i, 12), rv(i, 15)};
+        const Q rot = rq(i);   // rtg_solver.cuh hand_x_mean
+        const float x0 = qrotate(rot, rv(i, 18)).x;
+        r = mean5(qrotate(rot, tip[0]).x - x0, qrotate(rot, tip[1]).x - x0, qrotate(rot, tip[2]).x - x0,
+                  qrotate(rot, tip[3]).x - x0, qrotate(rot, tip[4]).x - x0);
+    } else if (F == F_SQRTCR) {
+        r = cr_sqrt(rq(i).w + 1.5f);
+    } else if (F == F_SCRCP) {
+        const NormRcp n = sqrt_clamp_rcp(rq(i).w + 1.5f, 1e-9f);
+        r = n.n + (float)n.r.r;
+    } else if (F == F_RCP64) {
+        const Q q = rq(i);
+        const Q u = mulr_q(q, rcp64(q.w + 2.0f));
+        r = u.x + u.y + u.z + u.w;
     }
     out[i] = r;
 }
 
+static const uint32_t *g_tab;
 template <int F>
 static float run(float *d)
 {
     hipEvent_t s, e;
     (void)hipEventCreate(&s);
     (void)hipEventCreate(&e);
-    hipLaunchKernelGGL(kcost<F>, dim3(NLANES / 256), dim3(256), 0, 0, d);
+    hipLaunchKernelGGL(kcost<F>, dim3(NLANES / 256), dim3(256), 0, 0, d, g_tab);
     (void)hipEventRecord(s);
     const int reps = 5;
-    for (int k = 0; k < reps; ++k) hipLaunchKernelGGL(kcost<F>, dim3(NLANES / 256), dim3(256), 0, 0, d);
+    for (int k = 0; k < reps; ++k) hipLaunchKernelGGL(kcost<F>, dim3(NLANES / 256), dim3(256), 0, 0, d, g_tab);
     (void)hipEventRecord(e);
     (void)hipEventSynchronize(e);
     float ms = 0;
@@ -149,6 +176,16 @@ int main()
 {
     float *d;
     if (hipMalloc(&d, NLANES * sizeof(float)) != hipSuccess) return 1;
+    uint32_t *tab;   // every code 4: the table path with move 0 for every w in [0.25, 1)
+    if (hipMalloc(&tab, kAngTabWords * sizeof(uint32_t)) != hipSuccess) return 1;
+    if (hipMemset(tab, 0, kAngTabWords * sizeof(uint32_t)) != hipSuccess) return 1;
+    {
+        uint32_t *h = (uint32_t *)malloc(kAngTabWords * sizeof(uint32_t));
+        for (uint32_t k = 0; k < kAngTabWords; ++k) h[k] = 0x24924924u;   // 3-bit codes 4,4,... (10 per word)
+        if (hipMemcpy(tab, h, kAngTabWords * sizeof(uint32_t), hipMemcpyHostToDevice) != hipSuccess) return 1;
+        free(h);
+    }
+    g_tab = tab;
     float t[F_COUNT];
     all<0>(d, t);
     printf("%-22s %10s %12s\n", "function", "us/2^21", "ps/call net");
