@@ -35,6 +35,15 @@
 #ifndef RTG_EXP_NO_TABLE
 #define RTG_EXP_NO_TABLE 0
 #endif
+#ifndef RTG_EXP_LARTG_RCP64
+#define RTG_EXP_LARTG_RCP64 0   // A/B knob (same values): SLARTG / SLASV2 quotients by rcp64 + mulr_k<2> (round 4's form)
+#endif
+#ifndef RTG_EXP_SQRT64
+#define RTG_EXP_SQRT64 0   // A/B knob (same values): cr_sqrt as round 4's v_sqrt_f64 + Newton
+#endif
+#ifndef RTG_EXP_ACOS_LIBM
+#define RTG_EXP_ACOS_LIBM 0   // A/B knob (same values): cr_acos as round 4's libm f64 acos
+#endif
 #ifndef RTG_EXP_STUB_SVD
 #define RTG_EXP_STUB_SVD 0   // measurement knob (tools/build_variants.sh): R = identity-ish, wrong answers
 #endif

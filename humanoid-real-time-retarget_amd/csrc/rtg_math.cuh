@@ -33,9 +33,8 @@ RTG_DEV float ieee_sqrtf(float x) { return __builtin_sqrtf(x); }   // IEEE sqrt 
 // Correctly rounded f32 sqrt in 6 instructions: v_sqrt_f64 (not accurate enough alone: it misses on 4 % of
 // inputs) plus one Newton correction gives ~2^-100, and sqrt of an f32 is never within 2^-51 of an f32
 // midpoint, so the single rounding is exact.  0 / inf / NaN / negative: the residual is 0 or NaN and the raw
-// v_sqrt_f64 value (IEEE for those) is kept.  Proven equal to __builtin_sqrtf on all 2^32 inputs by
-// tools/check_fastmath.hip (run by tests/test_gpu_parity.py).
-RTG_DEV float cr_sqrt(float x)
+// v_sqrt_f64 value (IEEE for those) is kept.  The rare-input path of cr_sqrt below.
+RTG_DEV float cr_sqrt64(float x)
 {
     const double d = (double)x;
     const double y = __builtin_amdgcn_sqrt(d);
@@ -43,20 +42,102 @@ RTG_DEV float cr_sqrt(float x)
     const double y1 = __builtin_fma(r, 0.5 * __builtin_amdgcn_rcp(y), y);
     return (float)((r == 0.0 || r != r) ? y : y1);
 }
-RTG_DEV float cr_acos(float x) { return (float)::acos((double)x); }
+// Correctly rounded f32 sqrt in f32 arithmetic (round 5): v_sqrt_f32 is within 1 ulp for x >= 2^-96, and of the
+// candidates s - ulp, s, s + ulp the signs of the exact residuals x - (s - ulp) s and x - (s + ulp) s (one fma each)
+// pick the correctly rounded one -- the sequence LLVM emits for a correctly rounded f32 sqrt, without its denormal
+// scaling.  x below 2^-96 (0, denormals, negatives), inf and NaN take cr_sqrt64 behind one rare-case branch.  No f64
+// instruction on the common path (cr_sqrt64: three f64 ops and two quarter-rate f64 transcendentals).  Proven equal
+// to __builtin_sqrtf on all 2^32 inputs by tools/check_fastmath.hip [1] (run by tests/test_gpu_parity.py).
+__device__ __attribute__((noinline)) float cr_sqrt64_call(float x) { return cr_sqrt64(x); }
+RTG_DEV float cr_sqrt(float x)
+{
+#if RTG_EXP_SQRT64   // A/B knob (same values): round 4's f64 form everywhere
+    return cr_sqrt64(x);
+#endif
+    float s = __builtin_amdgcn_sqrtf(x);
+    const float sdn = __uint_as_float(__float_as_uint(s) - 1u), sup = __uint_as_float(__float_as_uint(s) + 1u);
+    const float rdn = __builtin_fmaf(-sdn, s, x), rup = __builtin_fmaf(-sup, s, x);
+    s = rdn <= 0.0f ? sdn : s;
+    s = rup > 0.0f ? sup : s;
+    if (__builtin_expect(!(x >= 0x1p-96f && x <= 3.40282347e38f), 0)) s = cr_sqrt64_call(x);
+    return s;
+}
+// Rounding test for an f64 approximation y of a value whose f32 rounding is wanted: true when the bits f32 rounding
+// drops (29 of them, for an f32-normal |y|) are not within D f64 ulps of the midpoint 2^28, i.e. every value within
+// D ulps of y rounds to (float)y.  An approximation with relative error <= 2^-k is within 2^(53-k) ulps.  Integer
+// work only (v_and, v_sub, v_cmp).  0 and results below the f32 normal range read as not safe.
+RTG_DEV bool f32_round_safe(double y, uint32_t D)
+{
+    const uint64_t b = (uint64_t)__double_as_longlong(y);
+    const uint32_t lo = (uint32_t)b & 0x1FFFFFFFu;
+    const uint32_t ex = (uint32_t)(b >> 52) & 0x7FFu;
+    return (lo - (0x10000000u - D)) > 2u * D && ex >= 1023u - 126u && ex <= 1023u + 127u;
+}
+RTG_DEV float acos_libm(float x) { return (float)::acos((double)x); }
+// the rare-case call of cr_acos, out of line: inlined into the hot path, its registers raised the side kernel from
+// 127 to 145 VGPRs (3 waves/SIMD instead of 4)
+__device__ __attribute__((noinline)) float acos_libm_call(float x) { return acos_libm(x); }
+// Correctly rounded f32 acos (round 5): torch.acos's value, rounded once.  acos x = pi/2 - sign(x) asin|x| for
+// |x| <= 1/2 and 2 asin s (x > 0) / pi - 2 asin s (x < 0) with s = sqrt((1 - |x|) / 2) otherwise -- one instruction
+// stream for both, asin s = s + s t P(t) with t = s^2 in [0, 1/4] (P: degree-9 minimax of (asin sqrt t - sqrt t) /
+// t^1.5, error 2^-44 -> 2^-46 relative in asin), all in f64.  s comes from f32 seeds: s_hi = v_sqrt_f32(t), then
+// s = s_hi + (t - s_hi^2) / (2 s_hi) with v_rcp_f32 (relative error <= 2^-46).  The result is within 2^-45 of acos
+// x, i.e. 2^8 f64 ulps; f32_round_safe with D = 2^12 accepts it, otherwise (about 1 call in 2^16, and |x| > 1, NaN,
+// x = +-1) the libm f64 acos runs behind one rare-case branch.  tools/check_fastmath.hip [6] proves it equal to
+// (float)acos((double)x) for every f32 x.
+RTG_DEV float acos_fast(float x, bool &ok)
+{
+    const float ax = __builtin_fabsf(x);
+    const bool big = ax > 0.5f, neg = x < 0.0f;
+    const float t32 = (1.0f - ax) * 0.5f;   // exact for ax in [1/2, 1]
+    const float shi = __builtin_amdgcn_sqrtf(t32), rhi = __builtin_amdgcn_rcpf(shi);
+    const double ad = (double)ax, sd = (double)shi;
+    const double t = big ? (double)t32 : ad * ad;   // ad * ad is exact (24-bit operands)
+    const double sb = __builtin_fma(__builtin_fma(-sd, sd, t), 0.5 * (double)rhi, sd);
+    const double sv = big ? sb : ad;
+    double p = 0.02812845967375316;
+    p = __builtin_fma(p, t, -0.0031884549095405512);
+    p = __builtin_fma(p, t, 0.0157919883306133);
+    p = __builtin_fma(p, t, 0.013158578722490823);
+    p = __builtin_fma(p, t, 0.01744580641234927);
+    p = __builtin_fma(p, t, 0.02236569402301675);
+    p = __builtin_fma(p, t, 0.03038220079156473);
+    p = __builtin_fma(p, t, 0.04464285200108894);
+    p = __builtin_fma(p, t, 0.07500000003992044);
+    p = __builtin_fma(p, t, 0.16666666666661556);
+    const double as = __builtin_fma(sv * t, p, sv);
+    const double A = big ? (neg ? 3.141592653589793 : 0.0) : 1.5707963267948966;
+    const double Bc = big ? (neg ? -2.0 : 2.0) : (neg ? 1.0 : -1.0);
+    const double y = __builtin_fma(Bc, as, A);
+    ok = f32_round_safe(y, 1u << 12) && ax < 1.0f;
+    return (float)y;
+}
+RTG_DEV float cr_acos(float x)
+{
+#if RTG_EXP_ACOS_LIBM   // A/B knob (same values): round 4's libm f64 acos everywhere
+    return acos_libm(x);
+#endif
+    bool ok;
+    float r = acos_fast(x, ok);
+    if (__builtin_expect(!ok, 0)) r = acos_libm_call(x);
+    return r;
+}
 RTG_DEV float cr_sin(float x) { return (float)::sin((double)x); }
 RTG_DEV float cr_cos(float x) { return (float)::cos((double)x); }
 // sin and cos of one argument, correctly rounded: fast shared-reduction path
 // (rtg_crmath.h, exhaustively checked against glibc) with the libm f64 call as
 // the exact fallback for the ~1-in-10^7 values the rounding test declines.
 struct SC { float s, c; };
+// the rare-case libm calls of cr_sincos, out of line (registers: see acos_libm_call)
+__device__ __attribute__((noinline)) float sin_libm_call(double x) { return (float)::sin(x); }
+__device__ __attribute__((noinline)) float cos_libm_call(double x) { return (float)::cos(x); }
 RTG_DEV SC cr_sincos(double x)
 {
     const crm::SinCos r = crm::crm_sincos(x);
     SC out{r.s, r.c};
     if (__builtin_expect(!(r.s_ok && r.c_ok), 0)) {   // one rare-case branch for the pair
-        if (!r.s_ok) out.s = (float)::sin(x);
-        if (!r.c_ok) out.c = (float)::cos(x);
+        if (!r.s_ok) out.s = sin_libm_call(x);
+        if (!r.c_ok) out.c = cos_libm_call(x);
     }
     return out;
 }
@@ -473,6 +554,12 @@ RTG_DEV ExpDof exp_dof_table_part(float w, const uint32_t *__restrict__ tab)
     return ExpDof{__uint_as_float(__float_as_uint(P) + code - kAngTabBias), sin_theta, mask, mask && code == 0u};
 }
 RTG_DEV float exp_dof_finish(const ExpDof &e, float qk) { return e.mask ? e.angle * (qk / e.sin_theta) : 0.0f; }
+// the exact path of one read-out whose mask holds (w outside the table or a code-0 entry), out of line
+__device__ __attribute__((noinline)) float exp_dof_exact(float w, float qk)
+{
+    const float angle = normalize_angle(2.0f * cr_acos(w));
+    return angle * (qk / cr_sqrt(1.0f - w * w));
+}
 RTG_DEV float qexp_component_tab(Q q, int k, const uint32_t *__restrict__ tab)
 {
     return exp_dof_tab(q.w, k == 0 ? q.x : (k == 1 ? q.y : q.z), tab);
@@ -654,10 +741,14 @@ RTG_DEV void la_lartg(float f, float g, float &c, float &s, float &r)   // SLART
     // outputs behind ONE rare-case branch -- the same operations per case as the reference's cascade
     {
         const float d = la_sqrt(f * f + g * g);
+#if RTG_EXP_LARTG_RCP64   // A/B knob (round 5): the two quotients through rcp64 + mulr_k<2> (same values)
         const Rcp rd = rcp64(d);
         const float num[2] = {f1, g};
         float quo[2];
         mulr_k<2>(num, rd, quo);
+#else
+        const float quo[2] = {fdiv(f1, d), fdiv(g, d)};
+#endif
         c = quo[0];
         r = __builtin_copysignf(d, f);
         s = f < 0.0f ? -quo[1] : quo[1];   // g / r with r = +-d (RN is sign-symmetric)
@@ -730,6 +821,7 @@ RTG_DEV void la_lasv2(float f, float g, float h, float &ssmin, float &ssmax, flo
             if (mm == 0.0f) t = l == 0.0f ? la_sign(2.0f, ft) * la_sign(1.0f, gt) : fdiv(gt, la_sign(d, ft)) + fdiv(m, t);
             else t = (fdiv(m, s + t) + fdiv(m, r + l)) * (1.0f + a);
             const float l2 = la_sqrt(t * t + 4.0f);
+#if RTG_EXP_LARTG_RCP64
             const Rcp rl = rcp64(l2);
             {
                 const float num[2] = {2.0f, t};
@@ -744,6 +836,12 @@ RTG_DEV void la_lasv2(float f, float g, float h, float &ssmin, float &ssmax, flo
             mulr_k<2>(num, ra, quo);
             clt = quo[0];
             slt = quo[1];
+#else
+            crt = fdiv(2.0f, l2);
+            srt = fdiv(t, l2);
+            clt = fdiv(crt + srt * m, a);
+            slt = fdiv(fdiv(ht, ft) * srt, a);
+#endif
         }
     }
     if (swap) { csl = srt; snl = crt; csr = slt; snr = clt; }
@@ -1056,10 +1154,11 @@ RTG_DEV void kabsch_rot(const float A[9], float R[9])
 #pragma unroll
         for (int k = 0; k < 3; ++k)
             R[i * 3 + k] = (z.u[i] * z.vt[3 * k] + z.u[i + 3] * z.vt[1 + 3 * k]) + z.u[i + 6] * z.vt[2 + 3 * k];
-    const double det = (double)R[0] * ((double)R[4] * R[8] - (double)R[5] * R[7]) -
-                       (double)R[1] * ((double)R[3] * R[8] - (double)R[5] * R[6]) +
-                       (double)R[2] * ((double)R[3] * R[7] - (double)R[4] * R[6]);
-    if (det < 0.0) {
+    // R = U Vt is orthogonal to ~1e-6 (U and Vt are products of plane rotations and reflectors) or all NaN, so
+    // |det R| = 1 +- 1e-6 and the sign any f32 evaluation gives is torch.linalg.det's (the oracle keeps f64)
+    const float det = R[0] * (R[4] * R[8] - R[5] * R[7]) - R[1] * (R[3] * R[8] - R[5] * R[6]) +
+                      R[2] * (R[3] * R[7] - R[4] * R[6]);
+    if (det < 0.0f) {
 #pragma unroll
         for (int k = 0; k < 3; ++k) z.vt[2 + 3 * k] = -z.vt[2 + 3 * k];
 #pragma unroll

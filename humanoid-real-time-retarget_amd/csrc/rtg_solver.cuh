@@ -70,8 +70,7 @@ struct Emit {
             for (int j = s0; j < s0 + n; ++j)
                 if ((exact >> j) & 1u) {
                     const float2 v = st[j * sst];
-                    const float angle = normalize_angle(2.0f * cr_acos(v.x));
-                    row[j < 7 ? 11 + j : 13 + j] = angle * (v.y / cr_sqrt(1.0f - v.x * v.x));   // mask holds here
+                    row[j < 7 ? 11 + j : 13 + j] = exp_dof_exact(v.x, v.y);
                 }
         }
     }

@@ -26,7 +26,7 @@ class BaseHumanoidRetargeter(ABC):
     SOLVER_KIND: Optional[int] = None
 
     def __init__(self, source_zero_pose: RobotZeroPose, target_zero_pose: RobotZeroPose, precise_gripper=False, *,
-                 frame_server: Optional[bool] = None, idle_ms: int = 5):
+                 frame_server: Optional[bool] = None, idle_ms: int = 100):
         self.source_zero_pose = source_zero_pose
         self.target_zero_pose = target_zero_pose
         self._motion_local_rotation = []
@@ -36,13 +36,16 @@ class BaseHumanoidRetargeter(ABC):
         self._frame_runner = None
         self.configure_per_frame(frame_server, idle_ms)
 
-    def configure_per_frame(self, frame_server: Optional[bool] = None, idle_ms: int = 5):
+    def configure_per_frame(self, frame_server: Optional[bool] = None, idle_ms: int = 100):
         """How single host frames are served (an addition to the reference API).
 
         frame_server=True (the default for FULL_BODY_POS; RTG_FRAME_SERVER=0 turns it off): a resident workgroup
         serves the frames with no launch per frame (rtg.realtime.FrameServer).  It ends after ``idle_ms`` without a
-        frame (default 5 ms: a device-wide synchronize between frames waits at most that long), on :meth:`close`,
-        or at interpreter exit, and relaunches itself on the next frame.  frame_server=False, and every other
+        frame, on :meth:`close`, or at interpreter exit, and relaunches itself on the next frame.  Default 100 ms,
+        measured with the teleop loop's own work between frames (tools/extra_bench.py teleop_gaps,
+        profiles/r05/teleop/): with 5-33 ms between frames a 5 ms server ended and relaunched every frame (60-186 us
+        median per call) while a 50-200 ms one served each frame in 26-31 us (FrameGraph: 54-151 us).  While the
+        server runs, a device-wide synchronize waits until it ends: close() it first.  frame_server=False, and every other
         solver kind: one launch per frame over pinned memory on a private stream (rtg.realtime.FrameGraph) --
         nothing stays resident."""
         if frame_server is None:

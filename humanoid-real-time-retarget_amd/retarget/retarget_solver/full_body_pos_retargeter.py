@@ -19,7 +19,7 @@ from retarget.retarget_solver.base_retargeter import BaseHumanoidRetargeter
 class VtrdynFullBodyPosRetargeter(BaseHumanoidRetargeter):
     SOLVER_KIND = _lib.SOLVER_FULL_BODY_POS
 
-    def __init__(self, mocap_zero_pose, target_zero_pose, precise_gripper=False, *, frame_server=None, idle_ms=5):
+    def __init__(self, mocap_zero_pose, target_zero_pose, precise_gripper=False, *, frame_server=None, idle_ms=100):
         super().__init__(mocap_zero_pose, target_zero_pose, precise_gripper, frame_server=frame_server,
                          idle_ms=idle_ms)
         self.precise_gripper = precise_gripper

@@ -268,14 +268,15 @@ def test_frame_server_matches_batched(gpu):
 def test_per_frame_calls_do_not_stall_device_synchronize(gpu):
     """a torch.cuda.synchronize() between teleop frames returns at once with the one-launch path
     (frame_server=False, nothing resident) and within the server's idle_ms with the resident server -- the default,
-    5 ms; close() ends it at once; one runner serves both retarget() (body_rot) and a caller that drops it."""
+    100 ms since round 5 (teleop loops leave 5-33 ms between frames: profiles/r05/teleop/); close() ends it at
+    once; one runner serves both retarget() (body_rot) and a caller that drops it."""
     import time
 
     from retarget.retarget_solver import VtrdynFullBodyPosRetargeter
     from robot_kinematics_model import RobotZeroPose
     g = golden("full_body_pos_precise")
     zf, zh = RobotZeroPose.from_asset("vtrdyn_full"), RobotZeroPose.from_asset("hu_v5")
-    for server, idle_ms, bound_s in ((False, 200, 0.05), (True, 10, 0.15), (None, None, 0.05)):
+    for server, idle_ms, bound_s in ((False, 200, 0.05), (True, 10, 0.15), (None, None, 0.25)):
         kw = {} if server is None else dict(frame_server=server, idle_ms=idle_ms)   # None: the defaults
         hu = VtrdynFullBodyPosRetargeter(zf, zh, precise_gripper=True, **kw)
         worst = 0.0

@@ -5,7 +5,9 @@
 //  [3] qexp_component_tab (exp-map angle table) == qexp_component for every f32 w bit pattern;
 //  [4] sqrt_clamp_rcp (one v_rsq_f64) == clamp(cr_sqrt) + rcp64, bitwise, for every f32 s;
 //  [5] mulr_k (K quotients by one denominator behind one subnormal branch) == K IEEE f32 divisions, on 2^30
-//      hashed (a0, a1, a2, n) with a quarter of the groups steered to a subnormal first quotient.
+//      hashed (a0, a1, a2, n) with a quarter of the groups steered to a subnormal first quotient;
+//  [6] cr_acos (f64 asin kernel + rounding test, libm fallback) == (float)acos((double)x) for EVERY f32 x.
+// Since round 5 [1] checks the f32-arithmetic cr_sqrt (v_sqrt_f32 + two residual fmas).
 // Built with the library's flags by __graft_entry__.build(); run by tests/test_gpu_parity.py.
 #include <hip/hip_runtime.h>
 #include <cstdio>
@@ -20,7 +22,7 @@ __device__ __forceinline__ bool same(float a, float b)
     return __float_as_uint(a) == __float_as_uint(b) || (a != a && b != b);
 }
 
-__device__ unsigned long long g_done[6];   // threads that ran each check (a failed launch must not read as a pass)
+__device__ unsigned long long g_done[7];   // threads that ran each check (a failed launch must not read as a pass)
 __device__ __forceinline__ void ran(int k)
 {
     if (threadIdx.x == 0) atomicAdd(&g_done[k], (unsigned long long)blockDim.x);
@@ -141,11 +143,24 @@ __global__ void k_divk(uint64_t base, unsigned long long *bad)
     if (!same(q[0], a[0] / n) || !same(q[1], a[1] / n) || !same(q[2], a[2] / n)) atomicAdd(bad + 5, 1ull);
 }
 
+// [6] cr_acos for every f32 bit pattern; g_acos_slow counts the |x| < 1 inputs the fast path hands to libm
+__device__ unsigned long long g_acos_slow;
+__global__ void k_acos(uint64_t base, unsigned long long *bad)
+{
+    const uint32_t u = (uint32_t)(base + (uint64_t)blockIdx.x * blockDim.x + threadIdx.x);
+    const float x = __uint_as_float(u);
+    ran(6);
+    bool ok;
+    (void)acos_fast(x, ok);
+    if (!ok && __builtin_fabsf(x) < 1.0f) atomicAdd(&g_acos_slow, 1ull);
+    if (!same(cr_acos(x), acos_libm(x))) atomicAdd(bad + 6, 1ull);
+}
+
 int main()
 {
     unsigned long long *bad;
-    (void)hipMalloc(&bad, 6 * sizeof(unsigned long long));
-    (void)hipMemset(bad, 0, 6 * sizeof(unsigned long long));
+    (void)hipMalloc(&bad, 7 * sizeof(unsigned long long));
+    (void)hipMemset(bad, 0, 7 * sizeof(unsigned long long));
     uint32_t *tab;
     (void)hipMalloc(&tab, kAngTabWords * sizeof(uint32_t));
     hipLaunchKernelGGL(k_build_tab, dim3((kAngTabWords + 255u) / 256u), dim3(256), 0, 0, tab);
@@ -155,6 +170,7 @@ int main()
         hipLaunchKernelGGL(k_div, dim3((unsigned)(chunk / 256)), dim3(256), 0, 0, base, bad);
         hipLaunchKernelGGL(k_exptab, dim3((unsigned)(chunk / 256)), dim3(256), 0, 0, base, tab, bad);
         hipLaunchKernelGGL(k_normrcp, dim3((unsigned)(chunk / 256)), dim3(256), 0, 0, base, bad);
+        hipLaunchKernelGGL(k_acos, dim3((unsigned)(chunk / 256)), dim3(256), 0, 0, base, bad);
     }
     hipLaunchKernelGGL(k_divk, dim3((unsigned)(chunk / 256)), dim3(256), 0, 0, 0ull, bad);
     hipLaunchKernelGGL(k_div_special, dim3(64), dim3(64), 0, 0, bad);
@@ -162,11 +178,12 @@ int main()
         printf("launch/run failure: %s\n", hipGetErrorString(hipGetLastError()));
         return 2;
     }
-    unsigned long long h[6] = {0, 0, 0, 0, 0, 0}, d[6] = {0, 0, 0, 0, 0, 0};
+    unsigned long long h[7] = {0, 0, 0, 0, 0, 0, 0}, d[7] = {0, 0, 0, 0, 0, 0, 0}, slow = 0;
     (void)hipMemcpy(h, bad, sizeof h, hipMemcpyDeviceToHost);
     (void)hipMemcpyFromSymbol(d, HIP_SYMBOL(g_done), sizeof d);
-    const unsigned long long want[6] = {1ull << 32, 1ull << 32, 4096ull, 1ull << 32, 1ull << 32, 1ull << 30};
-    for (int k = 0; k < 6; ++k)
+    (void)hipMemcpyFromSymbol(&slow, HIP_SYMBOL(g_acos_slow), sizeof slow);
+    const unsigned long long want[7] = {1ull << 32, 1ull << 32, 4096ull, 1ull << 32, 1ull << 32, 1ull << 30, 1ull << 32};
+    for (int k = 0; k < 7; ++k)
         if (d[k] != want[k]) {
             printf("check %d covered %llu of %llu inputs\n", k, d[k], want[k]);
             return 2;
@@ -177,10 +194,12 @@ int main()
     printf("[3] exp-map angle table: 4294967296 w bit patterns, %llu mismatches\n", h[3]);
     printf("[4] sqrt_clamp_rcp: 4294967296 inputs x 2 clamps, %llu mismatches\n", h[4]);
     printf("[5] grouped mulr_k<3>: 1073741824 groups, %llu mismatches\n", h[5]);
+    printf("[6] cr_acos: 4294967296 inputs, %llu mismatches (libm fallback on %llu of the 2130706430 |x| < 1)\n",
+           h[6], slow);
     uint32_t f[16];
     (void)hipMemcpyFromSymbol(f, HIP_SYMBOL(g_first), sizeof f);
     for (unsigned k = 0; k < (h[1] < 4 ? h[1] : 4); ++k)
         printf("  a=%08x n=%08x fast=%08x ieee=%08x\n", f[4 * k], f[4 * k + 1], f[4 * k + 2], f[4 * k + 3]);
     (void)hipFree(tab);
-    return (h[0] || h[1] || h[2] || h[3] || h[4] || h[5]) ? 1 : 0;
+    return (h[0] || h[1] || h[2] || h[3] || h[4] || h[5] || h[6]) ? 1 : 0;
 }

@@ -104,6 +104,43 @@ def latency():
     return out
 
 
+def teleop_gaps():
+    """The teleop loop's per-frame call with the loop's own work between frames: the reference's
+    sim_full_body_teleop.py:91-126 follows every retarget with a MuJoCo step, a viewer render and a recorder call,
+    so frames arrive every few to tens of ms.  For each gap (a sleep between calls, excluded from the timing) the
+    drop-in retarget() is timed with the resident frame server at several idle_ms (the server ends after idle_ms
+    without a frame and is relaunched by the next one) and with the one-launch FrameGraph (frame_server=False)."""
+    sys.path.insert(0, os.path.join(REPO, "humanoid-real-time-retarget_amd"))
+    from retarget.retarget_solver import VtrdynFullBodyPosRetargeter
+    from robot_kinematics_model import RobotZeroPose
+    g = np.load(os.path.join(G, "full_body_pos_precise.npz"))
+    fb, fl, fr = (torch.from_numpy(np.ascontiguousarray(g[k][0])) for k in ("body", "lh", "rh"))
+    configs = [("frame_server_idle5", True, 5), ("frame_server_idle50", True, 50), ("frame_server_idle200", True, 200),
+               ("frame_graph", False, 5)]
+    out = {}
+    n = int(os.environ.get("RTG_GAP_FRAMES", "60"))
+    for gap_ms in (0, 2, 5, 10, 20, 33):
+        row = {}
+        for name, server, idle in configs:
+            hu = VtrdynFullBodyPosRetargeter(RobotZeroPose.from_asset("vtrdyn_full"), RobotZeroPose.from_asset("hu_v5"),
+                                             precise_gripper=True, frame_server=server, idle_ms=idle)
+            for _ in range(5):
+                hu.retarget(fb, fl, fr)
+            ts = []
+            for _ in range(n):
+                if gap_ms:
+                    time.sleep(gap_ms * 1e-3)
+                t0 = time.perf_counter()
+                hu.retarget(fb, fl, fr)
+                ts.append(time.perf_counter() - t0)
+            hu.close()
+            row[name] = {"median_us": round(float(np.median(ts) * 1e6), 1),
+                         "p90_us": round(float(np.quantile(ts, 0.9) * 1e6), 1)}
+        out[f"gap_{gap_ms}ms"] = row
+        print(gap_ms, row, flush=True)
+    return out
+
+
 def fk():
     res = {}
     B = 262144
