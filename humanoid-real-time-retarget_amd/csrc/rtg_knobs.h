@@ -44,6 +44,9 @@
 #ifndef RTG_EXP_ACOS_LIBM
 #define RTG_EXP_ACOS_LIBM 0   // A/B knob (same values): cr_acos as round 4's libm f64 acos
 #endif
+#ifndef RTG_EXP_EULER_SCIPY
+#define RTG_EXP_EULER_SCIPY 0   // A/B knob (same values): the 'XYZ' split through the scipy restatement for every frame
+#endif
 #ifndef RTG_EXP_STUB_SVD
 #define RTG_EXP_STUB_SVD 0   // measurement knob (tools/build_variants.sh): R = identity-ish, wrong answers
 #endif

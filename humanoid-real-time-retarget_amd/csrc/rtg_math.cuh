@@ -1273,6 +1273,68 @@ RTG_DEV Q elementary_quat(int axis, double angle)
     return Q{axis == 0 ? s : 0.0f, axis == 1 ? s : 0.0f, axis == 2 ? s : 0.0f, c};
 }
 
+// ---- the 'XYZ' split of the solvers without atan2 (round 5)
+// scipy's as_euler('XYZ') (intrinsic; scipy_as_euler with i = 2, j = 1, k = 0, sign -1) of q = (x, y, z, w) gives,
+// with a = w - y, b = z - x, c = w + y, d = -(x + z) and hs = atan2(b, a), hd = atan2(d, c):
+//   X: -(hs + hd)   Y: 2 atan2(|c + id|, |a + ib|) - pi/2   Z: hs - hd,   each wrapped into [-pi, pi]
+// and each elementary quaternion is (sin A/2, cos A/2).  Every A is the principal argument of a complex number whose
+// half angle needs no trigonometry:  e^{-i(hs + hd)} ~ conj((a + ib)(c + id)) = (ac - bd) - i(ad + bc);
+// e^{i(hs - hd)} ~ (a + ib)(c - id) = (ac + bd) + i(bc - ad);  and e^{i A_Y} ~ m + 2i(yw + xz) with
+// m = |a + ib| |c + id| (the modulus of the other two; n2 = |q|^2 is this one's).  For z = re + i im of modulus M,
+// u = M + |re| (no cancellation) and t = 1 / sqrt(2 M u):  re >= 0: (sin, cos)(A/2) = (im t, u t);
+// re < 0: (sign(im) u t, |im| t).  The products of the exact f64 differences a..d are single-rounded (fma), so every
+// output is within 2^-48 of its value; the reference's own f64 pipeline (normalise, hypot, atan2, the angle sums,
+// the wrap, sin / cos) is within ~2^-50 absolute.  An output is accepted when its f32 rounding is the same at
+// +-2^-47 (absolute); otherwise -- and for n2 not > 0 (scipy refuses), NaN / inf, the gimbal cases (m < 1e-6 n2:
+// scipy's 1e-7 tests), the wrap boundary (re < 0 with |im| < 2^-30 M) and im == 0 -- the scipy restatement below runs
+// (quat_in_xyz_axis).  tools/check_fastmath.hip [7] compares the two on 2^30 quaternions.
+RTG_DEV double rsq_nr(double v)   // 1 / sqrt(v), v > 0 finite: v_rsq_f64 (2^-23) and two Newton steps
+{
+    double r = __builtin_amdgcn_rsq(v);
+    const double h = 0.5 * v;
+    r = r * __builtin_fma(-h * r, r, 1.5);
+    r = r * __builtin_fma(-h * r, r, 1.5);
+    return r;
+}
+RTG_DEV bool f32_round_abs_safe(double y, double E, float &out)   // every value within E of y rounds alike
+{
+    out = (float)y;
+    return (float)(y - E) == (float)(y + E);
+}
+// (sin, cos) of half the principal argument of re + i im (modulus M > 0); false when the rounding test or the wrap
+// boundary declines
+RTG_DEV bool half_arg(double re, double im, double M, float &s, float &c)
+{
+    const double u = M + __builtin_fabs(re);
+    const double t = rsq_nr(2.0 * M * u);
+    const double P = u * t, Qv = im * t;
+    const bool pos = re >= 0.0;
+    const double sv = pos ? Qv : __builtin_copysign(P, im), cv = pos ? P : __builtin_fabs(Qv);
+    const double E = 0x1p-47;
+    bool ok = f32_round_abs_safe(sv, E, s);
+    ok = f32_round_abs_safe(cv, E, c) && ok;
+    return ok && im != 0.0 && (pos || __builtin_fabs(im) >= 0x1p-30 * M);
+}
+RTG_DEV bool quat_in_xyz_fast(Q qf, Q out[3])
+{
+    const double X = qf.x, Y = qf.y, Z = qf.z, W = qf.w;
+    const double a = W - Y, b = Z - X, c = W + Y, d = -(X + Z);   // exact: f32 operands
+    const double n2 = __builtin_fma(W, W, __builtin_fma(Z, Z, __builtin_fma(Y, Y, X * X)));
+    const double rab2 = __builtin_fma(b, b, a * a), rcd2 = __builtin_fma(d, d, c * c);
+    const double m2 = rab2 * rcd2;
+    const double m = m2 * rsq_nr(m2);
+    const double bd = b * d, ad = a * d, bc = b * c;
+    float sx, cx, sy, cy, sz, cz;
+    bool ok = n2 > 0.0 && n2 < 0x1p1000 && m >= 1e-6 * n2;
+    ok = half_arg(__builtin_fma(a, c, -bd), -__builtin_fma(a, d, bc), m, sx, cx) && ok;
+    ok = half_arg(m, 2.0 * __builtin_fma(Y, W, X * Z), n2, sy, cy) && ok;
+    ok = half_arg(__builtin_fma(a, c, bd), __builtin_fma(b, c, -ad), m, sz, cz) && ok;
+    out[0] = Q{sx, 0.0f, 0.0f, cx};
+    out[1] = Q{0.0f, sy, 0.0f, cy};
+    out[2] = Q{0.0f, 0.0f, sz, cz};
+    return ok;
+}
+
 // quat_in_xyz_axis (transform3d.py:52-59); true where the reference raises (scipy_as_euler)
 RTG_DEV bool quat_in_xyz_axis(Q q, int s0, int s1, int s2, bool extrinsic, Q out[3])
 {
@@ -1281,6 +1343,17 @@ RTG_DEV bool quat_in_xyz_axis(Q q, int s0, int s1, int s2, bool extrinsic, Q out
     out[0] = elementary_quat(s0, ang[0]);
     out[1] = elementary_quat(s1, ang[1]);
     out[2] = elementary_quat(s2, ang[2]);
+    return refused;
+}
+// quat_in_xyz_axis(q, 'XYZ') as the solvers call it (full_body_pos_retargeter.py:142/165, full_body_retargeter.py
+// :121/138): the atan2-free form above, the scipy restatement where it declines.  Same values (check [7]).
+RTG_DEV bool quat_in_xyz_intrinsic(Q q, Q out[3])
+{
+#if RTG_EXP_EULER_SCIPY   // A/B knob (same values): the scipy restatement for every frame (round 4)
+    return quat_in_xyz_axis(q, 0, 1, 2, false, out);
+#endif
+    bool refused = false;
+    if (__builtin_expect(!quat_in_xyz_fast(q, out), 0)) refused = quat_in_xyz_axis(q, 0, 1, 2, false, out);
     return refused;
 }
 

@@ -151,7 +151,7 @@ template <int L0>
 RTG_DEV bool emit_euler_xyz(const Emit &E, Q local)
 {
     Q eul[3];
-    const bool refused = quat_in_xyz_axis(local, 0, 1, 2, false, eul);
+    const bool refused = quat_in_xyz_intrinsic(local, eul);
     E.link<L0>(eul[0]);
     E.link<L0 + 1>(eul[1]);
     E.link<L0 + 2>(eul[2]);

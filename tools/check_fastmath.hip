@@ -6,7 +6,10 @@
 //  [4] sqrt_clamp_rcp (one v_rsq_f64) == clamp(cr_sqrt) + rcp64, bitwise, for every f32 s;
 //  [5] mulr_k (K quotients by one denominator behind one subnormal branch) == K IEEE f32 divisions, on 2^30
 //      hashed (a0, a1, a2, n) with a quarter of the groups steered to a subnormal first quotient;
-//  [6] cr_acos (f64 asin kernel + rounding test, libm fallback) == (float)acos((double)x) for EVERY f32 x.
+//  [6] cr_acos (f64 asin kernel + rounding test, libm fallback) == (float)acos((double)x) for EVERY f32 x;
+//  [7] quat_in_xyz_intrinsic (atan2-free 'XYZ' split, scipy fallback) == quat_in_xyz_axis(q, 'XYZ'), outputs and
+//      refusal, on 2^30 hashed quaternions from eight families (unnormalised, unit, near gimbal lock, exact zero
+//      components, tiny / huge scales, raw bit patterns, near the +-pi wrap, tiny angles).
 // Since round 5 [1] checks the f32-arithmetic cr_sqrt (v_sqrt_f32 + two residual fmas).
 // Built with the library's flags by __graft_entry__.build(); run by tests/test_gpu_parity.py.
 #include <hip/hip_runtime.h>
@@ -22,7 +25,7 @@ __device__ __forceinline__ bool same(float a, float b)
     return __float_as_uint(a) == __float_as_uint(b) || (a != a && b != b);
 }
 
-__device__ unsigned long long g_done[7];   // threads that ran each check (a failed launch must not read as a pass)
+__device__ unsigned long long g_done[8];   // threads that ran each check (a failed launch must not read as a pass)
 __device__ __forceinline__ void ran(int k)
 {
     if (threadIdx.x == 0) atomicAdd(&g_done[k], (unsigned long long)blockDim.x);
@@ -156,11 +159,58 @@ __global__ void k_acos(uint64_t base, unsigned long long *bad)
     if (!same(cr_acos(x), acos_libm(x))) atomicAdd(bad + 6, 1ull);
 }
 
+// [7] the 'XYZ' split, fast form vs scipy restatement; g_xyz_slow counts the quaternions the fast form declines
+__device__ unsigned long long g_xyz_slow;
+__device__ __forceinline__ float hf(uint64_t h, int k) { return (float)((h >> (11 * k)) & 0x3FFFFFu) * 0x1p-21f - 1.0f; }
+__global__ void k_xyz(uint64_t base, unsigned long long *bad)
+{
+    const uint64_t i = base + (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const uint64_t h = mix(i), h2 = mix(i ^ 0x5bd1e995u);
+    ran(7);
+    const int fam = (int)(h2 & 7u);
+    Q q{hf(h, 0), hf(h, 1), hf(h, 2), hf(h, 3)};
+    if (fam == 1 || fam >= 6) q = qnormalize(q);
+    if (fam == 2) {   // Y near +-90 degrees: x, z tiny against y, w (or an exact gimbal)
+        const float e = ldexpf(hf(h2, 1), -(int)((h2 >> 8) % 40u));
+        q = Q{e * hf(h2, 2), 0.7071068f + 0.1f * hf(h2, 3) * e, e * hf(h2, 4), 0.7071068f};
+    } else if (fam == 3) {   // exact zeros
+        const uint32_t mz = (uint32_t)(h2 >> 8) & 15u;
+        q = Q{(mz & 1) ? 0.0f : q.x, (mz & 2) ? 0.0f : q.y, (mz & 4) ? -0.0f : q.z, (mz & 8) ? 0.0f : q.w};
+    } else if (fam == 4) {
+        const float sc = (h2 >> 8) & 1 ? 1e-19f : 1e19f;
+        q = Q{q.x * sc, q.y * sc, q.z * sc, q.w * sc};
+    } else if (fam == 5) {
+        q = Q{__uint_as_float((uint32_t)h), __uint_as_float((uint32_t)(h >> 32)), __uint_as_float((uint32_t)h2),
+              __uint_as_float((uint32_t)(h2 >> 32))};
+    } else if (fam == 6) {   // X / Z arguments near +-pi: w and y small against x, z
+        const float e = ldexpf(1.0f, -(int)((h2 >> 8) % 30u));
+        q = Q{q.x, q.y * e, q.z, q.w * e};
+    } else if (fam == 7) {   // small rotations
+        const float e = ldexpf(1.0f, -(int)((h2 >> 8) % 26u));
+        q = Q{q.x * e, q.y * e, q.z * e, 1.0f};
+    }
+    Q f[3], r[3];
+    const bool okf = quat_in_xyz_fast(q, f);
+    if (!okf) atomicAdd(&g_xyz_slow, 1ull);
+    const bool rf = quat_in_xyz_intrinsic(q, f);
+    const bool rr = quat_in_xyz_axis(q, 0, 1, 2, false, r);
+    bool eq = rf == rr;
+    for (int k = 0; k < 3; ++k)
+        eq = eq && same(f[k].x, r[k].x) && same(f[k].y, r[k].y) && same(f[k].z, r[k].z) && same(f[k].w, r[k].w);
+    if (!eq) {
+        const unsigned long long n = atomicAdd(bad + 7, 1ull);
+        if (n < 4) {
+            g_first[8 + 2 * n] = __float_as_uint(q.x) ^ __float_as_uint(q.w);
+            g_first[9 + 2 * n] = (uint32_t)i;
+        }
+    }
+}
+
 int main()
 {
     unsigned long long *bad;
-    (void)hipMalloc(&bad, 7 * sizeof(unsigned long long));
-    (void)hipMemset(bad, 0, 7 * sizeof(unsigned long long));
+    (void)hipMalloc(&bad, 8 * sizeof(unsigned long long));
+    (void)hipMemset(bad, 0, 8 * sizeof(unsigned long long));
     uint32_t *tab;
     (void)hipMalloc(&tab, kAngTabWords * sizeof(uint32_t));
     hipLaunchKernelGGL(k_build_tab, dim3((kAngTabWords + 255u) / 256u), dim3(256), 0, 0, tab);
@@ -173,17 +223,20 @@ int main()
         hipLaunchKernelGGL(k_acos, dim3((unsigned)(chunk / 256)), dim3(256), 0, 0, base, bad);
     }
     hipLaunchKernelGGL(k_divk, dim3((unsigned)(chunk / 256)), dim3(256), 0, 0, 0ull, bad);
+    hipLaunchKernelGGL(k_xyz, dim3((unsigned)(chunk / 256)), dim3(256), 0, 0, 0ull, bad);
     hipLaunchKernelGGL(k_div_special, dim3(64), dim3(64), 0, 0, bad);
     if (hipDeviceSynchronize() != hipSuccess || hipGetLastError() != hipSuccess) {
         printf("launch/run failure: %s\n", hipGetErrorString(hipGetLastError()));
         return 2;
     }
-    unsigned long long h[7] = {0, 0, 0, 0, 0, 0, 0}, d[7] = {0, 0, 0, 0, 0, 0, 0}, slow = 0;
+    unsigned long long h[8] = {0, 0, 0, 0, 0, 0, 0, 0}, d[8] = {0, 0, 0, 0, 0, 0, 0, 0}, slow = 0, xslow = 0;
     (void)hipMemcpy(h, bad, sizeof h, hipMemcpyDeviceToHost);
     (void)hipMemcpyFromSymbol(d, HIP_SYMBOL(g_done), sizeof d);
     (void)hipMemcpyFromSymbol(&slow, HIP_SYMBOL(g_acos_slow), sizeof slow);
-    const unsigned long long want[7] = {1ull << 32, 1ull << 32, 4096ull, 1ull << 32, 1ull << 32, 1ull << 30, 1ull << 32};
-    for (int k = 0; k < 7; ++k)
+    (void)hipMemcpyFromSymbol(&xslow, HIP_SYMBOL(g_xyz_slow), sizeof xslow);
+    const unsigned long long want[8] = {1ull << 32, 1ull << 32, 4096ull, 1ull << 32, 1ull << 32, 1ull << 30, 1ull << 32,
+                                        1ull << 30};
+    for (int k = 0; k < 8; ++k)
         if (d[k] != want[k]) {
             printf("check %d covered %llu of %llu inputs\n", k, d[k], want[k]);
             return 2;
@@ -196,10 +249,13 @@ int main()
     printf("[5] grouped mulr_k<3>: 1073741824 groups, %llu mismatches\n", h[5]);
     printf("[6] cr_acos: 4294967296 inputs, %llu mismatches (libm fallback on %llu of the 2130706430 |x| < 1)\n",
            h[6], slow);
+    printf("[7] 'XYZ' split, fast vs scipy restatement: 1073741824 quaternions, %llu mismatches (fallback on %llu)\n",
+           h[7], xslow);
     uint32_t f[16];
     (void)hipMemcpyFromSymbol(f, HIP_SYMBOL(g_first), sizeof f);
     for (unsigned k = 0; k < (h[1] < 4 ? h[1] : 4); ++k)
         printf("  a=%08x n=%08x fast=%08x ieee=%08x\n", f[4 * k], f[4 * k + 1], f[4 * k + 2], f[4 * k + 3]);
     (void)hipFree(tab);
-    return (h[0] || h[1] || h[2] || h[3] || h[4] || h[5] || h[6]) ? 1 : 0;
+    for (unsigned k = 0; k < (h[7] < 4 ? h[7] : 4); ++k) printf("  xyz mismatch at i=%u\n", f[9 + 2 * k]);
+    return (h[0] || h[1] || h[2] || h[3] || h[4] || h[5] || h[6] || h[7]) ? 1 : 0;
 }
