@@ -1284,8 +1284,10 @@ RTG_DEV Q elementary_quat(int axis, double angle)
 // u = M + |re| (no cancellation) and t = 1 / sqrt(2 M u):  re >= 0: (sin, cos)(A/2) = (im t, u t);
 // re < 0: (sign(im) u t, |im| t).  The products of the exact f64 differences a..d are single-rounded (fma), so every
 // output is within 2^-48 of its value; the reference's own f64 pipeline (normalise, hypot, atan2, the angle sums,
-// the wrap, sin / cos) is within ~2^-50 absolute.  An output is accepted when its f32 rounding is the same at
-// +-2^-47 (absolute); otherwise -- and for n2 not > 0 (scipy refuses), NaN / inf, the gimbal cases (m < 1e-6 n2:
+// the wrap, sin / cos) is within ~2^-50 (1 + 1/|a + ib| + 1/|c + id|) |q| absolute.  An output is accepted when its
+// f32 rounding is the same at +-2^-49 (1 + ...) -- the first version, with a fixed 2^-47, differed from the
+// restatement on 5,892 of 2^30 near-gimbal quaternions (check [7]); otherwise -- and for n2 not > 0 (scipy
+// refuses), NaN / inf, the gimbal cases (m < 1e-6 n2:
 // scipy's 1e-7 tests), the wrap boundary (re < 0 with |im| < 2^-30 M) and im == 0 -- the scipy restatement below runs
 // (quat_in_xyz_axis).  tools/check_fastmath.hip [7] compares the two on 2^30 quaternions.
 RTG_DEV double rsq_nr(double v)   // 1 / sqrt(v), v > 0 finite: v_rsq_f64 (2^-23) and two Newton steps
@@ -1301,16 +1303,13 @@ RTG_DEV bool f32_round_abs_safe(double y, double E, float &out)   // every value
     out = (float)y;
     return (float)(y - E) == (float)(y + E);
 }
-// (sin, cos) of half the principal argument of re + i im (modulus M > 0); false when the rounding test or the wrap
-// boundary declines
-RTG_DEV bool half_arg(double re, double im, double M, float &s, float &c)
+// (sin, cos) of half the principal argument of re + i im (modulus M > 0), given t = 1 / sqrt(2 M u) with
+// u = M + |re|; false when the rounding test at +-E or the wrap boundary declines
+RTG_DEV bool half_arg(double re, double im, double M, double u, double t, double E, float &s, float &c)
 {
-    const double u = M + __builtin_fabs(re);
-    const double t = rsq_nr(2.0 * M * u);
     const double P = u * t, Qv = im * t;
     const bool pos = re >= 0.0;
     const double sv = pos ? Qv : __builtin_copysign(P, im), cv = pos ? P : __builtin_fabs(Qv);
-    const double E = 0x1p-47;
     bool ok = f32_round_abs_safe(sv, E, s);
     ok = f32_round_abs_safe(cv, E, c) && ok;
     return ok && im != 0.0 && (pos || __builtin_fabs(im) >= 0x1p-30 * M);
@@ -1324,11 +1323,19 @@ RTG_DEV bool quat_in_xyz_fast(Q qf, Q out[3])
     const double m2 = rab2 * rcd2;
     const double m = m2 * rsq_nr(m2);
     const double bd = b * d, ad = a * d, bc = b * c;
+    // Y: re = m, im = 2 (yw + xz), modulus n2
+    const double u1 = n2 + m, t1 = rsq_nr(2.0 * n2 * u1);
+    // The reference's a..d carry ~2^-52 |q| of rounding (its normalised q), which its atan2 of (b, a) / (d, c)
+    // amplifies by |q| / |a + ib| and |q| / |c + id|: near gimbal lock the margin widens with
+    // 1 / |a + ib| + 1 / |c + id| = sqrt(2 n2 u1) / m = 1 / (t1 m)
+    const double E = 0x1p-49 * (1.0 + __builtin_amdgcn_rcp(t1 * m));
     float sx, cx, sy, cy, sz, cz;
     bool ok = n2 > 0.0 && n2 < 0x1p1000 && m >= 1e-6 * n2;
-    ok = half_arg(__builtin_fma(a, c, -bd), -__builtin_fma(a, d, bc), m, sx, cx) && ok;
-    ok = half_arg(m, 2.0 * __builtin_fma(Y, W, X * Z), n2, sy, cy) && ok;
-    ok = half_arg(__builtin_fma(a, c, bd), __builtin_fma(b, c, -ad), m, sz, cz) && ok;
+    ok = half_arg(m, 2.0 * __builtin_fma(Y, W, X * Z), n2, u1, t1, E, sy, cy) && ok;
+    const double re0 = __builtin_fma(a, c, -bd), re2 = __builtin_fma(a, c, bd);
+    const double u0 = m + __builtin_fabs(re0), u2 = m + __builtin_fabs(re2);
+    ok = half_arg(re0, -__builtin_fma(a, d, bc), m, u0, rsq_nr(2.0 * m * u0), E, sx, cx) && ok;
+    ok = half_arg(re2, __builtin_fma(b, c, -ad), m, u2, rsq_nr(2.0 * m * u2), E, sz, cz) && ok;
     out[0] = Q{sx, 0.0f, 0.0f, cx};
     out[1] = Q{0.0f, sy, 0.0f, cy};
     out[2] = Q{0.0f, 0.0f, sz, cz};

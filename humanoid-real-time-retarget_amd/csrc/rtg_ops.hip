@@ -573,61 +573,77 @@ __global__ __launch_bounds__(256) void k_velocity_tile(const float *__restrict__
     // every thread issues the loads of NB elements before it uses any (latency, not bandwidth, bounds a
     // load-then-use loop at this occupancy)
     if (!ANGULAR) {
-        constexpr int NB = 8;    // measured: 16 and 32 slower (profiles/r04/aux/nb_ab.log)
+        // Round 5: a thread owns a run of SEG rows of one channel and loads the run's SEG + 2 raw values (frames
+        // x0 - 1 .. x0 + SEG) all at once -- 64 lanes on consecutive channels read one row's 256 contiguous bytes
+        // per instruction -- then takes the SEG gradients from its own registers (round 4: two global loads per
+        // gradient, 8 gradients at a time, four memory round trips per tile).  Runs that reach a sequence end take
+        // the clamped, one-sided per-element form.
+        constexpr int SEG = 20;
         const float *p = src + seq * L * C;
-        const uint32_t n = nx * (uint32_t)C;
-        RowWalk w(threadIdx.x, (uint32_t)C);
-        for (uint32_t e0 = threadIdx.x; e0 < n; e0 += 256 * NB) {
-            float hi[NB], lo[NB], hf[NB];
-            uint32_t at[NB];
+        const uint32_t nseg = (nx + SEG - 1) / SEG;
+        const uint32_t items = nseg * (uint32_t)C;
+        for (uint32_t it = threadIdx.x; it < items; it += 256u) {
+            const uint32_t sgi = it / (uint32_t)C, ch = it - sgi * (uint32_t)C;
+            const int r0 = (int)sgi * SEG, x0 = t0 - R + r0;
+            const int nr = min(SEG, (int)nx - r0);
+            float *dst = sg + ch * NS + r0;
+            if (x0 >= 1 && x0 + nr <= L - 1) {   // every frame of the run and its neighbours inside the sequence
+                const float *q = p + (int64_t)(x0 - 1) * C + ch;
+                float raw[SEG + 2];
 #pragma unroll
-            for (int k = 0; k < NB; ++k) {
-                const uint32_t e = e0 + 256u * k;
-                const int x = t0 - R + (int)w.rr;
-                const int t = x < 0 ? 0 : (x > L - 1 ? L - 1 : x);
-                const int64_t i = (int64_t)t * C + w.ch;
-                // np.gradient: (p[t+1] - p[t-1]) / 2 inside, one-sided differences / 1 at the ends (x / 2 and
-                // x * 0.5 are the same correctly rounded value)
-                const int64_t ih = t == L - 1 ? i : i + C, il = t == 0 ? i : i - C;
-                hf[k] = (t == 0 || t == L - 1) ? 1.0f : 0.5f;
-                at[k] = w.ch * NS + w.rr;
-                if (e < n) { hi[k] = p[ih]; lo[k] = p[il]; }
-                w.next((uint32_t)C);
+                for (int k = 0; k < SEG + 2; ++k) raw[k] = k < nr + 2 ? q[(int64_t)k * C] : 0.0f;
+                // np.gradient inside the sequence: (p[t+1] - p[t-1]) / 2 (x / 2 == x * 0.5, correctly rounded)
+#pragma unroll
+                for (int j = 0; j < SEG; ++j)
+                    if (j < nr) dst[j] = ((raw[j + 2] - raw[j]) * 0.5f) / dt;
+            } else {
+                for (int j = 0; j < nr; ++j) {
+                    const int x = x0 + j;
+                    const int t = x < 0 ? 0 : (x > L - 1 ? L - 1 : x);
+                    const int64_t i = (int64_t)t * C + ch;
+                    // one-sided differences / 1 at the ends
+                    const int64_t ih = t == L - 1 ? i : i + C, il = t == 0 ? i : i - C;
+                    const float hf = (t == 0 || t == L - 1) ? 1.0f : 0.5f;
+                    dst[j] = ((p[ih] - p[il]) * hf) / dt;
+                }
             }
-#pragma unroll
-            for (int k = 0; k < NB; ++k)
-                if (e0 + 256u * k < n) sg[at[k]] = ((hi[k] - lo[k]) * hf[k]) / dt;
         }
     } else {
-        constexpr int NB = 2;    // measured: 2 > 4 > 8 (78 VGPRs, 6 waves/SIMD at 2)
+        // Round 5, as the linear branch: a thread owns a run of SEGA rows of one joint and loads the run's SEGA + 1
+        // quaternions (frames x0 .. x0 + SEGA) at once; runs that reach a sequence end take the clamped form
+        constexpr int SEGA = 6;
         const int J = vt.J;
         const float *r = src + seq * L * J * 4;
-        const uint32_t n = nx * (uint32_t)J;
-        RowWalk w(threadIdx.x, (uint32_t)J);
-        for (uint32_t e0 = threadIdx.x; e0 < n; e0 += 256 * NB) {
-            Q qa[NB], qb[NB];
-            bool last[NB];
-            uint32_t at[NB];
+        const uint32_t nseg = (nx + SEGA - 1) / SEGA;
+        const uint32_t items = nseg * (uint32_t)J;
+        auto put = [&](float *dst, Q d) {   // the three channels of one raw angular velocity
+            const Q aa = qangle_axis_abs(d);
+            dst[0] = (aa.y * aa.x) / dt;
+            dst[NS] = (aa.z * aa.x) / dt;
+            dst[2 * NS] = (aa.w * aa.x) / dt;
+        };
+        for (uint32_t it = threadIdx.x; it < items; it += 256u) {
+            const uint32_t sgi = it / (uint32_t)J, jn = it - sgi * (uint32_t)J;
+            const int r0 = (int)sgi * SEGA, x0 = t0 - R + r0;
+            const int nr = min(SEGA, (int)nx - r0);
+            float *dst = sg + 3u * jn * NS + r0;
+            if (x0 >= 0 && x0 + nr < L) {   // every row inside the sequence and before its last frame
+                const float *q = r + 4 * ((int64_t)x0 * J + jn);
+                Q qs[SEGA + 1];
 #pragma unroll
-            for (int k = 0; k < NB; ++k) {
-                const uint32_t e = e0 + 256u * k;
-                const int x = t0 - R + (int)w.rr;
-                const int t = x < 0 ? 0 : (x > L - 1 ? L - 1 : x);
-                const int64_t i = (int64_t)t * J + w.ch;
-                last[k] = t >= L - 1;
-                at[k] = 3u * w.ch * NS + w.rr;
-                if (e < n && !last[k]) { qa[k] = ld4(r + 4 * (i + J)); qb[k] = ld4(r + 4 * i); }
-                w.next((uint32_t)J);
-            }
+                for (int k = 0; k < SEGA + 1; ++k) qs[k] = k <= nr ? ld4(q + 4 * (int64_t)k * J) : qident();
 #pragma unroll
-            for (int k = 0; k < NB; ++k) {
-                if (e0 + 256u * k >= n) continue;
-                Q d = qident();
-                if (!last[k]) d = qmul_norm(qa[k], qconj(qb[k]));
-                const Q aa = qangle_axis_abs(d);
-                sg[at[k]] = (aa.y * aa.x) / dt;
-                sg[at[k] + NS] = (aa.z * aa.x) / dt;
-                sg[at[k] + 2 * NS] = (aa.w * aa.x) / dt;
+                for (int j = 0; j < SEGA; ++j)
+                    if (j < nr) put(dst + j, qmul_norm(qs[j + 1], qconj(qs[j])));
+            } else {
+                for (int j = 0; j < nr; ++j) {
+                    const int x = x0 + j;
+                    const int t = x < 0 ? 0 : (x > L - 1 ? L - 1 : x);
+                    const int64_t i = (int64_t)t * J + jn;
+                    Q d = qident();   // the last frame: identity (no forward neighbour)
+                    if (t < L - 1) d = qmul_norm(ld4(r + 4 * (i + J)), qconj(ld4(r + 4 * i)));
+                    put(dst + j, d);
+                }
             }
         }
     }

@@ -33,14 +33,15 @@ __device__ __forceinline__ V rv(uint32_t i, uint32_t k) { return V{sn(i, k), sn(
 enum {
     F_EMPTY, F_EXP, F_ACOS, F_SINCOS, F_ATAN2, F_NORMANG, F_RADB, F_FAA, F_QNORM, F_ROTMAT, F_KAB3, F_KAB5,
     F_EULER, F_QXYZ, F_SHPR, F_ELPY, F_QROT, F_DIV, F_EXPTAB, F_QMULNORM, F_HANDX, F_SQRTCR, F_SCRCP, F_RCP64,
-    F_COUNT
+    F_QXYZF, F_GESDD3, F_LARTG, F_LASV2, F_LARFG2, F_COUNT
 };
 static const char *kNames[F_COUNT] = {"empty", "qexp_component", "cr_acos", "cr_sincos", "f_atan2f",
                                       "normalize_angle", "radians_between", "qfrom_angle_axis", "qnormalize",
                                       "qfrom_rotmat", "cal_joint_quat<3>", "cal_joint_quat<5>", "scipy_as_euler",
                                       "quat_in_xyz_axis", "shoulder_pr", "elbow_py", "qrotate", "f32 div",
                                       "exp_dof (table)", "qmul_norm", "hand_x_mean", "cr_sqrt", "sqrt_clamp_rcp",
-                                      "rcp64+mulr_q"};
+                                      "rcp64+mulr_q", "quat_in_xyz_intrinsic",
+                                      "la_gesdd3 (5-pt A)", "la_lartg", "la_lasv2", "la_larfg<2>"};
 
 template <int F>
 __global__ __launch_bounds__(256) void kcost(float *out, const uint32_t *__restrict__ tab)
@@ -139,6 +140,37 @@ __global__ __launch_bounds__(256) void kcost(float *out, const uint32_t *__restr
     } else if (F == F_SCRCP) {
         const NormRcp n = sqrt_clamp_rcp(rq(i).w + 1.5f, 1e-9f);
         r = n.n + (float)n.r.r;
+    } else if (F == F_QXYZF) {   // the solvers' 'XYZ' split (round 5: atan2-free, scipy fallback)
+        Q e[3];
+        quat_in_xyz_intrinsic(rq(i), e);
+        r = e[0].x + e[1].y + e[2].z;
+    } else if (F == F_GESDD3) {   // the SVD alone on a wrist-fit-like A (column-major)
+        const Q q0 = rq(i);
+        const V Z[5] = {V{0.1f, 0.02f, 0.03f}, V{0.12f, 0.01f, 0.0f}, V{0.11f, -0.01f, -0.02f},
+                        V{0.1f, -0.03f, -0.03f}, V{0.03f, 0.04f, 0.02f}};
+        float a[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
+        for (int k = 0; k < 5; ++k) {
+            const V v = qrotate(q0, Z[k]);
+            const V m{v.x + 0.002f * sn(i, 20 + k), v.y + 0.002f * sn(i, 30 + k), v.z};
+            a[0] += m.x * Z[k].x; a[3] += m.x * Z[k].y; a[6] += m.x * Z[k].z;
+            a[1] += m.y * Z[k].x; a[4] += m.y * Z[k].y; a[7] += m.y * Z[k].z;
+            a[2] += m.z * Z[k].x; a[5] += m.z * Z[k].y; a[8] += m.z * Z[k].z;
+        }
+        Svd3 z;
+        la_gesdd3(a, z);
+        r = z.u[0] + z.vt[4];
+    } else if (F == F_LARTG) {
+        float c, sv, rr;
+        la_lartg(sn(i, 1), sn(i, 2), c, sv, rr);
+        r = c + sv + rr;
+    } else if (F == F_LASV2) {
+        float a0, a1, a2, a3, a4, a5;
+        la_lasv2(sn(i, 1), sn(i, 2), sn(i, 3), a0, a1, a2, a3, a4, a5);
+        r = a0 + a1 + a2 + a3 + a4 + a5;
+    } else if (F == F_LARFG2) {
+        float al = sn(i, 1), x0 = sn(i, 2), x1 = sn(i, 3);
+        const float tau = la_larfg<2>(al, x0, x1);
+        r = tau + al + x0 + x1;
     } else if (F == F_RCP64) {
         const Q q = rq(i);
         const Q u = mulr_q(q, rcp64(q.w + 2.0f));

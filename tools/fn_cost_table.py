@@ -14,7 +14,8 @@ import sys
 NAMES = ["empty", "qexp_component", "cr_acos", "cr_sincos", "f_atan2f", "normalize_angle", "radians_between",
          "qfrom_angle_axis", "qnormalize", "qfrom_rotmat", "cal_joint_quat<3>", "cal_joint_quat<5>", "scipy_as_euler",
          "quat_in_xyz_axis", "shoulder_pr", "elbow_py", "qrotate", "f32 div", "exp_dof (table)", "qmul_norm",
-         "hand_x_mean", "cr_sqrt", "sqrt_clamp_rcp", "rcp64+mulr_q"]
+         "hand_x_mean", "cr_sqrt", "sqrt_clamp_rcp", "rcp64+mulr_q", "quat_in_xyz_intrinsic",
+         "la_gesdd3 (5-pt A)", "la_lartg", "la_lasv2", "la_larfg<2>"]
 # issue cycles of a wave64 instruction relative to a plain f32 op (f64 add/mul/fma x2, f64
 # transcendentals x8, f32 transcendentals x4)
 WEIGHT = {"SQ_INSTS_VALU_ADD_F64": 1, "SQ_INSTS_VALU_MUL_F64": 1, "SQ_INSTS_VALU_FMA_F64": 1,
@@ -27,7 +28,8 @@ def main(d, out=None):
         for r in csv.DictReader(open(f)):
             m = re.search(r"kcost<(\d+)>", r["Kernel_Name"])
             if m:
-                acc[int(m.group(1))][r["Counter_Name"]][r["Dispatch_Id"]] += float(r["Counter_Value"])
+                # one pass per file: a dispatch id repeats across passes
+                acc[int(m.group(1))][r["Counter_Name"]][(f, r["Dispatch_Id"])] += float(r["Counter_Value"])
     per = {}
     for i, cs in acc.items():
         waves = sum(cs["SQ_WAVES"].values()) / len(cs["SQ_WAVES"])
