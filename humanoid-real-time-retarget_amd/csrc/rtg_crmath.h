@@ -48,12 +48,18 @@ struct SinCos {
     bool s_ok, c_ok;   // false: the caller must use its exact fallback for that value
 };
 
+// Round 5: the test reads the 29 bits f32 rounding drops from y's representation instead of rounding y(1 -+ 2^-44)
+// twice (integer work only): accepted when they are not within 512 f64 ulps of the midpoint 2^28 -- at least the old
+// margin (|y| 2^-44 is 256..512 ulps), so every accepted value is still correctly rounded -- and |y| is in the f32
+// normal range (0 and subnormal results take the exact fallback).
 RTG_HD bool round_ok(double y, float &out)
 {
-    const double e = (y < 0 ? -y : y) * 0x1p-44;
-    const float lo = (float)(y - e), hi = (float)(y + e);
     out = (float)y;
-    return lo == hi;
+    uint64_t b;
+    memcpy(&b, &y, sizeof b);
+    const uint32_t lo = (uint32_t)b & 0x1FFFFFFFu;
+    const uint32_t ex = (uint32_t)(b >> 52) & 0x7FFu;
+    return (uint32_t)(lo - (0x10000000u - 512u)) > 1024u && ex >= 1023u - 126u && ex <= 1023u + 127u;
 }
 
 RTG_HD SinCos crm_sincos(double x)
@@ -93,9 +99,12 @@ RTG_HD SinCos crm_sincos(double x)
     pc = RTG_FMA(z, pc, C2);
     pc = RTG_FMA(z, pc, C1);
     const double cs = RTG_FMA(z * z, pc, RTG_FMA(-0.5, z, 1.0));
+    // quadrant n: sin = (sn, cs, -sn, -cs)[n], cos = (cs, -sn, -cs, sn)[n] -- one swap and two sign flips
     const int n = (int)(int64_t)k & 3;
-    const double vs = (n == 0) ? sn : (n == 1) ? cs : (n == 2) ? -sn : -cs;
-    const double vc = (n == 0) ? cs : (n == 1) ? -sn : (n == 2) ? -cs : sn;
+    const bool swap = (n & 1) != 0;
+    const double sa = swap ? cs : sn, ca = swap ? sn : cs;
+    const double vs = (n & 2) ? -sa : sa;
+    const double vc = ((n + 1) & 2) ? -ca : ca;
     r.s_ok = round_ok(vs, r.s);
     r.c_ok = round_ok(vc, r.c);
     r.s = special ? (float)x0 : r.s;

@@ -373,8 +373,10 @@ __global__ __launch_bounds__(kFkTile) void k_dof_fk(TopoView T, DofView D, const
                         a = (c - a) + a;
                     }
                     const int ax = ld_const(D.axis + (j - 1));
-                    const Q lq = qfrom_angle_axis(a, V{ax == 0 ? 1.0f : 0.0f, ax == 1 ? 1.0f : 0.0f,
-                                                       ax == 2 ? 1.0f : 0.0f});
+                    // the axis is an exact unit vector: its normalisation is the identity (sqrt(1) = 1, 0 and 1
+                    // divided by 1), so the unit-axis form gives quat_from_angle_axis's bits without it (round 5)
+                    const Q lq = qfrom_angle_unit_axis(a, V{ax == 0 ? 1.0f : 0.0f, ax == 1 ? 1.0f : 0.0f,
+                                                            ax == 2 ? 1.0f : 0.0f});
                     if ((sc & 0xFF) != kNoSlot) slot_get(slots, sc & 0xFF, g, t);
                     const V rv = qrotate(g, ld_const(T.local_t + j));
                     ng = qmul_norm(g, lq);

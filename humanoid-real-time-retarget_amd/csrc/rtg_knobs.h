@@ -21,6 +21,12 @@
 #ifndef RTG_EXP_SKIP_SIGNAL
 #define RTG_EXP_SKIP_SIGNAL 0   // measurement knob: block 0's first R10 hand-over is never raised, so its partner wave
 #endif                          // times out (tests the RTG_DEVERR_HANDOVER_TIMEOUT report; wrong answers)
+#ifndef RTG_VEL_SEG
+#define RTG_VEL_SEG 20   // rows per thread in the linear velocity tile's load phase (round 5)
+#endif
+#ifndef RTG_VEL_LDS_MIN
+#define RTG_VEL_LDS_MIN 0   // A/B knob: the velocity tile's LDS request raised to this many bytes (blocks per CU)
+#endif
 // ---- used by rtg_fk.hip
 #ifndef RTG_EXP_FK_COPY
 #define RTG_EXP_FK_COPY 0   // measurement knob: k_fk_stream copies its windows out without the chain (wrong answers)

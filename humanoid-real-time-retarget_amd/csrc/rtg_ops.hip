@@ -578,7 +578,7 @@ __global__ __launch_bounds__(256) void k_velocity_tile(const float *__restrict__
         // per instruction -- then takes the SEG gradients from its own registers (round 4: two global loads per
         // gradient, 8 gradients at a time, four memory round trips per tile).  Runs that reach a sequence end take
         // the clamped, one-sided per-element form.
-        constexpr int SEG = 20;
+        constexpr int SEG = RTG_VEL_SEG;
         const float *p = src + seq * L * C;
         const uint32_t nseg = (nx + SEG - 1) / SEG;
         const uint32_t items = nseg * (uint32_t)C;
@@ -609,41 +609,37 @@ __global__ __launch_bounds__(256) void k_velocity_tile(const float *__restrict__
             }
         }
     } else {
-        // Round 5, as the linear branch: a thread owns a run of SEGA rows of one joint and loads the run's SEGA + 1
-        // quaternions (frames x0 .. x0 + SEGA) at once; runs that reach a sequence end take the clamped form
-        constexpr int SEGA = 6;
+        // measured: NB 2 > 4 > 8 (78 VGPRs, 6 waves/SIMD at 2); round 5's per-thread runs of 6 joint rows (the linear
+        // branch's form) 128-132 vs 124-125 us (86 VGPRs, 5 waves/SIMD; profiles/r05/aux/)
+        constexpr int NB = 2;
         const int J = vt.J;
         const float *r = src + seq * L * J * 4;
-        const uint32_t nseg = (nx + SEGA - 1) / SEGA;
-        const uint32_t items = nseg * (uint32_t)J;
-        auto put = [&](float *dst, Q d) {   // the three channels of one raw angular velocity
-            const Q aa = qangle_axis_abs(d);
-            dst[0] = (aa.y * aa.x) / dt;
-            dst[NS] = (aa.z * aa.x) / dt;
-            dst[2 * NS] = (aa.w * aa.x) / dt;
-        };
-        for (uint32_t it = threadIdx.x; it < items; it += 256u) {
-            const uint32_t sgi = it / (uint32_t)J, jn = it - sgi * (uint32_t)J;
-            const int r0 = (int)sgi * SEGA, x0 = t0 - R + r0;
-            const int nr = min(SEGA, (int)nx - r0);
-            float *dst = sg + 3u * jn * NS + r0;
-            if (x0 >= 0 && x0 + nr < L) {   // every row inside the sequence and before its last frame
-                const float *q = r + 4 * ((int64_t)x0 * J + jn);
-                Q qs[SEGA + 1];
+        const uint32_t n = nx * (uint32_t)J;
+        RowWalk w(threadIdx.x, (uint32_t)J);
+        for (uint32_t e0 = threadIdx.x; e0 < n; e0 += 256 * NB) {
+            Q qa[NB], qb[NB];
+            bool last[NB];
+            uint32_t at[NB];
 #pragma unroll
-                for (int k = 0; k < SEGA + 1; ++k) qs[k] = k <= nr ? ld4(q + 4 * (int64_t)k * J) : qident();
+            for (int k = 0; k < NB; ++k) {
+                const uint32_t e = e0 + 256u * k;
+                const int x = t0 - R + (int)w.rr;
+                const int t = x < 0 ? 0 : (x > L - 1 ? L - 1 : x);
+                const int64_t i = (int64_t)t * J + w.ch;
+                last[k] = t >= L - 1;
+                at[k] = 3u * w.ch * NS + w.rr;
+                if (e < n && !last[k]) { qa[k] = ld4(r + 4 * (i + J)); qb[k] = ld4(r + 4 * i); }
+                w.next((uint32_t)J);
+            }
 #pragma unroll
-                for (int j = 0; j < SEGA; ++j)
-                    if (j < nr) put(dst + j, qmul_norm(qs[j + 1], qconj(qs[j])));
-            } else {
-                for (int j = 0; j < nr; ++j) {
-                    const int x = x0 + j;
-                    const int t = x < 0 ? 0 : (x > L - 1 ? L - 1 : x);
-                    const int64_t i = (int64_t)t * J + jn;
-                    Q d = qident();   // the last frame: identity (no forward neighbour)
-                    if (t < L - 1) d = qmul_norm(ld4(r + 4 * (i + J)), qconj(ld4(r + 4 * i)));
-                    put(dst + j, d);
-                }
+            for (int k = 0; k < NB; ++k) {
+                if (e0 + 256u * k >= n) continue;
+                Q d = qident();
+                if (!last[k]) d = qmul_norm(qa[k], qconj(qb[k]));
+                const Q aa = qangle_axis_abs(d);
+                sg[at[k]] = (aa.y * aa.x) / dt;
+                sg[at[k] + NS] = (aa.z * aa.x) / dt;
+                sg[at[k] + 2 * NS] = (aa.w * aa.x) / dt;
             }
         }
     }
@@ -690,7 +686,8 @@ static hipError_t launch_velocity_tile(const float *src, int64_t nseq, int64_t L
 {
     const uint32_t tiles = (uint32_t)((L + T - 1) / T);
     const int64_t per = ((int64_t)1 << 30) / tiles;   // sequences per launch
-    const size_t lds = (size_t)vel_lds_stride(T, taps.radius) * C * sizeof(float);
+    size_t lds = (size_t)vel_lds_stride(T, taps.radius) * C * sizeof(float);
+    if (RTG_VEL_LDS_MIN > 0 && lds < (size_t)RTG_VEL_LDS_MIN) lds = RTG_VEL_LDS_MIN;   // measurement knob: fewer blocks/CU
     for (int64_t q0 = 0; q0 < nseq; q0 += per) {
         const int64_t nq = nseq - q0 < per ? nseq - q0 : per;
         const VelTile vt{q0, (uint32_t)L, T, tiles, (uint32_t)(nq * tiles), (int32_t)C, (int32_t)J};
@@ -1018,7 +1015,7 @@ extern "C" const char *rtg_build_info(void)
 {
     return "{\"abi\":" RTG_STR(RTG_ABI_VERSION) ",\"arch\":\"gfx950\",\"knobs\":{"
         RTG_KNOB(RTG_SIDES_WAVES) RTG_KNOB(RTG_LATENCY_MAX_B)
-        RTG_KNOB(RTG_EXP_TIMESTAMPS) RTG_KNOB(RTG_EXP_SKIP_SIGNAL) RTG_KNOB(RTG_EXP_STUB_SVD) RTG_KNOB(RTG_EXP_NO_TABLE) RTG_KNOB(RTG_EXP_FK_COPY) RTG_KNOB(RTG_EXP_FK_NOPOS) RTG_KNOB(RTG_EXP_MULR_NOBRANCH) RTG_KNOB(RTG_EXP_LARTG_RCP64) RTG_KNOB(RTG_EXP_SQRT64) RTG_KNOB(RTG_EXP_ACOS_LIBM) RTG_KNOB(RTG_EXP_EULER_SCIPY)
+        RTG_KNOB(RTG_EXP_TIMESTAMPS) RTG_KNOB(RTG_EXP_SKIP_SIGNAL) RTG_KNOB(RTG_EXP_STUB_SVD) RTG_KNOB(RTG_EXP_NO_TABLE) RTG_KNOB(RTG_EXP_FK_COPY) RTG_KNOB(RTG_EXP_FK_NOPOS) RTG_KNOB(RTG_EXP_MULR_NOBRANCH) RTG_KNOB(RTG_EXP_LARTG_RCP64) RTG_KNOB(RTG_EXP_SQRT64) RTG_KNOB(RTG_EXP_ACOS_LIBM) RTG_KNOB(RTG_EXP_EULER_SCIPY) RTG_KNOB(RTG_VEL_SEG) RTG_KNOB(RTG_VEL_LDS_MIN)
         "\"RTG_EXP_HOT_INPUTS\":\"" RTG_STR(RTG_EXP_HOT_INPUTS) "\"},\"wrong_answer_knobs\":"
         RTG_STR(RTG_WRONG_ANSWER_KNOBS) "}";
 }
