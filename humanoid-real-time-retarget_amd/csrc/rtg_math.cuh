@@ -195,12 +195,19 @@ RTG_DEV void mulr_k(const float (&a)[K], const Rcp &r, float (&q)[K])
     }
 #endif
 }
+// the subnormal-quotient path of mulr_q, out of line (registers: see acos_libm_call); returned by value
+__device__ __attribute__((noinline)) Q div_q_call(Q v, float n) { return Q{v.x / n, v.y / n, v.z / n, v.w / n}; }
 RTG_DEV Q mulr_q(Q v, const Rcp &r)
 {
-    const float a[4] = {v.x, v.y, v.z, v.w};
-    float q[4];
-    mulr_k<4>(a, r, q);
-    return Q{q[0], q[1], q[2], q[3]};
+    const double p[4] = {(double)v.x * r.r, (double)v.y * r.r, (double)v.z * r.r, (double)v.w * r.r};
+    bool sub = false;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) sub = sub || (__builtin_fabs(p[i]) < 0x1p-126 && p[i] != 0.0);
+    Q q{(float)p[0], (float)p[1], (float)p[2], (float)p[3]};
+#if !RTG_EXP_MULR_NOBRANCH
+    if (__builtin_expect(sub, 0)) q = div_q_call(v, r.n);   // = mulr_k<4>: every quotient by IEEE division
+#endif
+    return q;
 }
 RTG_DEV V mulr_v(V v, const Rcp &r)
 {
