@@ -814,6 +814,14 @@ template <int L0>
 RTG_DEV bool emit_euler_xyz_lanes(const Emit &E, Q qf)
 {
     const int sub = threadIdx.x & 63;
+    {   // round 5: the atan2-free split (quat_in_xyz_fast, same values) on every lane -- qf is the same on all, so the
+        // branch is uniform; where it declines, the lane-parallel scipy restatement below runs
+        Q eul[3];
+        if (quat_in_xyz_fast(qf, eul)) {   // implies |q| > 0: scipy does not refuse it
+            if (sub < 3) link_rt(E, L0 + sub, sub == 0 ? eul[0] : (sub == 1 ? eul[1] : eul[2]));
+            return false;
+        }
+    }
     // scipy_as_euler(q, 0, 1, 2, intrinsic): i = 2, j = 1, k = 0, not symmetric, sign = (2-1)(1-0)(0-2)/2 = -1
     double q[4] = {(double)qf.x, (double)qf.y, (double)qf.z, (double)qf.w};
     const double nrm = sqrt(q[0] * q[0] + q[1] * q[1] + q[2] * q[2] + q[3] * q[3]);
