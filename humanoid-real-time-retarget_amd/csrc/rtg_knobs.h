@@ -27,6 +27,9 @@
 #ifndef RTG_VEL_LDS_MIN
 #define RTG_VEL_LDS_MIN 0   // A/B knob: the velocity tile's LDS request raised to this many bytes (blocks per CU)
 #endif
+#ifndef RTG_VEL_ANG_PIPE
+#define RTG_VEL_ANG_PIPE 1   // angular velocity tile: next batch's loads issued before this batch's arithmetic
+#endif
 // ---- used by rtg_fk.hip
 #ifndef RTG_EXP_FK_COPY
 #define RTG_EXP_FK_COPY 0   // measurement knob: k_fk_stream copies its windows out without the chain (wrong answers)

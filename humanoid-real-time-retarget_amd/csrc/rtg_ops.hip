@@ -616,10 +616,12 @@ __global__ __launch_bounds__(256) void k_velocity_tile(const float *__restrict__
         const float *r = src + seq * L * J * 4;
         const uint32_t n = nx * (uint32_t)J;
         RowWalk w(threadIdx.x, (uint32_t)J);
-        for (uint32_t e0 = threadIdx.x; e0 < n; e0 += 256 * NB) {
-            Q qa[NB], qb[NB];
-            bool last[NB];
-            uint32_t at[NB];
+        // round 5: software-pipelined -- the next batch's quaternion pairs are loaded before this batch's
+        // arithmetic (RTG_VEL_ANG_PIPE; 0: round 4's load-then-compute batches)
+        Q qa[NB], qb[NB];
+        bool last[NB];
+        uint32_t at[NB];
+        auto fetch = [&](uint32_t e0) {
 #pragma unroll
             for (int k = 0; k < NB; ++k) {
                 const uint32_t e = e0 + 256u * k;
@@ -631,16 +633,30 @@ __global__ __launch_bounds__(256) void k_velocity_tile(const float *__restrict__
                 if (e < n && !last[k]) { qa[k] = ld4(r + 4 * (i + J)); qb[k] = ld4(r + 4 * i); }
                 w.next((uint32_t)J);
             }
+        };
+        if (threadIdx.x < n) fetch(threadIdx.x);
+        for (uint32_t e0 = threadIdx.x; e0 < n; e0 += 256 * NB) {
+            Q ca[NB], cb[NB];
+            bool cl[NB];
+            uint32_t cat[NB];
+#pragma unroll
+            for (int k = 0; k < NB; ++k) { ca[k] = qa[k]; cb[k] = qb[k]; cl[k] = last[k]; cat[k] = at[k]; }
+#if RTG_VEL_ANG_PIPE
+            if (e0 + 256 * NB < n) fetch(e0 + 256 * NB);
+#endif
 #pragma unroll
             for (int k = 0; k < NB; ++k) {
                 if (e0 + 256u * k >= n) continue;
                 Q d = qident();
-                if (!last[k]) d = qmul_norm(qa[k], qconj(qb[k]));
+                if (!cl[k]) d = qmul_norm(ca[k], qconj(cb[k]));
                 const Q aa = qangle_axis_abs(d);
-                sg[at[k]] = (aa.y * aa.x) / dt;
-                sg[at[k] + NS] = (aa.z * aa.x) / dt;
-                sg[at[k] + 2 * NS] = (aa.w * aa.x) / dt;
+                sg[cat[k]] = (aa.y * aa.x) / dt;
+                sg[cat[k] + NS] = (aa.z * aa.x) / dt;
+                sg[cat[k] + 2 * NS] = (aa.w * aa.x) / dt;
             }
+#if !RTG_VEL_ANG_PIPE
+            if (e0 + 256 * NB < n) fetch(e0 + 256 * NB);
+#endif
         }
     }
     __syncthreads();
@@ -1015,7 +1031,7 @@ extern "C" const char *rtg_build_info(void)
 {
     return "{\"abi\":" RTG_STR(RTG_ABI_VERSION) ",\"arch\":\"gfx950\",\"knobs\":{"
         RTG_KNOB(RTG_SIDES_WAVES) RTG_KNOB(RTG_LATENCY_MAX_B)
-        RTG_KNOB(RTG_EXP_TIMESTAMPS) RTG_KNOB(RTG_EXP_SKIP_SIGNAL) RTG_KNOB(RTG_EXP_STUB_SVD) RTG_KNOB(RTG_EXP_NO_TABLE) RTG_KNOB(RTG_EXP_FK_COPY) RTG_KNOB(RTG_EXP_FK_NOPOS) RTG_KNOB(RTG_EXP_MULR_NOBRANCH) RTG_KNOB(RTG_EXP_LARTG_RCP64) RTG_KNOB(RTG_EXP_SQRT64) RTG_KNOB(RTG_EXP_ACOS_LIBM) RTG_KNOB(RTG_EXP_EULER_SCIPY) RTG_KNOB(RTG_VEL_SEG) RTG_KNOB(RTG_VEL_LDS_MIN)
+        RTG_KNOB(RTG_EXP_TIMESTAMPS) RTG_KNOB(RTG_EXP_SKIP_SIGNAL) RTG_KNOB(RTG_EXP_STUB_SVD) RTG_KNOB(RTG_EXP_NO_TABLE) RTG_KNOB(RTG_EXP_FK_COPY) RTG_KNOB(RTG_EXP_FK_NOPOS) RTG_KNOB(RTG_EXP_MULR_NOBRANCH) RTG_KNOB(RTG_EXP_LARTG_RCP64) RTG_KNOB(RTG_EXP_SQRT64) RTG_KNOB(RTG_EXP_ACOS_LIBM) RTG_KNOB(RTG_EXP_EULER_SCIPY) RTG_KNOB(RTG_VEL_SEG) RTG_KNOB(RTG_VEL_LDS_MIN) RTG_KNOB(RTG_VEL_ANG_PIPE)
         "\"RTG_EXP_HOT_INPUTS\":\"" RTG_STR(RTG_EXP_HOT_INPUTS) "\"},\"wrong_answer_knobs\":"
         RTG_STR(RTG_WRONG_ANSWER_KNOBS) "}";
 }
