@@ -28,7 +28,7 @@
 #define RTG_VEL_LDS_MIN 0   // A/B knob: the velocity tile's LDS request raised to this many bytes (blocks per CU)
 #endif
 #ifndef RTG_VEL_ANG_PIPE
-#define RTG_VEL_ANG_PIPE 1   // angular velocity tile: next batch's loads issued before this batch's arithmetic
+#define RTG_VEL_ANG_PIPE 0   // A/B knob: angular velocity tile with the next batch's loads issued before this batch's arithmetic (measured 119-121 vs 116 us: off)
 #endif
 // ---- used by rtg_fk.hip
 #ifndef RTG_EXP_FK_COPY
