@@ -616,8 +616,8 @@ __global__ __launch_bounds__(256) void k_velocity_tile(const float *__restrict__
         const float *r = src + seq * L * J * 4;
         const uint32_t n = nx * (uint32_t)J;
         RowWalk w(threadIdx.x, (uint32_t)J);
-        // round 5: software-pipelined -- the next batch's quaternion pairs are loaded before this batch's
-        // arithmetic (RTG_VEL_ANG_PIPE; 0: round 4's load-then-compute batches)
+        // batches of NB elements: loads, then arithmetic (RTG_VEL_ANG_PIPE=1 issues the next batch's loads before this
+        // batch's arithmetic: measured slower, 119-121 vs 116 us, profiles/r05/aux/angpipe_*)
         Q qa[NB], qb[NB];
         bool last[NB];
         uint32_t at[NB];
