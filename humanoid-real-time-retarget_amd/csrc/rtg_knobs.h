@@ -56,6 +56,9 @@
 #ifndef RTG_EXP_EULER_SCIPY
 #define RTG_EXP_EULER_SCIPY 0   // A/B knob (same values): the 'XYZ' split through the scipy restatement for every frame
 #endif
+#ifndef RTG_EXP_NO_RARE
+#define RTG_EXP_NO_RARE 0   // measurement knob: the rare-case branches of cr_sqrt / cr_acos / cr_sincos / mulr /
+#endif                      // sqrt_clamp_rcp removed (wrong answers on rare inputs): what branch-free code would gain
 #ifndef RTG_EXP_STUB_SVD
 #define RTG_EXP_STUB_SVD 0   // measurement knob (tools/build_variants.sh): R = identity-ish, wrong answers
 #endif

@@ -59,7 +59,7 @@ RTG_DEV float cr_sqrt(float x)
     const float rdn = __builtin_fmaf(-sdn, s, x), rup = __builtin_fmaf(-sup, s, x);
     s = rdn <= 0.0f ? sdn : s;
     s = rup > 0.0f ? sup : s;
-    if (__builtin_expect(!(x >= 0x1p-96f && x <= 3.40282347e38f), 0)) s = cr_sqrt64_call(x);
+    if (!RTG_EXP_NO_RARE && __builtin_expect(!(x >= 0x1p-96f && x <= 3.40282347e38f), 0)) s = cr_sqrt64_call(x);
     return s;
 }
 // Rounding test for an f64 approximation y of a value whose f32 rounding is wanted: true when the bits f32 rounding
@@ -119,7 +119,7 @@ RTG_DEV float cr_acos(float x)
 #endif
     bool ok;
     float r = acos_fast(x, ok);
-    if (__builtin_expect(!ok, 0)) r = acos_libm_call(x);
+    if (!RTG_EXP_NO_RARE && __builtin_expect(!ok, 0)) r = acos_libm_call(x);
     return r;
 }
 RTG_DEV float cr_sin(float x) { return (float)::sin((double)x); }
@@ -135,7 +135,7 @@ RTG_DEV SC cr_sincos(double x)
 {
     const crm::SinCos r = crm::crm_sincos(x);
     SC out{r.s, r.c};
-    if (__builtin_expect(!(r.s_ok && r.c_ok), 0)) {   // one rare-case branch for the pair
+    if (!RTG_EXP_NO_RARE && __builtin_expect(!(r.s_ok && r.c_ok), 0)) {   // one rare-case branch for the pair
         if (!r.s_ok) out.s = sin_libm_call(x);
         if (!r.c_ok) out.c = cos_libm_call(x);
     }
@@ -189,7 +189,7 @@ RTG_DEV void mulr_k(const float (&a)[K], const Rcp &r, float (&q)[K])
         sub = sub || (__builtin_fabs(p) < 0x1p-126 && p != 0.0);
     }
 #if !RTG_EXP_MULR_NOBRANCH
-    if (__builtin_expect(sub, 0)) {
+    if (!RTG_EXP_NO_RARE && __builtin_expect(sub, 0)) {
 #pragma unroll
         for (int i = 0; i < K; ++i) q[i] = a[i] / r.n;
     }
@@ -205,7 +205,7 @@ RTG_DEV Q mulr_q(Q v, const Rcp &r)
     for (int i = 0; i < 4; ++i) sub = sub || (__builtin_fabs(p[i]) < 0x1p-126 && p[i] != 0.0);
     Q q{(float)p[0], (float)p[1], (float)p[2], (float)p[3]};
 #if !RTG_EXP_MULR_NOBRANCH
-    if (__builtin_expect(sub, 0)) q = div_q_call(v, r.n);   // = mulr_k<4>: every quotient by IEEE division
+    if (!RTG_EXP_NO_RARE && __builtin_expect(sub, 0)) q = div_q_call(v, r.n);   // = mulr_k<4>: every quotient by IEEE division
 #endif
     return q;
 }
@@ -247,7 +247,7 @@ RTG_DEV NormRcp sqrt_clamp_rcp(float s, float lo)
     const double r1 = __builtin_fma(r0, e0, r0);
     const double e1 = __builtin_fma(-dn, r1, 1.0);
     NormRcp out{n, Rcp{__builtin_fma(r1, e1, r1), n}};
-    if (__builtin_expect(!(d > 0.0 && d < __builtin_inf() && n >= lo), 0)) {
+    if (!RTG_EXP_NO_RARE && __builtin_expect(!(d > 0.0 && d < __builtin_inf() && n >= lo), 0)) {
         const float nc = clamp_lo(cr_sqrt(s), lo);
         out = NormRcp{nc, rcp64(nc)};
     }
