@@ -59,7 +59,7 @@ RTG_HD bool round_ok(double y, float &out)
     memcpy(&b, &y, sizeof b);
     const uint32_t lo = (uint32_t)b & 0x1FFFFFFFu;
     const uint32_t ex = (uint32_t)(b >> 52) & 0x7FFu;
-    return (uint32_t)(lo - (0x10000000u - 512u)) > 1024u && ex >= 1023u - 126u && ex <= 1023u + 127u;
+    return ((uint32_t)(lo - (0x10000000u - 512u)) > 1024u) & (ex >= 1023u - 126u) & (ex <= 1023u + 127u);
 }
 
 RTG_HD SinCos crm_sincos(double x)
@@ -68,7 +68,7 @@ RTG_HD SinCos crm_sincos(double x)
     const double ax0 = x < 0 ? -x : x;
     // NaN / inf / huge: fallback; +-0: exact.  Selected at the end (no branch): the reduction below runs on a finite
     // stand-in for those x and its values are discarded.
-    const bool special = !(ax0 <= 0x1p17) || x == 0.0;
+    const bool special = !(ax0 <= 0x1p17) | (x == 0.0);
     const double x0 = x;
     x = special ? 0.5 : x;
     // pi/2 = P1 + P2 + P3 + P3T (fdlibm pio2_1, pio2_2, pio2_3: 33 significant bits each)
@@ -153,7 +153,7 @@ RTG_HD float crm_atanf_pos(float t)
 RTG_HD bool crm_atan2f_regular(float y, float x)
 {
     const int32_t hx = fbits(x), ix = hx & 0x7fffffff, iy = fbits(y) & 0x7fffffff;
-    return ix != 0 && iy != 0 && ix < 0x7f800000 && iy < 0x7f800000 && hx != 0x3f800000;
+    return (ix != 0) & (iy != 0) & (ix < 0x7f800000) & (iy < 0x7f800000) & (hx != 0x3f800000);
 }
 
 // e_atan2f.c, regular case only (see crm_atan2f_regular)

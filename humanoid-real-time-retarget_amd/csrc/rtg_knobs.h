@@ -9,6 +9,9 @@
 #ifndef RTG_SIDES_WAVES
 #define RTG_SIDES_WAVES 1   // min waves per SIMD for the side kernel (1: the compiler picks; measured best)
 #endif
+#ifndef RTG_QUAD_MAX_B
+#define RTG_QUAD_MAX_B 8192   // 2 <= B <= this: k_fbp_quad (16 frames per block, a frame's sub-steps on a lane quad)
+#endif
 #ifndef RTG_LATENCY_MAX_B
 #define RTG_LATENCY_MAX_B 49152   // 2 <= B <= this: k_fbp_latency5 (swept: faster up to 49152, slower at 65536)
 #endif
@@ -50,15 +53,21 @@
 #ifndef RTG_EXP_SQRT64
 #define RTG_EXP_SQRT64 0   // A/B knob (same values): cr_sqrt as round 4's v_sqrt_f64 + Newton
 #endif
+#ifndef RTG_EXP_SQRT_CALL
+#define RTG_EXP_SQRT_CALL 0   // A/B knob (same values): cr_sqrt's x < 2^-96 / inf / NaN behind a call (round 5's first form)
+#endif
 #ifndef RTG_EXP_ACOS_LIBM
 #define RTG_EXP_ACOS_LIBM 0   // A/B knob (same values): cr_acos as round 4's libm f64 acos
 #endif
 #ifndef RTG_EXP_EULER_SCIPY
 #define RTG_EXP_EULER_SCIPY 0   // A/B knob (same values): the 'XYZ' split through the scipy restatement for every frame
 #endif
+#ifndef RTG_VEL_IEEE_DIV
+#define RTG_VEL_IEEE_DIV 0   // A/B knob (same values): the velocity tiles' quotients by dt as IEEE divisions (round 4)
+#endif
 #ifndef RTG_EXP_NO_RARE
-#define RTG_EXP_NO_RARE 0   // measurement knob: the rare-case branches of cr_sqrt / cr_acos / cr_sincos / mulr /
-#endif                      // sqrt_clamp_rcp removed (wrong answers on rare inputs): what branch-free code would gain
+#define RTG_EXP_NO_RARE 0   // measurement knob, a bit mask: the rare-case branches of cr_sqrt (1) / cr_acos (2) /
+#endif                      // cr_sincos (4) / mulr (8) / sqrt_clamp_rcp (16) removed (wrong answers on rare inputs)
 #ifndef RTG_EXP_STUB_SVD
 #define RTG_EXP_STUB_SVD 0   // measurement knob (tools/build_variants.sh): R = identity-ish, wrong answers
 #endif

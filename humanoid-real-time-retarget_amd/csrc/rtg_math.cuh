@@ -45,7 +45,9 @@ RTG_DEV float cr_sqrt64(float x)
 // Correctly rounded f32 sqrt in f32 arithmetic (round 5): v_sqrt_f32 is within 1 ulp for x >= 2^-96, and of the
 // candidates s - ulp, s, s + ulp the signs of the exact residuals x - (s - ulp) s and x - (s + ulp) s (one fma each)
 // pick the correctly rounded one -- the sequence LLVM emits for a correctly rounded f32 sqrt, without its denormal
-// scaling.  x below 2^-96 (0, denormals, negatives), inf and NaN take cr_sqrt64 behind one rare-case branch.  No f64
+// scaling.  +-0 comes out of the same sequence exactly (v_sqrt_f32(+-0) = +-0 and neither residual test moves it:
+// quat_from_rotation_matrix clamps negative estimates to 0, so zeros are common there); x below 2^-96 (denormals,
+// negatives), inf and NaN take cr_sqrt64 behind one rare-case branch.  No f64
 // instruction on the common path (cr_sqrt64: three f64 ops and two quarter-rate f64 transcendentals).  Proven equal
 // to __builtin_sqrtf on all 2^32 inputs by tools/check_fastmath.hip [1] (run by tests/test_gpu_parity.py).
 __device__ __attribute__((noinline)) float cr_sqrt64_call(float x) { return cr_sqrt64(x); }
@@ -54,13 +56,31 @@ RTG_DEV float cr_sqrt(float x)
 #if RTG_EXP_SQRT64   // A/B knob (same values): round 4's f64 form everywhere
     return cr_sqrt64(x);
 #endif
+#if RTG_EXP_SQRT_CALL   // A/B knob (same values): the round-5 first form, x < 2^-96 / inf / NaN behind a call
     float s = __builtin_amdgcn_sqrtf(x);
     const float sdn = __uint_as_float(__float_as_uint(s) - 1u), sup = __uint_as_float(__float_as_uint(s) + 1u);
     const float rdn = __builtin_fmaf(-sdn, s, x), rup = __builtin_fmaf(-sup, s, x);
     s = rdn <= 0.0f ? sdn : s;
     s = rup > 0.0f ? sup : s;
-    if (!RTG_EXP_NO_RARE && __builtin_expect(!(x >= 0x1p-96f && x <= 3.40282347e38f), 0)) s = cr_sqrt64_call(x);
+    if (!(RTG_EXP_NO_RARE & 1) && __builtin_expect(!((x >= 0x1p-96f && x <= 3.40282347e38f) || x == 0.0f), 0))
+        s = cr_sqrt64_call(x);
     return s;
+#else
+    // branch-free: x < 2^-96 (tiny and denormal positives; negatives and -0, which the scaling keeps negative / -0
+    // and the sequence turns into NaN / -0) is scaled by 2^64 into the range where v_sqrt_f32 is within an ulp and
+    // the result scaled back by 2^-32 (both exact: sqrt(2^-149 2^64) = 2^-42.5 and the result stays normal).  +-0,
+    // inf and NaN come out of the sequence itself (v_sqrt_f32 returns them exactly; every residual test reads
+    // false on them).  The branch it replaces was a call (cr_sqrt64) at each of ~150 inlined sites of the side
+    // kernel: each site's call set-up and call-clobbered registers cost more than the 4 instructions here.
+    const bool tiny = x < 0x1p-96f;
+    const float xs = tiny ? x * 0x1p64f : x;
+    float s = __builtin_amdgcn_sqrtf(xs);
+    const float sdn = __uint_as_float(__float_as_uint(s) - 1u), sup = __uint_as_float(__float_as_uint(s) + 1u);
+    const float rdn = __builtin_fmaf(-sdn, s, xs), rup = __builtin_fmaf(-sup, s, xs);
+    s = rdn <= 0.0f ? sdn : s;
+    s = rup > 0.0f ? sup : s;
+    return tiny ? s * 0x1p-32f : s;
+#endif
 }
 // Rounding test for an f64 approximation y of a value whose f32 rounding is wanted: true when the bits f32 rounding
 // drops (29 of them, for an f32-normal |y|) are not within D f64 ulps of the midpoint 2^28, i.e. every value within
@@ -71,7 +91,7 @@ RTG_DEV bool f32_round_safe(double y, uint32_t D)
     const uint64_t b = (uint64_t)__double_as_longlong(y);
     const uint32_t lo = (uint32_t)b & 0x1FFFFFFFu;
     const uint32_t ex = (uint32_t)(b >> 52) & 0x7FFu;
-    return (lo - (0x10000000u - D)) > 2u * D && ex >= 1023u - 126u && ex <= 1023u + 127u;
+    return ((lo - (0x10000000u - D)) > 2u * D) & (ex >= 1023u - 126u) & (ex <= 1023u + 127u);
 }
 RTG_DEV float acos_libm(float x) { return (float)::acos((double)x); }
 // the rare-case call of cr_acos, out of line: inlined into the hot path, its registers raised the side kernel from
@@ -109,8 +129,11 @@ RTG_DEV float acos_fast(float x, bool &ok)
     const double A = big ? (neg ? 3.141592653589793 : 0.0) : 1.5707963267948966;
     const double Bc = big ? (neg ? -2.0 : 2.0) : (neg ? 1.0 : -1.0);
     const double y = __builtin_fma(Bc, as, A);
-    ok = f32_round_safe(y, 1u << 12) && ax < 1.0f;
-    return (float)y;
+    // x = +-1 (radians_between clamps its cosine to [-1, 1], so exactly parallel / antiparallel vectors give them):
+    // acos is +0 / RN(pi), set here rather than through the rare-case branch
+    const bool one = ax == 1.0f;
+    ok = (f32_round_safe(y, 1u << 12) & (ax < 1.0f)) | one;
+    return one ? (neg ? 3.14159274f : 0.0f) : (float)y;
 }
 RTG_DEV float cr_acos(float x)
 {
@@ -119,7 +142,7 @@ RTG_DEV float cr_acos(float x)
 #endif
     bool ok;
     float r = acos_fast(x, ok);
-    if (!RTG_EXP_NO_RARE && __builtin_expect(!ok, 0)) r = acos_libm_call(x);
+    if (!(RTG_EXP_NO_RARE & 2) && __builtin_expect(!ok, 0)) r = acos_libm_call(x);
     return r;
 }
 RTG_DEV float cr_sin(float x) { return (float)::sin((double)x); }
@@ -135,7 +158,7 @@ RTG_DEV SC cr_sincos(double x)
 {
     const crm::SinCos r = crm::crm_sincos(x);
     SC out{r.s, r.c};
-    if (!RTG_EXP_NO_RARE && __builtin_expect(!(r.s_ok && r.c_ok), 0)) {   // one rare-case branch for the pair
+    if (!(RTG_EXP_NO_RARE & 4) && __builtin_expect(!(r.s_ok & r.c_ok), 0)) {   // one rare-case branch for the pair
         if (!r.s_ok) out.s = sin_libm_call(x);
         if (!r.c_ok) out.c = cos_libm_call(x);
     }
@@ -186,10 +209,10 @@ RTG_DEV void mulr_k(const float (&a)[K], const Rcp &r, float (&q)[K])
     for (int i = 0; i < K; ++i) {
         const double p = (double)a[i] * r.r;
         q[i] = (float)p;
-        sub = sub || (__builtin_fabs(p) < 0x1p-126 && p != 0.0);
+        sub |= (__builtin_fabs(p) < 0x1p-126) & (p != 0.0);
     }
 #if !RTG_EXP_MULR_NOBRANCH
-    if (!RTG_EXP_NO_RARE && __builtin_expect(sub, 0)) {
+    if (!(RTG_EXP_NO_RARE & 8) && __builtin_expect(sub, 0)) {
 #pragma unroll
         for (int i = 0; i < K; ++i) q[i] = a[i] / r.n;
     }
@@ -202,10 +225,10 @@ RTG_DEV Q mulr_q(Q v, const Rcp &r)
     const double p[4] = {(double)v.x * r.r, (double)v.y * r.r, (double)v.z * r.r, (double)v.w * r.r};
     bool sub = false;
 #pragma unroll
-    for (int i = 0; i < 4; ++i) sub = sub || (__builtin_fabs(p[i]) < 0x1p-126 && p[i] != 0.0);
+    for (int i = 0; i < 4; ++i) sub |= (__builtin_fabs(p[i]) < 0x1p-126) & (p[i] != 0.0);
     Q q{(float)p[0], (float)p[1], (float)p[2], (float)p[3]};
 #if !RTG_EXP_MULR_NOBRANCH
-    if (!RTG_EXP_NO_RARE && __builtin_expect(sub, 0)) q = div_q_call(v, r.n);   // = mulr_k<4>: every quotient by IEEE division
+    if (!(RTG_EXP_NO_RARE & 8) && __builtin_expect(sub, 0)) q = div_q_call(v, r.n);   // = mulr_k<4>: every quotient by IEEE division
 #endif
     return q;
 }
@@ -247,7 +270,7 @@ RTG_DEV NormRcp sqrt_clamp_rcp(float s, float lo)
     const double r1 = __builtin_fma(r0, e0, r0);
     const double e1 = __builtin_fma(-dn, r1, 1.0);
     NormRcp out{n, Rcp{__builtin_fma(r1, e1, r1), n}};
-    if (!RTG_EXP_NO_RARE && __builtin_expect(!(d > 0.0 && d < __builtin_inf() && n >= lo), 0)) {
+    if (!(RTG_EXP_NO_RARE & 16) && __builtin_expect(!((d > 0.0) & (d < __builtin_inf()) & (n >= lo)), 0)) {
         const float nc = clamp_lo(cr_sqrt(s), lo);
         out = NormRcp{nc, rcp64(nc)};
     }
@@ -719,7 +742,7 @@ RTG_DEV float la_larfg(float &alpha, float &x0, float &x1)
     float xn = NX == 1 ? fabsf(x0) : la_lapy2(x0, x1);
     float beta = -__builtin_copysignf(la_lapy2(alpha, xn), alpha);   // discarded when xn == 0
     int knt = 0;
-    if (__builtin_expect(xn == 0.0f || fabsf(beta) < safmin, 0)) {   // ONE rare-case branch for both cases
+    if (__builtin_expect((xn == 0.0f) | (fabsf(beta) < safmin), 0)) {   // ONE rare-case branch for both cases
         if (xn == 0.0f) return 0.0f;
         do {
             ++knt;
@@ -760,7 +783,7 @@ RTG_DEV void la_lartg(float f, float g, float &c, float &s, float &r)   // SLART
         r = __builtin_copysignf(d, f);
         s = f < 0.0f ? -quo[1] : quo[1];   // g / r with r = +-d (RN is sign-symmetric)
     }
-    if (__builtin_expect(!(g != 0.0f && f != 0.0f && f1 > rtmin && f1 < rtmax && g1 > rtmin && g1 < rtmax), 0)) {
+    if (__builtin_expect(!((g != 0.0f) & (f != 0.0f) & (f1 > rtmin) & (f1 < rtmax) & (g1 > rtmin) & (g1 < rtmax)), 0)) {
         if (g == 0.0f) { c = 1.0f; s = 0.0f; r = f; }
         else if (f == 0.0f) { c = 0.0f; s = __builtin_copysignf(1.0f, g); r = g1; }
         else {

@@ -506,6 +506,7 @@ struct VelTile {
     uint32_t tiles;     // blocks per sequence
     uint32_t nblocks;   // blocks in this launch
     int32_t C, J;       // output channels per row; joints (angular) or input channels (linear)
+    double rdt;         // RN(1 / (double)dt): the quotients by dt as mulr products (rtg_math.cuh), the same values
 };
 // (row, channel) of flat element e = row * C + ch, advanced by 256 elements per step without a division
 struct RowWalk {
@@ -593,9 +594,20 @@ __global__ __launch_bounds__(256) void k_velocity_tile(const float *__restrict__
 #pragma unroll
                 for (int k = 0; k < SEG + 2; ++k) raw[k] = k < nr + 2 ? q[(int64_t)k * C] : 0.0f;
                 // np.gradient inside the sequence: (p[t+1] - p[t-1]) / 2 (x / 2 == x * 0.5, correctly rounded)
+#if RTG_VEL_IEEE_DIV   // A/B knob (same values): one IEEE division per gradient
 #pragma unroll
                 for (int j = 0; j < SEG; ++j)
                     if (j < nr) dst[j] = ((raw[j + 2] - raw[j]) * 0.5f) / dt;
+#else
+                // the SEG quotients by dt through the shared reciprocal (mulr_k: one rare-case branch per run)
+                float g[SEG], v[SEG];
+#pragma unroll
+                for (int j = 0; j < SEG; ++j) g[j] = (raw[j + 2] - raw[j]) * 0.5f;
+                mulr_k<SEG>(g, Rcp{vt.rdt, dt}, v);
+#pragma unroll
+                for (int j = 0; j < SEG; ++j)
+                    if (j < nr) dst[j] = v[j];
+#endif
             } else {
                 for (int j = 0; j < nr; ++j) {
                     const int x = x0 + j;
@@ -650,9 +662,16 @@ __global__ __launch_bounds__(256) void k_velocity_tile(const float *__restrict__
                 Q d = qident();
                 if (!cl[k]) d = qmul_norm(ca[k], qconj(cb[k]));
                 const Q aa = qangle_axis_abs(d);
+#if RTG_VEL_IEEE_DIV
                 sg[cat[k]] = (aa.y * aa.x) / dt;
                 sg[cat[k] + NS] = (aa.z * aa.x) / dt;
                 sg[cat[k] + 2 * NS] = (aa.w * aa.x) / dt;
+#else
+                const V av = mulr_v(V{aa.y * aa.x, aa.z * aa.x, aa.w * aa.x}, Rcp{vt.rdt, dt});
+                sg[cat[k]] = av.x;
+                sg[cat[k] + NS] = av.y;
+                sg[cat[k] + 2 * NS] = av.z;
+#endif
             }
 #if !RTG_VEL_ANG_PIPE
             if (e0 + 256 * NB < n) fetch(e0 + 256 * NB);
@@ -706,7 +725,7 @@ static hipError_t launch_velocity_tile(const float *src, int64_t nseq, int64_t L
     if (RTG_VEL_LDS_MIN > 0 && lds < (size_t)RTG_VEL_LDS_MIN) lds = RTG_VEL_LDS_MIN;   // measurement knob: fewer blocks/CU
     for (int64_t q0 = 0; q0 < nseq; q0 += per) {
         const int64_t nq = nseq - q0 < per ? nseq - q0 : per;
-        const VelTile vt{q0, (uint32_t)L, T, tiles, (uint32_t)(nq * tiles), (int32_t)C, (int32_t)J};
+        const VelTile vt{q0, (uint32_t)L, T, tiles, (uint32_t)(nq * tiles), (int32_t)C, (int32_t)J, 1.0 / (double)dt};
         if (taps.radius == 8)   // sigma 2, truncate 4: the reference's filter
             hipLaunchKernelGGL((k_velocity_tile<ANGULAR, 8>), dim3(vt.nblocks), dim3(256), lds, s, src, vt, dt, taps, out);
         else
@@ -1030,8 +1049,8 @@ int probe_valu_iters() { return kProbeIters; }
 extern "C" const char *rtg_build_info(void)
 {
     return "{\"abi\":" RTG_STR(RTG_ABI_VERSION) ",\"arch\":\"gfx950\",\"knobs\":{"
-        RTG_KNOB(RTG_SIDES_WAVES) RTG_KNOB(RTG_LATENCY_MAX_B)
-        RTG_KNOB(RTG_EXP_TIMESTAMPS) RTG_KNOB(RTG_EXP_SKIP_SIGNAL) RTG_KNOB(RTG_EXP_STUB_SVD) RTG_KNOB(RTG_EXP_NO_TABLE) RTG_KNOB(RTG_EXP_FK_COPY) RTG_KNOB(RTG_EXP_FK_NOPOS) RTG_KNOB(RTG_EXP_MULR_NOBRANCH) RTG_KNOB(RTG_EXP_LARTG_RCP64) RTG_KNOB(RTG_EXP_SQRT64) RTG_KNOB(RTG_EXP_ACOS_LIBM) RTG_KNOB(RTG_EXP_EULER_SCIPY) RTG_KNOB(RTG_VEL_SEG) RTG_KNOB(RTG_VEL_LDS_MIN) RTG_KNOB(RTG_VEL_ANG_PIPE) RTG_KNOB(RTG_EXP_NO_RARE)
+        RTG_KNOB(RTG_SIDES_WAVES) RTG_KNOB(RTG_QUAD_MAX_B) RTG_KNOB(RTG_LATENCY_MAX_B)
+        RTG_KNOB(RTG_EXP_TIMESTAMPS) RTG_KNOB(RTG_EXP_SKIP_SIGNAL) RTG_KNOB(RTG_EXP_STUB_SVD) RTG_KNOB(RTG_EXP_NO_TABLE) RTG_KNOB(RTG_EXP_FK_COPY) RTG_KNOB(RTG_EXP_FK_NOPOS) RTG_KNOB(RTG_EXP_MULR_NOBRANCH) RTG_KNOB(RTG_EXP_LARTG_RCP64) RTG_KNOB(RTG_EXP_SQRT64) RTG_KNOB(RTG_EXP_SQRT_CALL) RTG_KNOB(RTG_EXP_ACOS_LIBM) RTG_KNOB(RTG_EXP_EULER_SCIPY) RTG_KNOB(RTG_VEL_SEG) RTG_KNOB(RTG_VEL_LDS_MIN) RTG_KNOB(RTG_VEL_ANG_PIPE) RTG_KNOB(RTG_VEL_IEEE_DIV) RTG_KNOB(RTG_EXP_NO_RARE)
         "\"RTG_EXP_HOT_INPUTS\":\"" RTG_STR(RTG_EXP_HOT_INPUTS) "\"},\"wrong_answer_knobs\":"
         RTG_STR(RTG_WRONG_ANSWER_KNOBS) "}";
 }

@@ -13,6 +13,7 @@
 //
 // Kernels (launch_kind picks by batch size):
 //   B == 1                    k_fbp_frame1    one frame, its independent sub-steps on separate lanes (teleop)
+//   B <= RTG_QUAD_MAX_B       k_fbp_quad      five waves per 16-frame tile, a frame's sub-steps on a lane quad
 //   B <= RTG_LATENCY_MAX_B    k_fbp_latency5  five waves per 64-frame tile (latency-bound batches)
 //   larger                    k_solve_sides   two waves per 64-frame tile (throughput; the bench headline)
 // and k_frame_server, the resident per-frame server on k_fbp_frame1's tile.
@@ -766,12 +767,35 @@ RTG_DEV double rdl(double v, int l)
     return __builtin_bit_cast(double, ((uint64_t)hi << 32) | lo);
 }
 RTG_DEV Q rdl(Q q, int k) { return Q{rdl(q.x, k), rdl(q.y, k), rdl(q.z, k), rdl(q.w, k)}; }
+// Broadcast of sub-lane K within this lane's group of G lanes: G = 64, the wave (v_readlane: k_fbp_frame1, one frame
+// per block); G = 4, a quad (DPP quad_perm, one VALU op: k_fbp_quad, one frame per quad).  Called where every lane of
+// the group is active (DPP reads an inactive source lane as 0).
+template <int G, int K>
+RTG_DEV float gbc(float v)
+{
+    static_assert(G == 64 || G == 4, "group of 64 or 4 lanes");
+    if constexpr (G == 64) return rdl(v, K);
+    else return __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, v), K * 0x55, 0xF, 0xF, false));
+}
+template <int G, int K>
+RTG_DEV double gbc(double v)
+{
+    if constexpr (G == 64) return rdl(v, K);
+    const uint64_t u = __builtin_bit_cast(uint64_t, v);
+    const uint32_t lo = __builtin_bit_cast(uint32_t, gbc<G, K>(__builtin_bit_cast(float, (uint32_t)u)));
+    const uint32_t hi = __builtin_bit_cast(uint32_t, gbc<G, K>(__builtin_bit_cast(float, (uint32_t)(u >> 32))));
+    return __builtin_bit_cast(double, ((uint64_t)hi << 32) | lo);
+}
+template <int G, int K>
+RTG_DEV Q gbc(Q q) { return Q{gbc<G, K>(q.x), gbc<G, K>(q.y), gbc<G, K>(q.z), gbc<G, K>(q.w)}; }
+template <int G>
+RTG_DEV int sublane() { return (int)(threadIdx.x & (G - 1)); }
 
-// shoulder_pr (SHOULDER) / elbow_py of the frame: lane 0 the first angle's quaternion, lane 1 the second's
-template <bool SHOULDER>
+// shoulder_pr (SHOULDER) / elbow_py of the frame: sub-lane 0 the first angle's quaternion, sub-lane 1 the second's
+template <bool SHOULDER, int G = 64>
 RTG_DEV void arm_pair_lanes(V v1, ArmZero z0, Q parent, Q &first, Q &second)
 {
-    const int sub = threadIdx.x & 63;
+    const int sub = sublane<G>();
     Q q = qident();
     if (sub < 2) {
         const V ex{1.f, 0.f, 0.f}, ey{0.f, 1.f, 0.f}, ez{0.f, 0.f, 1.f};
@@ -787,8 +811,8 @@ RTG_DEV void arm_pair_lanes(V v1, ArmZero z0, Q parent, Q &first, Q &second)
         const V ax = l0 ? pn : (SHOULDER ? ex : ey);
         q = qfrom_angle_unit_axis(ang - (l0 ? z0.th0 : z0.ph0), ax);
     }
-    first = rdl(q, 0);
-    second = rdl(q, 1);
+    first = gbc<G, 0>(q);
+    second = gbc<G, 1>(q);
 }
 // Emit::link with a run-time link index (lane-parallel writers)
 RTG_DEV void link_rt(const Emit &E, int link, Q q)
@@ -797,28 +821,33 @@ RTG_DEV void link_rt(const Emit &E, int link, Q q)
     E.st[(link <= 18 ? link - 12 : link - 14) * E.sst] = make_float2(q.w, k == 0 ? q.x : (k == 1 ? q.y : q.z));
     if (E.lr) st4(E.lr + 4 * link, q);
 }
-template <int L0>
+template <int L0, int G = 64>
 RTG_DEV Q solve_arm_lanes(const Emit &E, V upper, V fore, ArmZero zs, ArmZero ze, Q parent)
 {
-    const bool w0 = (threadIdx.x & 63) == 0;
+    const bool w0 = sublane<G>() == 0;
     Q p, r, y, e;
-    arm_pair_lanes<true>(upper, zs, parent, p, r);
+    arm_pair_lanes<true, G>(upper, zs, parent, p, r);
     if (w0) { E.link<L0>(p); E.link<L0 + 1>(r); }
-    arm_pair_lanes<false>(fore, ze, qmul(qmul(parent, p), r), y, e);
+    arm_pair_lanes<false, G>(fore, ze, qmul(qmul(parent, p), r), y, e);
     if (w0) { E.link<L0 + 2>(y); E.link<L0 + 3>(e); }
     return qmul(qmul(qmul(p, r), y), e);
 }
-// emit_euler_xyz (quat_in_xyz_axis 'XYZ', scipy_as_euler's arithmetic) with the three atan2 on lanes 0-2 and one
-// elementary quaternion per lane; every lane holds the same qf, so every lane returns the same refusal flag
-template <int L0>
+// emit_euler_xyz (quat_in_xyz_axis 'XYZ', scipy_as_euler's arithmetic) with the three atan2 on sub-lanes 0-2 and one
+// elementary quaternion per sub-lane; every lane of the group holds the same qf, so every lane returns the same
+// refusal flag
+template <int L0, int G = 64>
 RTG_DEV bool emit_euler_xyz_lanes(const Emit &E, Q qf)
 {
-    const int sub = threadIdx.x & 63;
-    {   // round 5: the atan2-free split (quat_in_xyz_fast, same values) on every lane -- qf is the same on all, so the
-        // branch is uniform; where it declines, the lane-parallel scipy restatement below runs
+    const int sub = sublane<G>();
+    {   // round 5: the atan2-free split (quat_in_xyz_fast, same values) on every lane -- qf is the same on all lanes
+        // of the group, so the branch is uniform in it; where it declines, the lane-parallel scipy restatement runs
         Q eul[3];
         if (quat_in_xyz_fast(qf, eul)) {   // implies |q| > 0: scipy does not refuse it
-            if (sub < 3) link_rt(E, L0 + sub, sub == 0 ? eul[0] : (sub == 1 ? eul[1] : eul[2]));
+            // per-component selects (an indexed eul[sub] went through scratch memory)
+            const bool s0 = sub == 0, s1 = sub == 1;
+            const Q e{s0 ? eul[0].x : (s1 ? eul[1].x : eul[2].x), s0 ? eul[0].y : (s1 ? eul[1].y : eul[2].y),
+                      s0 ? eul[0].z : (s1 ? eul[1].z : eul[2].z), s0 ? eul[0].w : (s1 ? eul[1].w : eul[2].w)};
+            if (sub < 3) link_rt(E, L0 + sub, e);
             return false;
         }
     }
@@ -837,8 +866,8 @@ RTG_DEV bool emit_euler_xyz_lanes(const Emit &E, Q qf)
         at = ::atan2(Y, X);
     }
     double ang[3];
-    ang[1] = 2.0 * rdl(at, 0);
-    const double half_sum = rdl(at, 1), half_diff = rdl(at, 2);
+    ang[1] = 2.0 * gbc<G, 0>(at);
+    const double half_sum = gbc<G, 1>(at), half_diff = gbc<G, 2>(at);
     int kase = 0;
     if (fabs(ang[1]) <= 1e-7) kase = 1;
     else if (fabs(ang[1] - M_PI) <= 1e-7) kase = 2;
@@ -860,10 +889,11 @@ RTG_DEV bool emit_euler_xyz_lanes(const Emit &E, Q qf)
     if (sub < 3) link_rt(E, L0 + sub, elementary_quat(sub, sub == 0 ? ang[0] : (sub == 1 ? ang[1] : ang[2])));
     return refused;
 }
-// Emit::finalize with one slot per lane (slots s0 .. s0 + n - 1)
+// Emit::finalize with one slot per sub-lane (slots s0 .. s0 + n - 1, n <= G)
+template <int G = 64>
 RTG_DEV void finalize_lanes(const Emit &E, int s0, int n)
 {
-    const int sub = threadIdx.x & 63;
+    const int sub = sublane<G>();
     if (sub < n) {
         const int j = s0 + sub;
         const float2 v = E.st[j * E.sst];
@@ -928,7 +958,7 @@ RTG_DEV uint32_t fbp_frame1_tile(const SolverConsts &C, const float *rows, float
             const TipPts tp = load_tips(H);
             a = hand_x_mean(qconj(W), tp.h0, tp.t);   // the gripper needs only W (:142-158 / :165-175)
         }
-        W = rdl(W, 0);
+        W = gbc<64, 0>(W);
         lds_wait(&sflag[1 + side], C.err);   // the arm waited for R10 first: both are visible (release / acquire chain)
         const float4 t = sfit, c = schain[side];
         const Q R10{t.x, t.y, t.z, t.w}, chain{c.x, c.y, c.z, c.w};
@@ -969,6 +999,115 @@ __global__ __launch_bounds__(320) void k_fbp_frame1(SolverConsts C, const float 
     }
     __syncthreads();
     fbp_frame1_tile<PRECISE>(C, rows, dof, local_rot, body_rot);
+}
+
+// ----------------------------------------------------------------------------
+// FULL_BODY_POS for small batches (round 5, config 2): k_fbp_frame1's lane-parallel frame program on 16 frames per
+// block, one frame per QUAD of lanes.  k_fbp_latency5 puts 64 frames in a block, so B = 4096 fills 64 of the 256
+// CUs and each frame's chain runs its sub-steps one after another; here the same 4096 frames are 256 blocks (every
+// CU), and inside a frame the sub-steps that k_fbp_frame1 spreads over lanes -- the arm maps' two angles, the three
+// Euler elementary quaternions, up to four exp-map read-outs -- run on the quad's four lanes, their partial results
+// crossing by DPP quad broadcasts.  The waves' roles are k_fbp_latency5's (0 torso fit, 1 / 2 wrist fits then the
+// Euler split, 3 / 4 arm chains).  Every value comes from the same device functions on the same operands: the same
+// bits (test_solver_batch_invariance, the GPU parity suite).
+// ----------------------------------------------------------------------------
+constexpr int kQuadFrames = 16;
+template <bool PRECISE, bool SOA>
+__global__ __launch_bounds__(320) void k_fbp_quad(SolverConsts C, const float *__restrict__ in0,
+                                                  const float *__restrict__ in1, const float *__restrict__ in2,
+                                                  int64_t B, float *__restrict__ dof, float *__restrict__ local_rot,
+                                                  float *__restrict__ body_rot)
+{
+    constexpr int RP = 184;                      // LDS row pitch of a frame: body 63 | left hand 60 | right hand 60
+    __shared__ float rows[kQuadFrames * RP];
+    __shared__ float sdof[kQuadFrames * kDofStride];
+    __shared__ float4 sfit[kQuadFrames], schain[2][kQuadFrames];
+    __shared__ float2 sst[kQuadFrames * 14];
+    __shared__ int sflag[3];                     // R10 ready, left arm ready, right arm ready
+    __shared__ uint8_t sstat[3][kQuadFrames];    // status bits of the torso wave and the two wrist waves
+    const int64_t f0 = (int64_t)blockIdx.x * kQuadFrames;
+    const int nf = (int)((B - f0) < kQuadFrames ? (B - f0) : kQuadFrames);
+    // the tile's rows into LDS, all loads in flight together; a frame slot past B repeats the last frame (every lane
+    // runs the whole program -- the DPP broadcasts need the full quad -- and only live frames store)
+    if (SOA) {
+        for (int i = threadIdx.x; i < kQuadFrames * 183; i += 320) {
+            const int q = i & (kQuadFrames - 1), e = i >> 4;   // 16 consecutive frames of one component
+            const int64_t f = f0 + (q < nf ? q : nf - 1);
+            rows[q * RP + e] = e < 63 ? in0[e * B + f] : (e < 123 ? in1[(e - 63) * B + f] : in2[(e - 123) * B + f]);
+        }
+    } else {
+        for (int i = threadIdx.x; i < kQuadFrames * 183; i += 320) {
+            const int q = i / 183, e = i - q * 183;
+            const int64_t f = f0 + (q < nf ? q : nf - 1);
+            rows[q * RP + e] = e < 63 ? in0[f * 63 + e] : (e < 123 ? in1[f * 60 + (e - 63)] : in2[f * 60 + (e - 123)]);
+        }
+    }
+    if (threadIdx.x < 3) sflag[threadIdx.x] = 0;
+    __syncthreads();
+    const int w = threadIdx.x >> 6, lane = threadIdx.x & 63, q = lane >> 2, sub = lane & 3;
+    const int64_t f = f0 + q;
+    const bool live = q < nf;
+    const Emit E{sdof + q * kDofStride, live && local_rot ? local_rot + f * 124 : nullptr, C.ang_tab, sst + q * 14, 1};
+    const FV<false> b{rows + q * RP};
+    uint32_t st = 0;
+    if (w == 0) {
+        if (sub == 0) {
+            bool nan = false;
+            const Q t = fbp_torso(C, b, nan);
+            sfit[q] = make_float4(t.x, t.y, t.z, t.w);
+            st = nan ? kStTorsoSvd : 0u;
+        }
+        lds_signal(&sflag[0]);
+        if (sub == 0) emit_fixed_links(E);
+    } else if (w >= 3) {
+        const int side = w - 3;
+        const ArmPts ap = side ? load_arm<1>(b) : load_arm<0>(b);
+        lds_wait(&sflag[0], C.err);
+        const float4 t = sfit[q];
+        const Q R10{t.x, t.y, t.z, t.w};
+        const V up = vsub(ap.el, ap.sh), fo = vsub(ap.wr, ap.el);
+        const Q ch = side ? solve_arm_lanes<21, 4>(E, up, fo, C.rsh, C.rel, R10)
+                          : solve_arm_lanes<12, 4>(E, up, fo, C.lsh, C.lel, R10);
+        if (sub == 0) schain[side][q] = make_float4(ch.x, ch.y, ch.z, ch.w);
+        lds_signal(&sflag[1 + side]);
+        finalize_lanes<4>(E, side ? 7 : 0, 4);
+    } else {
+        const int side = w - 1;
+        const FV<false> H{rows + q * RP + (side ? 123 : 63)};
+        Q W = qident();
+        float a = 0.0f;
+        if (sub == 0) {
+            bool nan = false;
+            W = side ? fbp_wrist_fit<1>(C, H, nan) : fbp_wrist_fit<0>(C, H, nan);
+            st = nan ? (side ? kStRightSvd : kStLeftSvd) : 0u;
+            const TipPts tp = load_tips(H);
+            a = hand_x_mean(qconj(W), tp.h0, tp.t);   // the gripper needs only W (:142-158 / :165-175)
+        }
+        W = gbc<4, 0>(W);
+        lds_wait(&sflag[1 + side], C.err);   // the arm waited for R10 first: both are visible (release / acquire chain)
+        const float4 t = sfit[q], c = schain[side][q];
+        const Q R10{t.x, t.y, t.z, t.w}, chain{c.x, c.y, c.z, c.w};
+        if (sub == 0) {
+            fbp_gripper<PRECISE>(C, a, E.row + (side ? 27 : 18));
+            if (body_rot && live) {
+                float *const brow = body_rot + f * 236;
+                if (side) fbp_body_rows<1>(brow, R10, W);
+                else fbp_body_rows<0>(brow, R10, W);
+            }
+        }
+        const Q loc = qmul_norm(qconj(qmul_norm(R10, chain)), W);
+        const bool refused = side ? emit_euler_xyz_lanes<25, 4>(E, loc) : emit_euler_xyz_lanes<16, 4>(E, loc);
+        st |= refused ? (side ? kStRightEuler : kStLeftEuler) : 0u;
+        finalize_lanes<4>(E, side ? 11 : 4, 3);
+    }
+    if (w < 3 && sub == 0) sstat[w][q] = (uint8_t)st;
+    __syncthreads();
+    const uint32_t bits = (w == 0 && sub == 0 && live) ? (uint32_t)(sstat[0][q] | sstat[1][q] | sstat[2][q]) : 0u;
+    if (__syncthreads_or(bits != 0u)) {   // rare: a frame the reference raises on
+        if (bits) poison_frame(E.row, E.lr, body_rot ? body_rot + f * 236 : nullptr, bits);
+        __syncthreads();
+    }
+    store_dof_rows(dof + f0 * 30, sdof, nf, threadIdx.x, 320);   // f0 * 30 floats: 16-byte aligned
 }
 
 // ----------------------------------------------------------------------------
@@ -1037,6 +1176,11 @@ static void launch_kind(const SolverConsts &C, const float *in0, const float *in
         if (B == 1) {
             hipLaunchKernelGGL((k_fbp_frame1<PRECISE>), dim3(1), dim3(320), 0, s, C, in0, in1, in2, dof, local_rot,
                                body_rot);
+            return;
+        }
+        if (B <= RTG_QUAD_MAX_B) {
+            hipLaunchKernelGGL((k_fbp_quad<PRECISE, SOA>), dim3(grid_for(B, kQuadFrames)), dim3(320), 0, s, C, in0,
+                               in1, in2, B, dof, local_rot, body_rot);
             return;
         }
         if (B <= RTG_LATENCY_MAX_B) {

@@ -5,8 +5,9 @@ RuntimeError from torch.linalg.svd on a NaN Kabsch matrix (transform3d.py:40) or
 on a zero / NaN quaternion (transform3d.py:53).  The batched kernels mark such frames (rtg.h rtg_frame_error:
 every dof NaN, the code in dof[f, 0]'s payload, local_rot / body_rot rows NaN); the drop-in per-frame calls raise
 the reference's exception.  Every comparison with the oracle is on the raw bits (every NaN reading alike, see _bits;
-the frame codes compared exactly), through each kernel that serves FULL_BODY_POS: k_fbp_frame1 (B = 1), k_fbp_latency5 (B <= RTG_LATENCY_MAX_B) and
-k_solve_sides (larger, edge frames scattered through a ragged 65536 + 40 batch whose last tile is empty)."""
+the frame codes compared exactly), through each kernel that serves FULL_BODY_POS: k_fbp_frame1 (B = 1), k_fbp_quad (B <= RTG_QUAD_MAX_B: the fixture
+as one batch), k_fbp_latency5 (B <= RTG_LATENCY_MAX_B) and k_solve_sides (larger; edge frames scattered through
+ragged batches whose last tile is partly empty)."""
 import os
 import subprocess
 import sys
@@ -77,7 +78,7 @@ def test_edge_frames_gpu_equals_oracle_every_kernel(gpu, name, kind, precise):
     odof, olr, obr = _oracle(kind, d, precise)
     S = _solver(kind, precise)
     fbp = kind == 0
-    # the whole fixture as one batch (k_fbp_latency5 for FULL_BODY_POS, k_solve_sides otherwise)
+    # the whole fixture as one batch (k_fbp_quad for FULL_BODY_POS, k_solve_sides otherwise)
     dof, lr, br = S.retarget(ins, want_local_rot=True, want_body_rot=fbp)
     import oracle as orc
     np.testing.assert_array_equal(orc.frame_status(odof), _ref_status(name, d, precise))
@@ -91,19 +92,25 @@ def test_edge_frames_gpu_equals_oracle_every_kernel(gpu, name, kind, precise):
     np.testing.assert_array_equal(_bits(dof_s), _bits(odof))
     np.testing.assert_array_equal(frame_status(dof_s).cpu().numpy(), _ref_status(name, d, precise))
     np.testing.assert_array_equal(_bits(lr_s), _bits(olr))
-    # scattered through a ragged large batch (k_solve_sides; 65536 + 40 leaves the last block's second tile empty)
-    B = 65536 + 40
-    g = torch.Generator().manual_seed(5)
-    idx = torch.randint(0, n, (B,), generator=g)
-    idx[-n:] = torch.arange(n)   # every edge frame, including in the last, partly empty block
-    big = [t[idx.cuda()].contiguous() for t in ins]
-    dof_b, lr_b, br_b = S.retarget(big, want_local_rot=True, want_body_rot=fbp)
-    sel = idx.numpy()
-    np.testing.assert_array_equal(frame_status(dof_b).cpu().numpy(), _ref_status(name, d, precise)[sel])
-    np.testing.assert_array_equal(_bits(dof_b), _bits(odof)[sel])
-    np.testing.assert_array_equal(_bits(lr_b), _bits(olr)[sel])
-    if fbp:
-        np.testing.assert_array_equal(_bits(br_b), _bits(obr)[sel])
+    # scattered through ragged larger batches: k_solve_sides (65536 + 40 leaves the last block's second tile empty)
+    # and, for FULL_BODY_POS, k_fbp_latency5 (a size between the build's quad and latency bounds, 64-frame tiles)
+    from rtg import _lib
+    info = _lib.build_info()["knobs"]
+    sizes = [65536 + 40]
+    if fbp and info["RTG_QUAD_MAX_B"] + 40 <= info["RTG_LATENCY_MAX_B"]:
+        sizes.append(info["RTG_QUAD_MAX_B"] + 40)
+    for B in sizes:
+        g = torch.Generator().manual_seed(5)
+        idx = torch.randint(0, n, (B,), generator=g)
+        idx[-n:] = torch.arange(n)   # every edge frame, including in the last, partly empty block
+        big = [t[idx.cuda()].contiguous() for t in ins]
+        dof_b, lr_b, br_b = S.retarget(big, want_local_rot=True, want_body_rot=fbp)
+        sel = idx.numpy()
+        np.testing.assert_array_equal(frame_status(dof_b).cpu().numpy(), _ref_status(name, d, precise)[sel])
+        np.testing.assert_array_equal(_bits(dof_b), _bits(odof)[sel])
+        np.testing.assert_array_equal(_bits(lr_b), _bits(olr)[sel])
+        if fbp:
+            np.testing.assert_array_equal(_bits(br_b), _bits(obr)[sel])
         # one frame per launch (k_fbp_frame1)
         for i in range(n):
             d1, l1, b1 = S.retarget([t[i:i + 1] for t in ins], want_local_rot=True, want_body_rot=True)
