@@ -10,7 +10,7 @@
 #define RTG_SIDES_WAVES 1   // min waves per SIMD for the side kernel (1: the compiler picks; measured best)
 #endif
 #ifndef RTG_QUAD_MAX_B
-#define RTG_QUAD_MAX_B 8192   // 2 <= B <= this: k_fbp_quad (16 frames per block, a frame's sub-steps on a lane quad)
+#define RTG_QUAD_MAX_B 4096   // 2 <= B <= this: k_fbp_quad (swept: 16.7 vs 17.2-17.7 us up to 4096, 19.8 vs 17.5 at 8192)
 #endif
 #ifndef RTG_LATENCY_MAX_B
 #define RTG_LATENCY_MAX_B 49152   // 2 <= B <= this: k_fbp_latency5 (swept: faster up to 49152, slower at 65536)

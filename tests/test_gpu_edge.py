@@ -111,6 +111,7 @@ def test_edge_frames_gpu_equals_oracle_every_kernel(gpu, name, kind, precise):
         np.testing.assert_array_equal(_bits(lr_b), _bits(olr)[sel])
         if fbp:
             np.testing.assert_array_equal(_bits(br_b), _bits(obr)[sel])
+    if fbp:
         # one frame per launch (k_fbp_frame1)
         for i in range(n):
             d1, l1, b1 = S.retarget([t[i:i + 1] for t in ins], want_local_rot=True, want_body_rot=True)
