@@ -3,6 +3,7 @@
 // Host-side only: argument validation (mirroring the reference's assertions),
 // handle lifetime, and stream-ordered launches.  Launch entry points never
 // allocate, copy or synchronise, so callers may capture them into hipGraphs.
+#include <immintrin.h>
 #include <hip/hip_runtime.h>
 
 #include <cstdarg>
@@ -530,6 +531,53 @@ int rtg_frame_server_launch(rtg_solver_t s, const float *in, float *dof, float *
     return RTG_OK;
 }
 
+// The inbox's sequence word, stored after everything the host wrote before it and drained to the device: a device
+// inbox (rtg_server_inbox_alloc) is mapped write-combining, so its stores sit in the CPU's write-combining buffers
+// until a fence pushes them out (without one the device saw them 72 us - 7 ms late, tools/bar_probe.hip)
+static void store_inbox_seq(float *in, uint32_t word)
+{
+    _mm_sfence();   // the frame's rows first (write-combined stores are not ordered by x86's TSO)
+    __atomic_store_n(reinterpret_cast<uint32_t *>(in + RTG_SERVER_SEQ_WORD), word, __ATOMIC_RELEASE);
+    _mm_sfence();   // ... and the word itself out now
+}
+
+int rtg_server_inbox_alloc(float **inbox)
+{
+    if (!inbox) return fail(RTG_ERR_INVALID_ARGUMENT, "rtg_server_inbox_alloc: NULL inbox");
+    *inbox = nullptr;
+    void *p = nullptr;
+    const size_t bytes = RTG_SERVER_INBOX_FLOATS * sizeof(float);
+    int rc = hip_check(hipExtMallocWithFlags(&p, bytes, hipDeviceMallocUncached), "hipExtMallocWithFlags(inbox)");
+    if (rc != RTG_OK) return rc;
+    // the host reaches device memory at its own address only on a large-BAR device (MI355X: the whole HBM is in the
+    // BAR; hipPointerGetAttributes reports no separate host pointer for it); otherwise the caller keeps a pinned inbox
+    int dev = 0, large_bar = 0;
+    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&large_bar, hipDeviceAttributeIsLargeBar, dev) != hipSuccess ||
+        !large_bar) {
+        (void)hipGetLastError();
+        (void)hipFree(p);
+        return fail(RTG_ERR_UNSUPPORTED, "rtg_server_inbox_alloc: not a large-BAR device (the host cannot store into its memory)");
+    }
+    // zeroed by the host itself, through the BAR (no device-wide synchronize: a server may be running elsewhere)
+    std::memset(p, 0, bytes);
+    _mm_sfence();
+    *inbox = static_cast<float *>(p);
+    return RTG_OK;
+}
+
+int rtg_server_inbox_free(float *inbox)
+{
+    if (!inbox) return RTG_OK;
+    return hip_check(hipFree(inbox), "hipFree(inbox)");
+}
+
+int rtg_frame_server_signal(float *in, uint32_t word)
+{
+    if (!in) return fail(RTG_ERR_INVALID_ARGUMENT, "rtg_frame_server_signal: NULL inbox");
+    store_inbox_seq(in, word);
+    return RTG_OK;
+}
+
 int rtg_frame_server_post(uint32_t *ctl, uint32_t seq, float *in, const float *body, const float *left_hand,
                           const float *right_hand, const float *dof, const float *local_rot, const float *body_rot,
                           float *dof_dst, float *local_rot_dst, float *body_rot_dst, uint32_t timeout_us)
@@ -542,7 +590,7 @@ int rtg_frame_server_post(uint32_t *ctl, uint32_t seq, float *in, const float *b
     std::memcpy(in, body, 63 * sizeof(float));
     std::memcpy(in + 63, left_hand, 60 * sizeof(float));
     std::memcpy(in + 123, right_hand, 60 * sizeof(float));
-    __atomic_store_n(ctl, seq, __ATOMIC_RELEASE);   // after the rows (the device acquires ctl[0] at system scope)
+    store_inbox_seq(in, seq);   // after the rows (the device acquires the word at system scope)
     struct timespec t0, t;
     bool timed = false;
     for (uint32_t spins = 1; __atomic_load_n(ctl + 1, __ATOMIC_ACQUIRE) != seq; ++spins) {

@@ -1113,10 +1113,11 @@ __global__ __launch_bounds__(320) void k_fbp_quad(SolverConsts C, const float *_
 // ----------------------------------------------------------------------------
 // Per-frame server (the teleop loop without a launch per frame; sim_full_body_teleop.py:109-119 calls the solver
 // once per captured frame).  One resident workgroup of k_fbp_frame1's shape serves FULL_BODY_POS frames from
-// host-mapped memory: the host writes a frame's rows (body | left hand | right hand, AoS) into `in` and then a new
-// sequence number into ctl[0]; thread 0 sees it (system-scope acquire), the tile runs reading `in` and writing
+// its inbox: the host writes a frame's rows (body | left hand | right hand, AoS) into `in` and then a new sequence
+// number into in[RTG_SERVER_SEQ_WORD] (device memory through the BAR, or pinned host memory; rtg.h); thread 0 sees it
+// (system-scope acquire), the tile runs reading `in` and writing
 // dof / local_rot / body_rot straight into host memory, every wave's stores are released at system scope, and
-// thread 0 publishes the sequence number in ctl[1].  The loop ends on ctl[0] == RTG_SERVER_QUIT, or when no new
+// thread 0 publishes the sequence number in ctl[1].  The loop ends on the sequence word == RTG_SERVER_QUIT, or when no new
 // frame arrives for idle_ticks (100 MHz wall clock) -- every wave reaches one of the two -- and sets ctl[2].
 // Hand-over timeouts go to ctl[3] (the launch points C.err there).
 // ----------------------------------------------------------------------------
@@ -1134,7 +1135,8 @@ __global__ __launch_bounds__(320) void k_frame_server(SolverConsts C, const floa
             const uint64_t t0 = wall_clock64();
             uint32_t db;
             for (;;) {
-                db = __hip_atomic_load(ctl, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM);
+                db = __hip_atomic_load(reinterpret_cast<uint32_t *>(const_cast<float *>(in)) + RTG_SERVER_SEQ_WORD, __ATOMIC_ACQUIRE,
+                                       __HIP_MEMORY_SCOPE_SYSTEM);
                 if (db != last) break;
                 if (wall_clock64() - t0 > idle_ticks) {
                     db = RTG_SERVER_QUIT;

@@ -14,7 +14,7 @@ PKG_ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 LIB_PATH = os.environ.get("RTG_LIB", os.path.join(PKG_ROOT, "librtg_hip.so"))
 
 RTG_OK = 0
-ABI_VERSION = 3
+ABI_VERSION = 4
 
 # rtg_layout (input frame-batch layout of the solvers / producers)
 LAYOUT_AOS = 0
@@ -26,6 +26,8 @@ SOLVER_UPPER_BODY = 1
 SOLVER_FULL_BODY_ROT = 2
 SOLVER_BODY_ROT = 3
 SERVER_QUIT = 0xFFFFFFFF   # rtg.h RTG_SERVER_QUIT
+SERVER_INBOX_FLOATS = 256  # rtg.h RTG_SERVER_INBOX_FLOATS (the frame server's inbox)
+SERVER_SEQ_WORD = 192      # rtg.h RTG_SERVER_SEQ_WORD (its sequence number, a uint32 in that float)
 ERR_TIMEOUT = 5            # rtg.h RTG_ERR_TIMEOUT (rtg_frame_server_post)
 SERVER_ENDED = 6           # rtg.h RTG_SERVER_ENDED (rtg_frame_server_post: relaunch, post again)
 
@@ -117,6 +119,9 @@ SIGNATURES = {
     "rtg_frame_server_launch": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, ctypes.c_uint32,
                                         c_void_p]),
     "rtg_frame_server_post": (c_int, [c_void_p, ctypes.c_uint32] + [c_void_p] * 10 + [ctypes.c_uint32]),
+    "rtg_server_inbox_alloc": (c_int, [c_void_p]),
+    "rtg_server_inbox_free": (c_int, [c_void_p]),
+    "rtg_frame_server_signal": (c_int, [c_void_p, ctypes.c_uint32]),
     "rtg_quat_op_f32": (c_int, [c_int, c_void_p, c_void_p, c_void_p, c_int64, c_void_p, c_void_p]),
     "rtg_cal_joint_quat_f32": (c_int, [c_void_p, c_void_p, c_int32, c_int64, c_void_p, c_void_p]),
     "rtg_quat_in_xyz_axis_f32": (c_int, [c_void_p, c_char_p, c_int64, c_void_p, c_void_p]),

@@ -164,7 +164,8 @@ class FrameServer:
     occupies until it ends: close it before a device-wide synchronize.
     """
 
-    def __init__(self, solver: Solver, want_body_rot: bool = False, idle_ms: int = 200, timeout_s: float = 2.0):
+    def __init__(self, solver: Solver, want_body_rot: bool = False, idle_ms: int = 200, timeout_s: float = 2.0,
+                 device_inbox: bool = True):
         dev = require_gpu()
         if dev != solver.device:
             raise ValueError(f"the solver lives on {solver.device}; the current device is {dev}")
@@ -176,13 +177,24 @@ class FrameServer:
         self.tails = _IN_TAILS[solver.kind]
         self._in_offsets = np.cumsum([0] + [int(np.prod(t)) for t in self.tails])
         self.want_body_rot = bool(want_body_rot)
-        self.h_in = torch.zeros(int(self._in_offsets[-1]), dtype=torch.float32).pin_memory()
+        # the inbox (frame + sequence word, rtg.h RTG_SERVER_INBOX_FLOATS): device memory the host stores into through
+        # the BAR when the library can map it (4.0 vs 4.8 us per hand-over, tools/bar_probe.hip), else pinned memory
+        from ._lib import SERVER_INBOX_FLOATS
+        self.h_in = None
+        self._inbox = None
+        p = ctypes.c_void_p()
+        if device_inbox and lib().rtg_server_inbox_alloc(ctypes.byref(p)) == 0 and p.value:
+            self._inbox = p.value
+            self._free_inbox = lib().rtg_server_inbox_free
+            in_ptr = self._inbox
+        else:
+            self.h_in = torch.zeros(SERVER_INBOX_FLOATS, dtype=torch.float32).pin_memory()
+            in_ptr = self.h_in.data_ptr()
         self.h_out = torch.zeros(31 * 4 + 30 + (59 * 4 if want_body_rot else 0), dtype=torch.float32).pin_memory()
         self.h_ctl = torch.zeros(4, dtype=torch.int32).pin_memory()
-        self._h_in_np = self.h_in.numpy()
         self._ctl = self.h_ctl.numpy().view(np.uint32)
         out = self.h_out.data_ptr()
-        self._args = [solver.handle, self.h_in.data_ptr(), out + 4 * 124, out, out + 4 * 154 if want_body_rot else None,
+        self._args = [solver.handle, in_ptr, out + 4 * 124, out, out + 4 * 154 if want_body_rot else None,
                       self.h_ctl.data_ptr(), int(idle_ms)]
         self.stream = torch.cuda.Stream(dev)
         self.timeout_s = float(timeout_s)
@@ -195,7 +207,8 @@ class FrameServer:
         self._timeout_us = int(self.timeout_s * 1e6)
         self._fast = _fast_post.post if _fast_post is not None else None
         self._post_addr = ctypes.cast(self._post, ctypes.c_void_p).value
-        self._ctl_ptr, self._in_ptr = self.h_ctl.data_ptr(), self.h_in.data_ptr()
+        self._ctl_ptr, self._in_ptr = self.h_ctl.data_ptr(), in_ptr
+        self._signal = lib().rtg_frame_server_signal
         self._lr_ptr, self._dof_ptr = out, out + 4 * 124
         self._br_ptr = out + 4 * 154 if want_body_rot else None
         ref = weakref.ref(self)   # end the resident kernel at interpreter exit (before HIP tears down)
@@ -254,14 +267,20 @@ class FrameServer:
 
     def close(self):
         if self._running:
-            self._ctl[0] = self._quit
+            self._signal(self._in_ptr, int(self._quit))
             self.stream.synchronize()
             self._running = False
-            self._ctl[0] = self._ctl[1] = self.seq
+            self._ctl[1] = self.seq   # a relaunch starts from the last posted frame: word == ctl[1]
+            self._signal(self._in_ptr, self.seq)
         fn = getattr(self, "_atexit", None)
         if fn is not None:
             atexit.unregister(fn)
             self._atexit = None
+
+    def _release(self):
+        inbox, self._inbox = getattr(self, "_inbox", None), None
+        if inbox:
+            self._free_inbox(inbox)
 
     def __enter__(self):
         return self
@@ -272,6 +291,7 @@ class FrameServer:
     def __del__(self):
         try:
             self.close()
+            self._release()
         except Exception:
             pass
 

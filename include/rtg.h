@@ -28,7 +28,9 @@
 extern "C" {
 #endif
 
-#define RTG_ABI_VERSION 3   /* 3: frames the reference raises on are marked (rtg_frame_error), the solver error word, ctl[3];
+#define RTG_ABI_VERSION 4   /* 4: the frame server's sequence word lives in its inbox (in[RTG_SERVER_SEQ_WORD]; ctl[0]
+                                  reserved), the inbox may be device memory (rtg_server_inbox_alloc), rtg_frame_server_signal;
+                               3: frames the reference raises on are marked (rtg_frame_error), the solver error word, ctl[3];
                                2: the input-layout argument of rtg_retarget_f32 / rtg_ingest_vtrdyn_f32 / rtg_synth_full_body_f32 */
 
 typedef enum rtg_status {
@@ -235,35 +237,52 @@ int rtg_retarget_f32(rtg_solver_t solver, const float *in0, const float *in1, co
 
 /* Per-frame server for the teleop loop (sim_full_body_teleop.py:109-119 retargets one captured frame per
  * iteration through VtrdynFullBodyPosRetargeter.retarget, full_body_pos_retargeter.py:60-176): launches ONE
- * resident workgroup that serves FULL_BODY_POS frames from host-mapped (pinned) memory without a launch per frame.
- *   in        183 floats: body (21,3) | left hand (20,3) | right hand (20,3), rows as rtg_retarget_f32's AoS inputs
- *   dof (30), local_rot (31,4, may be NULL), body_rot (59,4, may be NULL): the server OWNS these buffers while it
+ * resident workgroup that serves FULL_BODY_POS frames without a launch per frame.
+ *   in        the server's inbox, RTG_SERVER_INBOX_FLOATS floats: the frame in floats 0..182 -- body (21,3) | left
+ *             hand (20,3) | right hand (20,3), rows as rtg_retarget_f32's AoS inputs -- and the frame sequence number
+ *             (uint32) in float RTG_SERVER_SEQ_WORD, stored by the host after the frame's rows.  Either device memory
+ *             from rtg_server_inbox_alloc (the host stores into it through the PCIe BAR: the faster hand-over) or
+ *             device-accessible pinned host memory.
+ *   dof (30), local_rot (31,4, may be NULL), body_rot (59,4, may be NULL): pinned host memory the server OWNS while it
  *             runs.  The dof row and the frame-dependent local_rot / body_rot rows are written per frame; the 73
  *             rows that never change (local_rot's fixed links, body_rot's identity rows) are written once per
  *             launch and again after a frame the reference raises on.  A client that clears or edits these
  *             buffers between frames must copy the rows out instead (rtg_frame_server_post does) or relaunch.
- *   ctl       4 x uint32: [0] frame sequence number, written by the host after the frame's inputs;
+ *   ctl       4 x uint32, pinned host memory: [0] reserved (ABI <= 3: the sequence number);
  *             [1] the last sequence number served, written by the device after that frame's outputs;
  *             [2] set to 1 by the device when the server has ended;
  *             [3] the server's error word (RTG_DEVERR_*), set before [1] of the frame it concerns.
- *             Zero ctl[1..3] before the launch.
- * Writing RTG_SERVER_QUIT into ctl[0] ends the server; so does idle_ms (1..60000) without a new frame.  All
- * buffers must be device-accessible host memory (hipHostMalloc / pinned).  The stream is occupied until the
- * server ends.  The values in the buffers after a frame is served (ctl[1]) are bit-identical to rtg_retarget_f32's at
- * B = 1. */
+ *             Zero ctl[1..3] before the launch, and have the inbox's sequence word equal ctl[1] (both 0 at first).
+ * Storing RTG_SERVER_QUIT as the sequence number (rtg_frame_server_signal) ends the server; so does idle_ms
+ * (1..60000) without a new frame.  The stream is occupied until the server ends.  The values in the buffers after a
+ * frame is served (ctl[1]) are bit-identical to rtg_retarget_f32's at B = 1. */
 #define RTG_SERVER_QUIT 0xFFFFFFFFu
+#define RTG_SERVER_INBOX_FLOATS 256
+#define RTG_SERVER_SEQ_WORD 192
 int rtg_frame_server_launch(rtg_solver_t solver, const float *in, float *dof, float *local_rot, float *body_rot,
                             uint32_t *ctl, uint32_t idle_ms, rtg_stream_t stream);
 
+/* A frame-server inbox in device memory that the host can store into (hipExtMallocWithFlags, uncached; the CPU
+ * reaches it through the PCIe BAR): RTG_SERVER_INBOX_FLOATS floats, zeroed.  Host stores into it are
+ * write-combined: rtg_frame_server_post / rtg_frame_server_signal drain them (sfence) in order.  Free with
+ * rtg_server_inbox_free.  A 184-float ping-pong through it takes 4.0 us against 4.8 us through pinned host memory
+ * on MI355X (tools/bar_probe.hip). */
+int rtg_server_inbox_alloc(float **inbox);
+int rtg_server_inbox_free(float *inbox);
+
+/* Stores `word` as the inbox's sequence number and drains it to the device (host only, no HIP call): RTG_SERVER_QUIT
+ * ends a running server; after it has ended, store ctl[1] back before a relaunch. */
+int rtg_frame_server_signal(float *in, uint32_t word);
+
 /* One frame through a running rtg_frame_server_launch server, on the host alone (no HIP call): the whole per-frame
  * round trip of the teleop loop (sim_full_body_teleop.py:115-119) in one C call.  Copies the frame's rows into the
- * server's pinned `in` (body (21,3) | left hand (20,3) | right hand (20,3)), posts `seq` (!= the last one posted,
- * != RTG_SERVER_QUIT) in ctl[0] after them, spins until the device publishes it in ctl[1], then copies the pinned
- * outputs the server writes (dof 30, local_rot 124, body_rot 236 floats) into the *_dst buffers that are not NULL.
- * Returns RTG_OK; RTG_SERVER_ENDED if the server ended (idle_ms) before it took the frame -- relaunch it and post
- * the same seq again; RTG_ERR_TIMEOUT after timeout_us (the frame may still be served later); RTG_ERR_DEVICE if
- * the server set its error word (ctl[3]) while serving the frame (the outputs are copied anyway; the word is
- * cleared). */
+ * server's inbox `in` (body (21,3) | left hand (20,3) | right hand (20,3)), stores `seq` (!= the last one posted,
+ * != RTG_SERVER_QUIT) as its sequence number after them, spins until the device publishes it in ctl[1], then copies
+ * the pinned outputs the server writes (dof 30, local_rot 124, body_rot 236 floats) into the *_dst buffers that are
+ * not NULL.  Returns RTG_OK; RTG_SERVER_ENDED if the server ended (idle_ms) before it took the frame -- relaunch it
+ * and post the same seq again; RTG_ERR_TIMEOUT after timeout_us (the frame may still be served later);
+ * RTG_ERR_DEVICE if the server set its error word (ctl[3]) while serving the frame (the outputs are copied anyway;
+ * the word is cleared). */
 int rtg_frame_server_post(uint32_t *ctl, uint32_t seq, float *in, const float *body, const float *left_hand,
                           const float *right_hand, const float *dof, const float *local_rot, const float *body_rot,
                           float *dof_dst, float *local_rot_dst, float *body_rot_dst, uint32_t timeout_us);

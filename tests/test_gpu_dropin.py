@@ -239,7 +239,8 @@ def test_per_frame_graph_matches_batched(gpu):
 
 def test_frame_server_matches_batched(gpu):
     """The resident per-frame server (rtg_frame_server_launch, rtg.realtime.FrameServer) serves frame after frame
-    with exactly the batched solve's rows, relaunches itself after an idle exit, and ends on close()."""
+    with exactly the batched solve's rows, relaunches itself after an idle exit, and ends on close() -- with its inbox
+    in device memory (rtg_server_inbox_alloc) and in pinned host memory."""
     import time
 
     from retarget.retarget_solver import VtrdynFullBodyPosRetargeter
@@ -251,16 +252,18 @@ def test_frame_server_matches_batched(gpu):
     n = 48
     lr_b, dof_b, br_b = hu.retarget_batch(torch.from_numpy(g["body"][:n]), torch.from_numpy(g["lh"][:n]),
                                           torch.from_numpy(g["rh"][:n]), want_body_rot=True)
-    with FrameServer(hu.solver, want_body_rot=True, idle_ms=20) as fs:
-        for i in range(n):
-            if i == n // 2:
-                time.sleep(0.1)   # past idle_ms: the server has ended; the next call relaunches it
-                assert fs._ctl[2] == 1
-            lr, dof, br = fs(g["body"][i], g["lh"][i], g["rh"][i])
-            np.testing.assert_array_equal(dof.numpy(), dof_b[i].numpy())
-            np.testing.assert_array_equal(lr.numpy(), lr_b[i].numpy())
-            np.testing.assert_array_equal(br.numpy(), br_b[i].numpy())
-    assert not fs._running and fs._ctl[2] == 1
+    for device_inbox in (True, False):   # the inbox in device memory through the BAR (MI355X), or pinned
+        with FrameServer(hu.solver, want_body_rot=True, idle_ms=20, device_inbox=device_inbox) as fs:
+            assert (fs._inbox is not None) == device_inbox
+            for i in range(n):
+                if i == n // 2:
+                    time.sleep(0.1)   # past idle_ms: the server has ended; the next call relaunches it
+                    assert fs._ctl[2] == 1
+                lr, dof, br = fs(g["body"][i], g["lh"][i], g["rh"][i])
+                np.testing.assert_array_equal(dof.numpy(), dof_b[i].numpy())
+                np.testing.assert_array_equal(lr.numpy(), lr_b[i].numpy())
+                np.testing.assert_array_equal(br.numpy(), br_b[i].numpy())
+        assert not fs._running and fs._ctl[2] == 1
     with pytest.raises(ValueError):
         FrameServer(hu.solver, want_body_rot=True)(g["body"][0], g["lh"][0])
 

@@ -287,24 +287,26 @@ def test_serializable_json_and_npy_roundtrip(tmp_path):
 
 def test_frame_server_post_protocol_on_the_host():
     """rtg_frame_server_post (the teleop per-frame round trip in one C call) against a host thread standing in for
-    k_frame_server: the frame's rows land in `in` before ctl[0] = seq, the outputs are copied out only after
-    ctl[1] = seq, a server that ended before taking the frame reports RTG_SERVER_ENDED, a silent one times out."""
+    k_frame_server: the frame's rows land in the inbox `in` before its sequence word (in[RTG_SERVER_SEQ_WORD]) = seq,
+    the outputs are copied out only after ctl[1] = seq, a server that ended before taking the frame reports
+    RTG_SERVER_ENDED, a silent one times out; rtg_frame_server_signal stores the word alone."""
     import threading
     import time
     from rtg import _lib
     lib = _lib.lib()
     vp = ctypes.c_void_p
     ctl = np.zeros(4, np.uint32)
-    inb = np.zeros(183, np.float32)
+    inb = np.zeros(_lib.SERVER_INBOX_FLOATS, np.float32)
+    word = inb[_lib.SERVER_SEQ_WORD:_lib.SERVER_SEQ_WORD + 1].view(np.uint32)
     out = np.zeros(390, np.float32)   # local_rot 124 | dof 30 | body_rot 236, as FrameServer lays out its pinned buffer
     rng = np.random.default_rng(5)
     body, lh, rh = (rng.normal(size=s).astype(np.float32) for s in ((21, 3), (20, 3), (20, 3)))
     seen = {}
 
     def device(seq):
-        while ctl[0] != seq:
+        while word[0] != seq:
             time.sleep(0)
-        seen["in"] = inb.copy()
+        seen["in"] = inb[:183].copy()
         out[:] = np.arange(390, dtype=np.float32) + seq
         ctl[1] = seq
 
@@ -331,6 +333,8 @@ def test_frame_server_post_protocol_on_the_host():
     assert post(9, timeout_us=20_000)[0] == _lib.ERR_TIMEOUT
     assert time.perf_counter() - t0 < 5.0
     assert b"not served" in lib.rtg_last_error()
+    assert lib.rtg_frame_server_signal(vp(inb.ctypes.data), _lib.SERVER_QUIT) == 0 and word[0] == _lib.SERVER_QUIT
+    assert lib.rtg_frame_server_signal(None, 1) == 1
     assert lib.rtg_frame_server_post(None, 1, *([None] * 10), 10) == 1
     assert lib.rtg_frame_server_post(vp(ctl.ctypes.data), _lib.SERVER_QUIT, *([vp(inb.ctypes.data)] * 5),
                                      *([None] * 5), 10) == 1

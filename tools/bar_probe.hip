@@ -2,7 +2,7 @@
 // server's hand-over cost when its inbox lives there instead of in pinned host memory?
 //
 //   hipcc --offload-arch=gfx950 -O2 tools/bar_probe.hip -o tools/bar_probe
-//   tools/bar_probe <mode>     mode: fg (hipExtMallocWithFlags hipDeviceMallocFinegrained)
+//   tools/bar_probe <mode> [sfence]   mode: fg (hipExtMallocWithFlags hipDeviceMallocFinegrained)
 //                                    uc (hipExtMallocWithFlags hipDeviceMallocUncached)
 //                                    host (hipHostMalloc, the server's current inbox)
 //
@@ -17,6 +17,7 @@
 #include <cstring>
 #include <vector>
 #include <algorithm>
+#include <immintrin.h>
 
 #define CK(x) do { hipError_t e_ = (x); if (e_ != hipSuccess) { printf("{\"error\": \"%s: %s\"}\n", #x, hipGetErrorString(e_)); return 1; } } while (0)
 
@@ -58,13 +59,14 @@ __global__ void k_pong(const float *in, volatile uint32_t *in_seq, float *out, u
 int main(int argc, char **argv)
 {
     const char *mode = argc > 1 ? argv[1] : "host";
+    const bool fence = argc > 2 && !strcmp(argv[2], "sfence");
     const int frames = 2000;
     int dev = 0;
     CK(hipSetDevice(dev));
     int large_bar = -1, direct_managed = -1, pageable = -1;
+    (void)hipDeviceGetAttribute(&large_bar, hipDeviceAttributeIsLargeBar, dev);
     (void)hipDeviceGetAttribute(&direct_managed, hipDeviceAttributeDirectManagedMemAccessFromHost, dev);
     (void)hipDeviceGetAttribute(&pageable, hipDeviceAttributePageableMemoryAccess, dev);
-    (void)large_bar;
     void *inbox = nullptr;   // 184 floats + the sequence word at float 192 (its own 64-byte piece)
     const size_t inbox_bytes = 256 * sizeof(float);
     if (!strcmp(mode, "fg")) CK(hipExtMallocWithFlags(&inbox, inbox_bytes, hipDeviceMallocFinegrained));
@@ -75,6 +77,13 @@ int main(int argc, char **argv)
     CK(hipHostMalloc((void **)&h_out, 64 * sizeof(float), hipHostMallocMapped));
     CK(hipHostMalloc((void **)&h_oseq, 64, hipHostMallocMapped));
     *h_oseq = 0;
+    {   // what the runtime reports for the inbox (rtg_server_inbox_alloc's mapping test reads the same record)
+        hipPointerAttribute_t a;
+        const hipError_t e = hipPointerGetAttributes(&a, inbox);
+        printf("{\"attributes\": {\"rc\": %d, \"type\": %d, \"ptr\": \"%p\", \"hostPointer\": \"%p\", "
+               "\"devicePointer\": \"%p\", \"isManaged\": %d, \"allocationFlags\": %u}}\n",
+               (int)e, (int)a.type, inbox, a.hostPointer, a.devicePointer, (int)a.isManaged, a.allocationFlags);
+    }
     float *fin = static_cast<float *>(inbox);
     uint32_t *iseq = reinterpret_cast<uint32_t *>(fin + 192);
     // the host store that faults if the CPU cannot reach this memory
@@ -99,7 +108,9 @@ int main(int argc, char **argv)
     for (uint32_t seq = 1; seq <= (uint32_t)frames; ++seq) {
         const auto t0 = std::chrono::steady_clock::now();
         for (int i = 0; i < 184; ++i) fin[i] = (float)(i + seq);
+        if (fence) _mm_sfence();   // device memory is mapped write-combining: drain the frame before the word
         __atomic_store_n(iseq, seq, __ATOMIC_RELEASE);
+        if (fence) _mm_sfence();   // ... and the word itself out of the write-combining buffer
         long spins = 0;
         while (__atomic_load_n(h_oseq, __ATOMIC_ACQUIRE) != seq) {
             if (++spins > 2000000000L) { ok = false; break; }
@@ -112,8 +123,8 @@ int main(int argc, char **argv)
     CK(hipStreamSynchronize(st));
     std::sort(us.begin(), us.end());
     const double med = us.empty() ? -1 : us[us.size() / 2], p99 = us.empty() ? -1 : us[us.size() * 99 / 100];
-    printf("{\"mode\": \"%s\", \"ok\": %s, \"frames\": %zu, \"median_us\": %.2f, \"p99_us\": %.2f, "
-           "\"direct_managed_access\": %d, \"pageable_access\": %d}\n",
-           mode, ok ? "true" : "false", us.size(), med, p99, direct_managed, pageable);
+    printf("{\"mode\": \"%s%s\", \"ok\": %s, \"frames\": %zu, \"median_us\": %.2f, \"p99_us\": %.2f, "
+           "\"direct_managed_access\": %d, \"pageable_access\": %d, \"large_bar\": %d}\n",
+           mode, fence ? "+sfence" : "", ok ? "true" : "false", us.size(), med, p99, direct_managed, pageable, large_bar);
     return ok ? 0 : 2;
 }

@@ -82,12 +82,15 @@ def latency():
     fg = FrameGraph(S, want_body_rot=False)
     fsrv = FrameServer(S, want_body_rot=False)
     fsrv_br = FrameServer(S, want_body_rot=True)
+    fsrv_pin = FrameServer(S, want_body_rot=False, device_inbox=False)   # round 4's inbox: pinned host memory
     for name, fn in (("dropin_retarget_per_frame", lambda: hu.retarget(fb, fl, fr)),
                      ("frame_server_dof_local_rot_body_rot", lambda: fsrv_br(fb, fl, fr)),
                      ("dropin_batch_of_one_no_graph",
                       lambda: hu.retarget_batch(fb[None], fl[None], fr[None], want_body_rot=True)),
                      ("frame_graph_dof_local_rot", lambda: fg(fb, fl, fr)),
-                     ("frame_server_dof_local_rot", lambda: fsrv(fb, fl, fr))):
+                     ("frame_server_dof_local_rot", lambda: fsrv(fb, fl, fr)),
+                     ("frame_server_dof_local_rot_pinned_inbox", lambda: fsrv_pin(fb, fl, fr)),
+                     ("frame_server_dof_local_rot_again", lambda: fsrv(fb, fl, fr))):
         for _ in range(20):
             fn()
         ts = []
@@ -98,8 +101,10 @@ def latency():
         out[name] = {"median_us": float(np.median(ts) * 1e6), "p99_us": float(np.quantile(ts, 0.99) * 1e6)}
     a, b = fg(fb, fl, fr), fsrv(fb, fl, fr)
     out["frame_server_bits_equal_frame_graph"] = bool(torch.equal(a[0], b[0]) and torch.equal(a[1], b[1]))
+    out["frame_server_inbox_in_device_memory"] = fsrv._inbox is not None
     fsrv.close()
     fsrv_br.close()
+    fsrv_pin.close()
     hu.close()
     return out
 
