@@ -148,6 +148,20 @@ RTG_DEV void chunk_to_lds(const ChunkRegs &r, float *lds, int nfr, int nC)
     RTG_REP8(RTG_ST)
 #undef RTG_ST
 }
+// The output rows as streaming (non-temporal) stores when RTG_FK_NT_STORE: they are never read back by the kernel,
+// and in the L2 they would evict the input lines a later window (or chunk) of the same rows still has to read
+typedef float f4v __attribute__((ext_vector_type(4)));
+RTG_DEV void out_st4(float *gp, const float *lp)
+{
+    const f4v v = *reinterpret_cast<const f4v *>(lp);
+    if (RTG_FK_NT_STORE) __builtin_nontemporal_store(v, reinterpret_cast<f4v *>(gp));
+    else *reinterpret_cast<f4v *>(gp) = v;
+}
+RTG_DEV void out_st1(float *gp, float v)
+{
+    if (RTG_FK_NT_STORE) __builtin_nontemporal_store(v, gp);
+    else *gp = v;
+}
 template <int W>
 RTG_DEV void chunk_store(float *__restrict__ g, const float *lds, int pitch, int64_t f0, int nfr, int J, int c0, int nC)
 {
@@ -157,10 +171,10 @@ RTG_DEV void chunk_store(float *__restrict__ g, const float *lds, int pitch, int
         float *gp = g + ((f0 + fr) * J + c0 + k) * W;
         const float *lp = lds + fr * pitch + k * W;
         if (W == 4) {
-            *reinterpret_cast<float4 *>(gp) = *reinterpret_cast<const float4 *>(lp);
+            out_st4(gp, lp);
         } else {
 #pragma unroll
-            for (int c = 0; c < W; ++c) gp[c] = lp[c];
+            for (int c = 0; c < W; ++c) out_st1(gp + c, lp[c]);
         }
     };
     if (nfr == kFkTile && nC == kFkChunk) {   // full window: unpredicated, LDS reads batch ahead of the stores
@@ -187,7 +201,7 @@ RTG_DEV void chunk_store_n(float *__restrict__ g, const float *lds, int pitch, i
             float *gp = g + ((f0 + fr) * J + c0 + k) * W;
             const float *lp = lds + fr * pitch + k * W;
 #pragma unroll
-            for (int c = 0; c < W; ++c) gp[c] = lp[c];
+            for (int c = 0; c < W; ++c) out_st1(gp + c, lp[c]);
         }
     }
 }
@@ -481,7 +495,9 @@ RTG_DEV void line_store(float *__restrict__ rows, const float *win, int m, int J
             float *gp = rows + (int64_t)W * P.g;
             const float *lp = win + P.fr * kRotPitch + P.sub * W;
             if (W == 4) {
-                *reinterpret_cast<float4 *>(gp) = *reinterpret_cast<const float4 *>(lp);
+                const f4v v = *reinterpret_cast<const f4v *>(lp);
+                if (RTG_LINE_NT_STORE) __builtin_nontemporal_store(v, reinterpret_cast<f4v *>(gp));   // A/B knob
+                else *reinterpret_cast<f4v *>(gp) = v;
             } else {
 #pragma unroll
                 for (int c = 0; c < W; ++c) gp[c] = lp[c];

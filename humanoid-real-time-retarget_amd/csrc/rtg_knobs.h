@@ -65,6 +65,22 @@
 #ifndef RTG_VEL_IEEE_DIV
 #define RTG_VEL_IEEE_DIV 0   // A/B knob (same values): the velocity tiles' quotients by dt as IEEE divisions (round 4)
 #endif
+#ifndef RTG_FK_NT_STORE
+#define RTG_FK_NT_STORE 0   // A/B knob (same values): the windowed FK kernels' output rows as non-temporal stores
+                            // (measured 200 vs 120 us on Hu FK: the 16-B-aligned row pieces straddle lines)
+#endif
+#ifndef RTG_DOF_NT_STORE
+#define RTG_DOF_NT_STORE 1   // A/B knob (same values): the solvers' DOF rows (whole 128-B lines) as non-temporal stores
+                             // (headline 101.3 vs 104.5 us SoA, 114.4 vs 117.7 AoS; profiles/r05/nt/)
+#endif
+#ifndef RTG_VEL_NT_STORE
+#define RTG_VEL_NT_STORE 0   // A/B knob (same values): the velocity tiles' output rows as non-temporal stores
+                             // (measured slower: linear 66 vs 63 us, angular 117 vs 113)
+#endif
+#ifndef RTG_LINE_NT_STORE
+#define RTG_LINE_NT_STORE 0   // A/B knob (same values): the line-synchronous inverse FK's whole-line stores non-temporal
+                              // (measured neutral: 74-76 vs 74-79 us)
+#endif
 #ifndef RTG_EXP_NO_RARE
 #define RTG_EXP_NO_RARE 0   // measurement knob, a bit mask: the rare-case branches of cr_sqrt (1) / cr_acos (2) /
 #endif                      // cr_sincos (4) / mulr (8) / sqrt_clamp_rcp (16) removed (wrong answers on rare inputs)

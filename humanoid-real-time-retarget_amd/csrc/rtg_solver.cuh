@@ -217,9 +217,12 @@ RTG_DEV void store_dof_rows(float *__restrict__ dst, const float *src, int64_t n
         return src[rr * kDofStride + (i - rr * 30)];
     };
     const int nvec = nvals >> 2;
+    typedef float f4v __attribute__((ext_vector_type(4)));
     for (int v = t; v < nvec; v += nthr) {
         const int i = v << 2;
-        *reinterpret_cast<float4 *>(dst + i) = make_float4(at(i), at(i + 1), at(i + 2), at(i + 3));
+        const f4v q = {at(i), at(i + 1), at(i + 2), at(i + 3)};
+        if (RTG_DOF_NT_STORE) __builtin_nontemporal_store(q, reinterpret_cast<f4v *>(dst + i));   // A/B knob
+        else *reinterpret_cast<f4v *>(dst + i) = q;
     }
     for (int i = (nvec << 2) + t; i < nvals; i += nthr) dst[i] = at(i);
 }
