@@ -6,6 +6,9 @@
 #pragma once
 
 // ---- used by rtg_solver.cuh
+#ifndef RTG_SIDES_TILES
+#define RTG_SIDES_TILES 2   // 64-frame tiles (two waves each) per k_solve_sides block
+#endif
 #ifndef RTG_SIDES_WAVES
 #define RTG_SIDES_WAVES 1   // min waves per SIMD for the side kernel (1: the compiler picks; measured best)
 #endif

@@ -235,7 +235,9 @@ RTG_DEV void store_dof_rows(float *__restrict__ dst, const float *src, int64_t n
 // never diverges, and each wave runs about half the frame program -- twice the waves in flight, about half the
 // per-frame latency, the same arithmetic per value.
 // ----------------------------------------------------------------------------
-constexpr int kSideFrames = 128;   // frames per 256-thread block
+constexpr int kSideTiles = RTG_SIDES_TILES;        // 64-frame tiles per block (two waves each)
+constexpr int kSideThreads = 128 * kSideTiles;
+constexpr int kSideFrames = 64 * kSideTiles;       // frames per block
 
 // torso fit R10 (full_body_pos_retargeter.py:69-70 / retarget_solver.py:49-50)
 template <typename View, typename Hook = NoHook>
@@ -413,7 +415,7 @@ RTG_DEV void lds_wait(int *flag, uint32_t *err)
 }
 
 template <int KIND, bool PRECISE, bool SOA>
-__global__ __launch_bounds__(256, RTG_SIDES_WAVES) void k_solve_sides(SolverConsts C, const float *__restrict__ in0,
+__global__ __launch_bounds__(kSideThreads, RTG_SIDES_WAVES) void k_solve_sides(SolverConsts C, const float *__restrict__ in0,
                                                      const float *__restrict__ in1, const float *__restrict__ in2,
                                                      const float *__restrict__ in3, int64_t B,
                                                      float *__restrict__ dof, float *__restrict__ local_rot,
@@ -421,7 +423,7 @@ __global__ __launch_bounds__(256, RTG_SIDES_WAVES) void k_solve_sides(SolverCons
 {
     __shared__ float sdof[kSideFrames * kDofStride];
     __shared__ float4 storso[kSideFrames];   // FULL_BODY_POS: R10 left -> right wave, then the left chain right -> left
-    __shared__ float2 sst[2 * 14 * 64];      // exp-map stash, [tile][slot][lane]
+    __shared__ float2 sst[kSideTiles * 14 * 64];   // exp-map stash, [tile][slot][lane]
     __shared__ uint8_t sstat[2][kSideFrames];   // each side's frame-status bits (kSt*)
     const int w = threadIdx.x >> 6, side = w & 1, lane = threadIdx.x & 63;
     const int r = (w >> 1) * 64 + lane;   // tile row
@@ -606,7 +608,7 @@ __global__ __launch_bounds__(256, RTG_SIDES_WAVES) void k_solve_sides(SolverCons
             __syncthreads();
         }
         const int64_t nrows = (B - f0) < kSideFrames ? (B - f0) : kSideFrames;
-        store_dof_rows(dof + f0 * 30, sdof, nrows, threadIdx.x, 256);
+        store_dof_rows(dof + f0 * 30, sdof, nrows, threadIdx.x, kSideThreads);
         TS(12);
     }
 }
@@ -1194,7 +1196,7 @@ static void launch_kind(const SolverConsts &C, const float *in0, const float *in
             return;
         }
     }
-    hipLaunchKernelGGL((k_solve_sides<KIND, PRECISE, SOA>), dim3(grid_for(B, kSideFrames)), dim3(256), 0, s, C, in0,
+    hipLaunchKernelGGL((k_solve_sides<KIND, PRECISE, SOA>), dim3(grid_for(B, kSideFrames)), dim3(kSideThreads), 0, s, C, in0,
                        in1, in2, in3, B, dof, local_rot, body_rot);
 }
 
