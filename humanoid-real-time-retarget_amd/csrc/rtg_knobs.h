@@ -9,6 +9,9 @@
 #ifndef RTG_SIDES_TILES
 #define RTG_SIDES_TILES 2   // 64-frame tiles (two waves each) per k_solve_sides block
 #endif
+#ifndef RTG_SIDES_SPLIT_READOUT
+#define RTG_SIDES_SPLIT_READOUT 0   // FULL_BODY_POS side kernel: the left wave also reads out the right chain's slots
+#endif
 #ifndef RTG_SIDES_WAVES
 #define RTG_SIDES_WAVES 1   // min waves per SIMD for the side kernel (1: the compiler picks; measured best)
 #endif

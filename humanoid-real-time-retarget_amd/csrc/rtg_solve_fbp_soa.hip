@@ -1,5 +1,5 @@
-// rtg_solve_fbp_soa.hip -- VtrdynFullBodyPosRetargeter kernels (SOA inputs): the side kernel, the
-// small-batch latency kernel.
+// rtg_solve_fbp_soa.hip -- VtrdynFullBodyPosRetargeter kernels (SOA inputs): the side kernel (the small-batch
+// kernels are in rtg_solve_fbp_small.hip).
 #include "rtg_solver.cuh"
 
 namespace rtg {

@@ -461,8 +461,8 @@ __global__ __launch_bounds__(kSideThreads, RTG_SIDES_WAVES) void k_solve_sides(S
         // Euler split / gripper -- 1.5 SVD-equivalents per wave.  Two per-tile LDS flags hand R10 (left -> right)
         // and the left chain (right -> left) over, so each wave waits only for what it reads; a third counts the
         // waves out, and the second one to finish stores the tile's DOF rows while the first exits.
-        __shared__ int sflag[2][3];   // per tile: [0] R10 ready, [1] left chain ready, [2] waves done
-        if (threadIdx.x < 6) (&sflag[0][0])[threadIdx.x] = 0;
+        __shared__ int sflag[2][4];   // per tile: [0] R10 ready, [1] left chain ready, [2] waves done, [3] right chain ready
+        if (threadIdx.x < 8) (&sflag[0][0])[threadIdx.x] = 0;
         __syncthreads();
         int *const fl = sflag[w >> 1];
         auto hook1 = [&](int k) { TS(1 + k); };    // 1: first fit's A formed (its points loaded), 2: its SVD + R done
@@ -503,6 +503,7 @@ __global__ __launch_bounds__(kSideThreads, RTG_SIDES_WAVES) void k_solve_sides(S
             }
             lds_signal(&fl[1]);   // the left chain and its exp-map slots 0-3 are in LDS
             if (live) chain = fbp_arm<1>(C, apR, R10, E);
+            if (RTG_SIDES_SPLIT_READOUT) lds_signal(&fl[3]);   // the right chain's exp-map slots 7-10 are in LDS
         } else if (live) {
             emit_fixed_links(E);
             bool nan = false;
@@ -524,8 +525,19 @@ __global__ __launch_bounds__(kSideThreads, RTG_SIDES_WAVES) void k_solve_sides(S
         }
         TS(7);
         // exp-map read-out: the left wave reads slots 0-6 (the left chain's 0-3, written by the right wave before
-        // the flag, and its own wrist's 4-6), the right wave 7-13 (all its own)
-        if (live) E.finalize(side ? 7 : 0, 7);
+        // the flag, and its own wrist's 4-6), the right wave 7-13 (all its own).  RTG_SIDES_SPLIT_READOUT: the left
+        // wave (the shorter program) also reads the right chain's slots 7-10, after the right wave's flag for them
+        if (RTG_SIDES_SPLIT_READOUT) {
+            if (side) {
+                if (live) E.finalize(11, 3);
+            } else {
+                if (live) E.finalize(0, 7);
+                lds_wait(&fl[3], C.err);
+                if (live) E.finalize(7, 4);
+            }
+        } else if (live) {
+            E.finalize(side ? 7 : 0, 7);
+        }
         st = side ? ((fit1_nan ? kStRightSvd : 0u) | (euler_refused ? kStRightEuler : 0u))
                   : ((fit1_nan ? kStTorsoSvd : 0u) | (fit2_nan ? kStLeftSvd : 0u) | (euler_refused ? kStLeftEuler : 0u));
         sstat[side][r] = (uint8_t)st;
@@ -1175,24 +1187,34 @@ __global__ __launch_bounds__(320) void k_frame_server(SolverConsts C, const floa
 // Kernel choice by batch size (measured crossovers).  Compile-time choices are `if constexpr`, so a
 // TU instantiates only the kernels it can launch (rtg_solve_fbp_aos.hip / rtg_solve_fbp_soa.hip /
 // rtg_solve_other.hip compile in parallel).
+// FULL_BODY_POS at B <= RTG_LATENCY_MAX_B: k_fbp_frame1 / k_fbp_quad / k_fbp_latency5, instantiated in their own TU
+// (rtg_solve_fbp_small.hip), which the Makefile compiles with the ILP-first scheduler: one or two waves per SIMD run
+// these latency-bound chains, where interleaving independent work inside a wave pays (measured 2 % at B = 1 and
+// 4096), unlike the throughput-bound side kernel (round 4: max-ilp raised it to 137 VGPRs, 3 waves/SIMD, slower)
+hipError_t launch_fbp_small(int precise, bool soa, const SolverConsts &C, const float *in0, const float *in1,
+                            const float *in2, int64_t B, float *dof, float *local_rot, float *body_rot, hipStream_t s);
+template <bool PRECISE, bool SOA>
+static void launch_fbp_small_kind(const SolverConsts &C, const float *in0, const float *in1, const float *in2,
+                                  int64_t B, float *dof, float *local_rot, float *body_rot, hipStream_t s)
+{
+    if (B == 1) {
+        hipLaunchKernelGGL((k_fbp_frame1<PRECISE>), dim3(1), dim3(320), 0, s, C, in0, in1, in2, dof, local_rot,
+                           body_rot);
+    } else if (B <= RTG_QUAD_MAX_B) {
+        hipLaunchKernelGGL((k_fbp_quad<PRECISE, SOA>), dim3(grid_for(B, kQuadFrames)), dim3(320), 0, s, C, in0,
+                           in1, in2, B, dof, local_rot, body_rot);
+    } else {
+        hipLaunchKernelGGL((k_fbp_latency5<PRECISE, SOA>), dim3(grid_for(B, kLatFrames)), dim3(320), 0, s, C,
+                           in0, in1, in2, B, dof, local_rot, body_rot);
+    }
+}
 template <int KIND, bool PRECISE, bool SOA>
 static void launch_kind(const SolverConsts &C, const float *in0, const float *in1, const float *in2,
                         const float *in3, int64_t B, float *dof, float *local_rot, float *body_rot, hipStream_t s)
 {
     if constexpr (KIND == RTG_SOLVER_FULL_BODY_POS) {
-        if (B == 1) {
-            hipLaunchKernelGGL((k_fbp_frame1<PRECISE>), dim3(1), dim3(320), 0, s, C, in0, in1, in2, dof, local_rot,
-                               body_rot);
-            return;
-        }
-        if (B <= RTG_QUAD_MAX_B) {
-            hipLaunchKernelGGL((k_fbp_quad<PRECISE, SOA>), dim3(grid_for(B, kQuadFrames)), dim3(320), 0, s, C, in0,
-                               in1, in2, B, dof, local_rot, body_rot);
-            return;
-        }
         if (B <= RTG_LATENCY_MAX_B) {
-            hipLaunchKernelGGL((k_fbp_latency5<PRECISE, SOA>), dim3(grid_for(B, kLatFrames)), dim3(320), 0, s, C,
-                               in0, in1, in2, B, dof, local_rot, body_rot);
+            (void)launch_fbp_small(PRECISE, SOA, C, in0, in1, in2, B, dof, local_rot, body_rot, s);   // errors: hipGetLastError
             return;
         }
     }

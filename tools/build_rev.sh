@@ -10,8 +10,11 @@ git -C "$repo" archive "$rev" humanoid-real-time-retarget_amd/csrc include | tar
 cd "$tmp/humanoid-real-time-retarget_amd/csrc"
 FLAGS="--offload-arch=gfx950 -O3 -std=c++17 -fPIC -ffp-contract=off -fhip-fp32-correctly-rounded-divide-sqrt -fno-fast-math -I../../include $*"
 objs=""
-for t in rtg_solve_fbp_aos rtg_solve_fbp_soa rtg_solve_other rtg_fk rtg_ops; do
-  /opt/rocm/bin/hipcc $FLAGS -c $t.hip -o $t.o &
+# the revision's own TU list and per-TU flags (rtg_solve_fbp_small exists from round 5 on, with SMALL_FLAGS)
+for f in rtg_*.hip; do
+  t=${f%.hip}
+  extra=""; [ "$t" = rtg_solve_fbp_small ] && extra="-mllvm -amdgpu-sched-strategy=max-ilp"
+  /opt/rocm/bin/hipcc $FLAGS $extra -c $t.hip -o $t.o &
   objs="$objs $t.o"
 done
 /opt/rocm/bin/hipcc $FLAGS -x hip -c rtg_api.cpp -o rtg_api.o &

@@ -7,12 +7,14 @@ set -eu
 cd "$(dirname "$0")/../humanoid-real-time-retarget_amd/csrc"
 mkdir -p ../variants
 FLAGS="--offload-arch=gfx950 -O3 -std=c++17 -fPIC -ffp-contract=off -fhip-fp32-correctly-rounded-divide-sqrt -fno-fast-math -I../../include"
-TUS="rtg_solve_fbp_aos rtg_solve_fbp_soa rtg_solve_other rtg_fk rtg_ops"
+TUS="rtg_solve_fbp_aos rtg_solve_fbp_soa rtg_solve_fbp_small rtg_solve_other rtg_fk rtg_ops"
+SMALL_FLAGS="-mllvm -amdgpu-sched-strategy=max-ilp"   # rtg_solve_fbp_small only (csrc/Makefile)
 for spec in "$@"; do
   name="${spec%%:*}"; defs="${spec#*:}"
   objs=""
   for t in $TUS; do
-    /opt/rocm/bin/hipcc $FLAGS $defs -c $t.hip -o /tmp/v_$name.$t.o &
+    extra=""; [ "$t" = rtg_solve_fbp_small ] && extra="$SMALL_FLAGS"
+    /opt/rocm/bin/hipcc $FLAGS $extra $defs -c $t.hip -o /tmp/v_$name.$t.o &
     objs="$objs /tmp/v_$name.$t.o"
   done
   /opt/rocm/bin/hipcc $FLAGS $defs -x hip -c rtg_api.cpp -o /tmp/v_$name.api.o &
