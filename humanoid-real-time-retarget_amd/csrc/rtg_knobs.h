@@ -10,7 +10,8 @@
 #define RTG_SIDES_TILES 2   // 64-frame tiles (two waves each) per k_solve_sides block
 #endif
 #ifndef RTG_SIDES_SPLIT_READOUT
-#define RTG_SIDES_SPLIT_READOUT 0   // FULL_BODY_POS side kernel: the left wave also reads out the right chain's slots
+#define RTG_SIDES_SPLIT_READOUT 1   // FULL_BODY_POS side kernel: the left wave also reads out the right chain's slots
+                                    // (medians 101.8 / 103.3 vs 102.9 / 104.0 us SoA, 115.1 / 116.2 vs 117.0 / 118.2 AoS)
 #endif
 #ifndef RTG_SIDES_WAVES
 #define RTG_SIDES_WAVES 1   // min waves per SIMD for the side kernel (1: the compiler picks; measured best)

@@ -13,7 +13,7 @@ objs=""
 # the revision's own TU list and per-TU flags (rtg_solve_fbp_small exists from round 5 on, with SMALL_FLAGS)
 for f in rtg_*.hip; do
   t=${f%.hip}
-  extra=""; [ "$t" = rtg_solve_fbp_small ] && extra="-mllvm -amdgpu-sched-strategy=max-ilp"
+  extra=""; { [ "$t" = rtg_solve_fbp_small ] || [ "$t" = rtg_fk ]; } && extra="-mllvm -amdgpu-sched-strategy=max-ilp"
   /opt/rocm/bin/hipcc $FLAGS $extra -c $t.hip -o $t.o &
   objs="$objs $t.o"
 done

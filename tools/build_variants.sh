@@ -13,7 +13,7 @@ for spec in "$@"; do
   name="${spec%%:*}"; defs="${spec#*:}"
   objs=""
   for t in $TUS; do
-    extra=""; [ "$t" = rtg_solve_fbp_small ] && extra="$SMALL_FLAGS"
+    extra=""; { [ "$t" = rtg_solve_fbp_small ] || [ "$t" = rtg_fk ]; } && extra="$SMALL_FLAGS"
     /opt/rocm/bin/hipcc $FLAGS $extra $defs -c $t.hip -o /tmp/v_$name.$t.o &
     objs="$objs /tmp/v_$name.$t.o"
   done
