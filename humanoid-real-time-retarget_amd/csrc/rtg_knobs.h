@@ -88,6 +88,9 @@
 #define RTG_LINE_NT_STORE 0   // A/B knob (same values): the line-synchronous inverse FK's whole-line stores non-temporal
                               // (measured neutral: 74-76 vs 74-79 us)
 #endif
+#ifndef RTG_IN_NT_LOAD
+#define RTG_IN_NT_LOAD 0   // A/B knob (same values): the solvers' SoA input planes loaded non-temporal
+#endif
 #ifndef RTG_EXP_NO_RARE
 #define RTG_EXP_NO_RARE 0   // measurement knob, a bit mask: the rare-case branches of cr_sqrt (1) / cr_acos (2) /
 #endif                      // cr_sincos (4) / mulr (8) / sqrt_clamp_rcp (16) removed (wrong answers on rare inputs)

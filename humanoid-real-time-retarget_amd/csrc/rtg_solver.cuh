@@ -180,7 +180,11 @@ template <>
 struct FV<true> {
     const float *__restrict__ p;
     int64_t s;
-    RTG_DEV float e(int64_t i) const { return p[i]; }
+    RTG_DEV float e(int64_t i) const
+    {
+        if (RTG_IN_NT_LOAD) return __builtin_nontemporal_load(p + i);   // A/B knob: streaming input planes
+        return p[i];
+    }
     RTG_DEV V p3(int j) const { return V{e((3 * j) * s), e((3 * j + 1) * s), e((3 * j + 2) * s)}; }
     RTG_DEV Q q4(int j) const { return Q{e((4 * j) * s), e((4 * j + 1) * s), e((4 * j + 2) * s), e((4 * j + 3) * s)}; }
 };
