@@ -359,13 +359,33 @@ __global__ __launch_bounds__(kFkTile) void k_dof_fk(TopoView T, DofView D, const
     const Q rroot = ld4(root_rot + f * 4);
     const V troot = ld3(root_t + f * 3);
     DofRegs cur, next;
+#if RTG_DOF_PF16
+    // A/B knob: two windows' angles (a 64-byte half of a Hu row) per prefetch, so each DOF line is requested by 3
+    // windows instead of 5 (the re-requests miss L2: FETCH 4.2x the DOF input)
+    DofRegs cur2, next2;
+    if (J > 1) { dof_load(next, drow, J, 0); dof_load(next2, drow, J, kFkChunk); }
+#else
     if (J > 1) dof_load(next, drow, J, 0);
+#endif
     Q g = qident();
     V t = V{0.0f, 0.0f, 0.0f};
     for (int c0 = 0; c0 < J; c0 += kFkChunk) {
         const int nC = (J - c0) < kFkChunk ? (J - c0) : kFkChunk;
+#if RTG_DOF_PF16
+        if ((c0 & kFkChunk) == 0) {
+            cur = next;
+            cur2 = next2;
+            if (c0 + 2 * kFkChunk < J) {
+                dof_load(next, drow, J, c0 + 2 * kFkChunk);
+                dof_load(next2, drow, J, c0 + 3 * kFkChunk);
+            }
+        } else {
+            cur = cur2;
+        }
+#else
         cur = next;
         if (c0 + kFkChunk < J) dof_load(next, drow, J, c0 + kFkChunk);
+#endif
         if (active) {
             float *R = rot + lane * kRotPitch;
 #pragma unroll

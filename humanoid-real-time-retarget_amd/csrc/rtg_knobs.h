@@ -94,6 +94,9 @@
 #ifndef RTG_VEL_W
 #define RTG_VEL_W 8   // velocity tiles: consecutive smoothed outputs per thread (8 vs 4: linear 61.2 vs 65.1 us, angular 110.5 vs 113.1)
 #endif
+#ifndef RTG_DOF_PF16
+#define RTG_DOF_PF16 0   // k_dof_fk: prefetch two 8-joint windows' angles at a time
+#endif
 #ifndef RTG_EXP_NO_RARE
 #define RTG_EXP_NO_RARE 0   // measurement knob, a bit mask: the rare-case branches of cr_sqrt (1) / cr_acos (2) /
 #endif                      // cr_sincos (4) / mulr (8) / sqrt_clamp_rcp (16) removed (wrong answers on rare inputs)
