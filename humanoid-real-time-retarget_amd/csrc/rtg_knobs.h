@@ -32,7 +32,7 @@
 #define RTG_EXP_SKIP_SIGNAL 0   // measurement knob: block 0's first R10 hand-over is never raised, so its partner wave
 #endif                          // times out (tests the RTG_DEVERR_HANDOVER_TIMEOUT report; wrong answers)
 #ifndef RTG_VEL_SEG
-#define RTG_VEL_SEG 20   // rows per thread in the linear velocity tile's load phase (round 5)
+#define RTG_VEL_SEG 10   // linear velocity tile: rows per thread run (10: 58.0 us vs 61.2 at 20 and 68.3 at 40, with RTG_VEL_W 8)
 #endif
 #ifndef RTG_VEL_LDS_MIN
 #define RTG_VEL_LDS_MIN 0   // A/B knob: the velocity tile's LDS request raised to this many bytes (blocks per CU)
