@@ -95,7 +95,11 @@
 #define RTG_VEL_W 8   // velocity tiles: consecutive smoothed outputs per thread (8 vs 4: linear 61.2 vs 65.1 us, angular 110.5 vs 113.1)
 #endif
 #ifndef RTG_DOF_PF16
-#define RTG_DOF_PF16 0   // k_dof_fk: prefetch two 8-joint windows' angles at a time
+#define RTG_DOF_PF16 0   // k_dof_fk: prefetch two 8-joint windows' angles at a time (measured slower: 135 vs 128 us;
+                         // 181 VGPRs, 2 waves per SIMD instead of 3)
+#endif
+#ifndef RTG_VEL_ANG_NB
+#define RTG_VEL_ANG_NB 2   // angular velocity tile: raw elements per thread per load batch (1-4 measured alike, ~110 us)
 #endif
 #ifndef RTG_EXP_NO_RARE
 #define RTG_EXP_NO_RARE 0   // measurement knob, a bit mask: the rare-case branches of cr_sqrt (1) / cr_acos (2) /
