@@ -44,12 +44,12 @@ RTG_DEV float cr_sqrt64(float x)
 }
 // Correctly rounded f32 sqrt in f32 arithmetic (round 5): v_sqrt_f32 is within 1 ulp for x >= 2^-96, and of the
 // candidates s - ulp, s, s + ulp the signs of the exact residuals x - (s - ulp) s and x - (s + ulp) s (one fma each)
-// pick the correctly rounded one -- the sequence LLVM emits for a correctly rounded f32 sqrt, without its denormal
-// scaling.  +-0 comes out of the same sequence exactly (v_sqrt_f32(+-0) = +-0 and neither residual test moves it:
-// quat_from_rotation_matrix clamps negative estimates to 0, so zeros are common there); x below 2^-96 (denormals,
-// negatives), inf and NaN take cr_sqrt64 behind one rare-case branch.  No f64
-// instruction on the common path (cr_sqrt64: three f64 ops and two quarter-rate f64 transcendentals).  Proven equal
-// to __builtin_sqrtf on all 2^32 inputs by tools/check_fastmath.hip [1] (run by tests/test_gpu_parity.py).
+// pick the correctly rounded one -- the sequence LLVM emits for a correctly rounded f32 sqrt.  +-0 comes out of the
+// same sequence exactly (v_sqrt_f32(+-0) = +-0 and neither residual test moves it: quat_from_rotation_matrix clamps
+// negative estimates to 0, so zeros are common there); x below 2^-96 (denormals, negatives) is scaled by 2^64 first
+// (below; RTG_EXP_SQRT_CALL keeps the first form, cr_sqrt64 behind one rare-case branch).  No f64 instruction (cr_sqrt64:
+// three f64 ops and two quarter-rate f64 transcendentals).  Proven equal to __builtin_sqrtf on all 2^32 inputs by
+// tools/check_fastmath.hip [1] (run by tests/test_gpu_parity.py).
 __device__ __attribute__((noinline)) float cr_sqrt64_call(float x) { return cr_sqrt64(x); }
 RTG_DEV float cr_sqrt(float x)
 {
