@@ -1032,7 +1032,9 @@ __global__ __launch_bounds__(320) void k_fbp_frame1(SolverConsts C, const float 
 // Euler split, 3 / 4 arm chains).  Every value comes from the same device functions on the same operands: the same
 // bits (test_solver_batch_invariance, the GPU parity suite).
 // ----------------------------------------------------------------------------
-constexpr int kQuadFrames = 16;
+constexpr int kQuadFrames = RTG_QUAD_FRAMES;   // 16 (one per lane quad of a wave) or 8
+static_assert(kQuadFrames == 16 || kQuadFrames == 8, "k_fbp_quad: 8 or 16 frames per block");
+constexpr int kQuadLog2 = kQuadFrames == 16 ? 4 : 3;
 template <bool PRECISE, bool SOA>
 __global__ __launch_bounds__(320) void k_fbp_quad(SolverConsts C, const float *__restrict__ in0,
                                                   const float *__restrict__ in1, const float *__restrict__ in2,
@@ -1052,7 +1054,7 @@ __global__ __launch_bounds__(320) void k_fbp_quad(SolverConsts C, const float *_
     // runs the whole program -- the DPP broadcasts need the full quad -- and only live frames store)
     if (SOA) {
         for (int i = threadIdx.x; i < kQuadFrames * 183; i += 320) {
-            const int q = i & (kQuadFrames - 1), e = i >> 4;   // 16 consecutive frames of one component
+            const int q = i & (kQuadFrames - 1), e = i >> kQuadLog2;   // consecutive frames of one component
             const int64_t f = f0 + (q < nf ? q : nf - 1);
             rows[q * RP + e] = e < 63 ? in0[e * B + f] : (e < 123 ? in1[(e - 63) * B + f] : in2[(e - 123) * B + f]);
         }
@@ -1065,9 +1067,10 @@ __global__ __launch_bounds__(320) void k_fbp_quad(SolverConsts C, const float *_
     }
     if (threadIdx.x < 3) sflag[threadIdx.x] = 0;
     __syncthreads();
-    const int w = threadIdx.x >> 6, lane = threadIdx.x & 63, q = lane >> 2, sub = lane & 3;
+    // with 8 frames per block a wave's upper 8 quads repeat the lower 8 (same rows, same values, never stored)
+    const int w = threadIdx.x >> 6, lane = threadIdx.x & 63, qq = lane >> 2, q = qq & (kQuadFrames - 1), sub = lane & 3;
     const int64_t f = f0 + q;
-    const bool live = q < nf;
+    const bool live = qq < nf;
     const Emit E{sdof + q * kDofStride, live && local_rot ? local_rot + f * 124 : nullptr, C.ang_tab, sst + q * 14, 1};
     const FV<false> b{rows + q * RP};
     uint32_t st = 0;
