@@ -16,8 +16,8 @@
 #ifndef RTG_SIDES_WAVES
 #define RTG_SIDES_WAVES 1   // min waves per SIMD for the side kernel (1: the compiler picks; measured best)
 #endif
-#ifndef RTG_QUAD_FRAMES
-#define RTG_QUAD_FRAMES 16   // k_fbp_quad frames per block (16: one per lane quad; 8: the upper quads repeat them)
+#ifndef RTG_QUAD8_MAX_B
+#define RTG_QUAD8_MAX_B 2048   // 2 <= B <= this: k_fbp_quad with 8 frames per block (one block per CU up to 2048)
 #endif
 #ifndef RTG_QUAD_MAX_B
 #define RTG_QUAD_MAX_B 4096   // 2 <= B <= this: k_fbp_quad (swept: 16.7 vs 17.2-17.7 us up to 4096, 19.8 vs 17.5 at 8192)

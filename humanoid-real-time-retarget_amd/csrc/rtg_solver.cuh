@@ -1032,15 +1032,17 @@ __global__ __launch_bounds__(320) void k_fbp_frame1(SolverConsts C, const float 
 // Euler split, 3 / 4 arm chains).  Every value comes from the same device functions on the same operands: the same
 // bits (test_solver_batch_invariance, the GPU parity suite).
 // ----------------------------------------------------------------------------
-constexpr int kQuadFrames = RTG_QUAD_FRAMES;   // 16 (one per lane quad of a wave) or 8
-static_assert(kQuadFrames == 16 || kQuadFrames == 8, "k_fbp_quad: 8 or 16 frames per block");
-constexpr int kQuadLog2 = kQuadFrames == 16 ? 4 : 3;
-template <bool PRECISE, bool SOA>
+// FPB frames per block: 16 (one per lane quad) or 8 (the upper eight quads of each wave repeat the lower eight --
+// same rows, same values, never stored): at one block per CU the eight-frame tile runs each SVD at the slowest of 8
+// frames' sweep counts instead of 16 (measured 15.3 vs 16.4 us for B <= 2048; launch_fbp_small_kind)
+template <bool PRECISE, bool SOA, int FPB>
 __global__ __launch_bounds__(320) void k_fbp_quad(SolverConsts C, const float *__restrict__ in0,
                                                   const float *__restrict__ in1, const float *__restrict__ in2,
                                                   int64_t B, float *__restrict__ dof, float *__restrict__ local_rot,
                                                   float *__restrict__ body_rot)
 {
+    static_assert(FPB == 16 || FPB == 8, "k_fbp_quad: 8 or 16 frames per block");
+    constexpr int kQuadFrames = FPB, kQuadLog2 = FPB == 16 ? 4 : 3;
     constexpr int RP = 184;                      // LDS row pitch of a frame: body 63 | left hand 60 | right hand 60
     __shared__ float rows[kQuadFrames * RP];
     __shared__ float sdof[kQuadFrames * kDofStride];
@@ -1207,9 +1209,12 @@ static void launch_fbp_small_kind(const SolverConsts &C, const float *in0, const
     if (B == 1) {
         hipLaunchKernelGGL((k_fbp_frame1<PRECISE>), dim3(1), dim3(320), 0, s, C, in0, in1, in2, dof, local_rot,
                            body_rot);
+    } else if (B <= RTG_QUAD8_MAX_B) {
+        hipLaunchKernelGGL((k_fbp_quad<PRECISE, SOA, 8>), dim3(grid_for(B, 8)), dim3(320), 0, s, C, in0, in1, in2, B,
+                           dof, local_rot, body_rot);
     } else if (B <= RTG_QUAD_MAX_B) {
-        hipLaunchKernelGGL((k_fbp_quad<PRECISE, SOA>), dim3(grid_for(B, kQuadFrames)), dim3(320), 0, s, C, in0,
-                           in1, in2, B, dof, local_rot, body_rot);
+        hipLaunchKernelGGL((k_fbp_quad<PRECISE, SOA, 16>), dim3(grid_for(B, 16)), dim3(320), 0, s, C, in0, in1, in2, B,
+                           dof, local_rot, body_rot);
     } else {
         hipLaunchKernelGGL((k_fbp_latency5<PRECISE, SOA>), dim3(grid_for(B, kLatFrames)), dim3(320), 0, s, C,
                            in0, in1, in2, B, dof, local_rot, body_rot);

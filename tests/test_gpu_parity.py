@@ -483,9 +483,10 @@ def test_config2_batch4096_vs_oracle(gpu):
 
 @pytest.mark.parametrize("layout", ["aos", "soa"])
 def test_quad_tile_ragged_batches_vs_oracle(gpu, layout):
-    """k_fbp_quad (2 <= B <= RTG_QUAD_MAX_B: 16 frames per block, one frame per lane quad) on ragged batch sizes:
-    DOFs, local and body rotations bit-exact with the oracle, in both input layouts, including a NaN frame the
-    reference raises on inside a partial last tile (NaNs compared as NaN; its status code bit for bit)."""
+    """k_fbp_quad (2 <= B <= RTG_QUAD_MAX_B: one frame per lane quad; 8 frames per block up to RTG_QUAD8_MAX_B,
+    16 above) on ragged batch sizes: DOFs, local and body rotations bit-exact with the oracle, in both input layouts,
+    including a NaN frame the reference raises on inside a partial last tile (NaNs compared as NaN; its status code
+    bit for bit)."""
     import oracle as orc
     from rtg import _lib, ops
     from rtg.runtime import frame_status
@@ -496,10 +497,10 @@ def test_quad_tile_ragged_batches_vs_oracle(gpu, layout):
         a = np.ascontiguousarray(a, np.float32)
         return np.where(np.isnan(a), np.uint32(0x7FC00000), a.view(np.uint32))
 
-    for B in (2, 15, 16, 17, 47):
+    for B in (2, 15, 16, 17, 47, 4089):
         body, lh, rh = ops.synth_full_body(_topo("vtrdyn_full"), B, seed=B)
-        if B == 47:
-            lh[45, 2] = float("nan")   # frame 45 of the last (15-frame) tile: its left wrist fit refuses
+        if B in (47, 4089):
+            lh[B - 2, 2] = float("nan")   # a frame of the partial last tile: its left wrist fit refuses
         ins = [body, lh, rh] if layout == "aos" else [t.permute(1, 2, 0).contiguous() for t in (body, lh, rh)]
         dof, lr, br = S.retarget(ins, want_local_rot=True, want_body_rot=True, layout=layout)
         odof, olr, obr = orc.full_body_pos(zp["vtrdyn_full_local_t"], zp["vtrdyn_full_global_t"], _np(body),
@@ -508,7 +509,7 @@ def test_quad_tile_ragged_batches_vs_oracle(gpu, layout):
         np.testing.assert_array_equal(frame_status(dof).cpu().numpy(), orc.frame_status(odof), err_msg=f"B={B}")
         np.testing.assert_array_equal(bits(_np(lr)), bits(olr), err_msg=f"B={B}")
         np.testing.assert_array_equal(bits(_np(br)), bits(obr), err_msg=f"B={B}")
-        assert (orc.frame_status(odof) != 0).sum() == (1 if B == 47 else 0)
+        assert (orc.frame_status(odof) != 0).sum() == (1 if B in (47, 4089) else 0)
 
 
 @pytest.mark.parametrize("kind", [0, 1, 2, 3])
