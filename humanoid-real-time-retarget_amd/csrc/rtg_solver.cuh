@@ -173,7 +173,14 @@ struct FV;
 template <>
 struct FV<false> {
     const float *__restrict__ p;
-    RTG_DEV V p3(int j) const { return ld3(p + 3 * j); }
+    RTG_DEV V p3(int j) const
+    {
+        if (RTG_AOS_NT_LOAD) {   // A/B knob: the AoS rows' points loaded non-temporal
+            const float *a = p + 3 * j;
+            return V{__builtin_nontemporal_load(a), __builtin_nontemporal_load(a + 1), __builtin_nontemporal_load(a + 2)};
+        }
+        return ld3(p + 3 * j);
+    }
     RTG_DEV Q q4(int j) const { return ld4(p + 4 * j); }
 };
 template <>
