@@ -148,20 +148,9 @@ RTG_DEV void chunk_to_lds(const ChunkRegs &r, float *lds, int nfr, int nC)
     RTG_REP8(RTG_ST)
 #undef RTG_ST
 }
-// The output rows as streaming (non-temporal) stores when RTG_FK_NT_STORE: they are never read back by the kernel,
-// and in the L2 they would evict the input lines a later window (or chunk) of the same rows still has to read
 typedef float f4v __attribute__((ext_vector_type(4)));
-RTG_DEV void out_st4(float *gp, const float *lp)
-{
-    const f4v v = *reinterpret_cast<const f4v *>(lp);
-    if (RTG_FK_NT_STORE) __builtin_nontemporal_store(v, reinterpret_cast<f4v *>(gp));
-    else *reinterpret_cast<f4v *>(gp) = v;
-}
-RTG_DEV void out_st1(float *gp, float v)
-{
-    if (RTG_FK_NT_STORE) __builtin_nontemporal_store(v, gp);
-    else *gp = v;
-}
+RTG_DEV void out_st4(float *gp, const float *lp) { *reinterpret_cast<f4v *>(gp) = *reinterpret_cast<const f4v *>(lp); }
+RTG_DEV void out_st1(float *gp, float v) { *gp = v; }
 template <int W>
 RTG_DEV void chunk_store(float *__restrict__ g, const float *lds, int pitch, int64_t f0, int nfr, int J, int c0, int nC)
 {
@@ -359,33 +348,13 @@ __global__ __launch_bounds__(kFkTile) void k_dof_fk(TopoView T, DofView D, const
     const Q rroot = ld4(root_rot + f * 4);
     const V troot = ld3(root_t + f * 3);
     DofRegs cur, next;
-#if RTG_DOF_PF16
-    // A/B knob: two windows' angles (a 64-byte half of a Hu row) per prefetch, so each DOF line is requested by 3
-    // windows instead of 5 (the re-requests miss L2: FETCH 4.2x the DOF input)
-    DofRegs cur2, next2;
-    if (J > 1) { dof_load(next, drow, J, 0); dof_load(next2, drow, J, kFkChunk); }
-#else
     if (J > 1) dof_load(next, drow, J, 0);
-#endif
     Q g = qident();
     V t = V{0.0f, 0.0f, 0.0f};
     for (int c0 = 0; c0 < J; c0 += kFkChunk) {
         const int nC = (J - c0) < kFkChunk ? (J - c0) : kFkChunk;
-#if RTG_DOF_PF16
-        if ((c0 & kFkChunk) == 0) {
-            cur = next;
-            cur2 = next2;
-            if (c0 + 2 * kFkChunk < J) {
-                dof_load(next, drow, J, c0 + 2 * kFkChunk);
-                dof_load(next2, drow, J, c0 + 3 * kFkChunk);
-            }
-        } else {
-            cur = cur2;
-        }
-#else
         cur = next;
         if (c0 + kFkChunk < J) dof_load(next, drow, J, c0 + kFkChunk);
-#endif
         if (active) {
             float *R = rot + lane * kRotPitch;
 #pragma unroll
@@ -515,9 +484,7 @@ RTG_DEV void line_store(float *__restrict__ rows, const float *win, int m, int J
             float *gp = rows + (int64_t)W * P.g;
             const float *lp = win + P.fr * kRotPitch + P.sub * W;
             if (W == 4) {
-                const f4v v = *reinterpret_cast<const f4v *>(lp);
-                if (RTG_LINE_NT_STORE) __builtin_nontemporal_store(v, reinterpret_cast<f4v *>(gp));   // A/B knob
-                else *reinterpret_cast<f4v *>(gp) = v;
+                out_st4(gp, lp);
             } else {
 #pragma unroll
                 for (int c = 0; c < W; ++c) gp[c] = lp[c];

@@ -40,9 +40,6 @@
 #ifndef RTG_VEL_LDS_MIN
 #define RTG_VEL_LDS_MIN 0   // A/B knob: the velocity tile's LDS request raised to this many bytes (blocks per CU)
 #endif
-#ifndef RTG_VEL_ANG_PIPE
-#define RTG_VEL_ANG_PIPE 0   // A/B knob: angular velocity tile with the next batch's loads issued before this batch's arithmetic (measured 119-121 vs 116 us: off)
-#endif
 // ---- used by rtg_fk.hip
 #ifndef RTG_EXP_FK_COPY
 #define RTG_EXP_FK_COPY 0   // measurement knob: k_fk_stream copies its windows out without the chain (wrong answers)
@@ -75,21 +72,9 @@
 #ifndef RTG_VEL_IEEE_DIV
 #define RTG_VEL_IEEE_DIV 0   // A/B knob (same values): the velocity tiles' quotients by dt as IEEE divisions (round 4)
 #endif
-#ifndef RTG_FK_NT_STORE
-#define RTG_FK_NT_STORE 0   // A/B knob (same values): the windowed FK kernels' output rows as non-temporal stores
-                            // (measured 200 vs 120 us on Hu FK: the 16-B-aligned row pieces straddle lines)
-#endif
 #ifndef RTG_DOF_NT_STORE
 #define RTG_DOF_NT_STORE 1   // A/B knob (same values): the solvers' DOF rows (whole 128-B lines) as non-temporal stores
                              // (headline 101.3 vs 104.5 us SoA, 114.4 vs 117.7 AoS; profiles/r05/nt/)
-#endif
-#ifndef RTG_VEL_NT_STORE
-#define RTG_VEL_NT_STORE 0   // A/B knob (same values): the velocity tiles' output rows as non-temporal stores
-                             // (measured slower: linear 66 vs 63 us, angular 117 vs 113)
-#endif
-#ifndef RTG_LINE_NT_STORE
-#define RTG_LINE_NT_STORE 0   // A/B knob (same values): the line-synchronous inverse FK's whole-line stores non-temporal
-                              // (measured neutral: 74-76 vs 74-79 us)
 #endif
 #ifndef RTG_IN_NT_LOAD
 #define RTG_IN_NT_LOAD 0   // A/B knob (same values): the solvers' SoA input planes loaded non-temporal
@@ -97,16 +82,8 @@
 #ifndef RTG_VEL_W
 #define RTG_VEL_W 8   // velocity tiles: consecutive smoothed outputs per thread (8 vs 4: linear 61.2 vs 65.1 us, angular 110.5 vs 113.1)
 #endif
-#ifndef RTG_DOF_PF16
-#define RTG_DOF_PF16 0   // k_dof_fk: prefetch two 8-joint windows' angles at a time (measured slower: 135 vs 128 us;
-                         // 181 VGPRs, 2 waves per SIMD instead of 3)
-#endif
 #ifndef RTG_VEL_ANG_NB
 #define RTG_VEL_ANG_NB 2   // angular velocity tile: raw elements per thread per load batch (1-4 measured alike, ~110 us)
-#endif
-#ifndef RTG_AOS_NT_LOAD
-#define RTG_AOS_NT_LOAD 0   // A/B knob (same values): AoS row points loaded non-temporal (measured 148 vs 117 us:
-                            // a row's line leaves the cache before its other points are read)
 #endif
 #ifndef RTG_EXP_NO_RARE
 #define RTG_EXP_NO_RARE 0   // measurement knob, a bit mask: the rare-case branches of cr_sqrt (1) / cr_acos (2) /

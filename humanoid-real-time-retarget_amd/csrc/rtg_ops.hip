@@ -628,8 +628,8 @@ __global__ __launch_bounds__(256) void k_velocity_tile(const float *__restrict__
         const float *r = src + seq * L * J * 4;
         const uint32_t n = nx * (uint32_t)J;
         RowWalk w(threadIdx.x, (uint32_t)J);
-        // batches of NB elements: loads, then arithmetic (RTG_VEL_ANG_PIPE=1 issues the next batch's loads before this
-        // batch's arithmetic: measured slower, 119-121 vs 116 us, profiles/r05/aux/angpipe_*)
+        // batches of NB elements: loads, then arithmetic (the next batch's loads issued before this batch's arithmetic
+        // measured slower, 119-121 vs 116 us, profiles/r05/aux/angpipe_*)
         Q qa[NB], qb[NB];
         bool last[NB];
         uint32_t at[NB];
@@ -653,9 +653,6 @@ __global__ __launch_bounds__(256) void k_velocity_tile(const float *__restrict__
             uint32_t cat[NB];
 #pragma unroll
             for (int k = 0; k < NB; ++k) { ca[k] = qa[k]; cb[k] = qb[k]; cl[k] = last[k]; cat[k] = at[k]; }
-#if RTG_VEL_ANG_PIPE
-            if (e0 + 256 * NB < n) fetch(e0 + 256 * NB);
-#endif
 #pragma unroll
             for (int k = 0; k < NB; ++k) {
                 if (e0 + 256u * k >= n) continue;
@@ -673,9 +670,7 @@ __global__ __launch_bounds__(256) void k_velocity_tile(const float *__restrict__
                 sg[cat[k] + 2 * NS] = av.z;
 #endif
             }
-#if !RTG_VEL_ANG_PIPE
             if (e0 + 256 * NB < n) fetch(e0 + 256 * NB);
-#endif
         }
     }
     __syncthreads();
@@ -692,9 +687,7 @@ __global__ __launch_bounds__(256) void k_velocity_tile(const float *__restrict__
 #pragma unroll
             for (int r = 0; r < W; ++r)
                 if (r0 + r < rows) {
-                    float *op = o + (int64_t)(r0 + r) * C + w.ch;
-                    if (RTG_VEL_NT_STORE) __builtin_nontemporal_store((float)acc[r], op);   // A/B knob
-                    else *op = (float)acc[r];
+                    o[(int64_t)(r0 + r) * C + w.ch] = (float)acc[r];
                 }
             w.next((uint32_t)C);
         }
@@ -1054,7 +1047,7 @@ extern "C" const char *rtg_build_info(void)
 {
     return "{\"abi\":" RTG_STR(RTG_ABI_VERSION) ",\"arch\":\"gfx950\",\"knobs\":{"
         RTG_KNOB(RTG_SIDES_WAVES) RTG_KNOB(RTG_SIDES_TILES) RTG_KNOB(RTG_SIDES_SPLIT_READOUT) RTG_KNOB(RTG_QUAD8_MAX_B) RTG_KNOB(RTG_QUAD_MAX_B) RTG_KNOB(RTG_LATENCY_MAX_B)
-        RTG_KNOB(RTG_EXP_TIMESTAMPS) RTG_KNOB(RTG_EXP_SKIP_SIGNAL) RTG_KNOB(RTG_EXP_STUB_SVD) RTG_KNOB(RTG_EXP_NO_TABLE) RTG_KNOB(RTG_EXP_FK_COPY) RTG_KNOB(RTG_EXP_FK_NOPOS) RTG_KNOB(RTG_EXP_MULR_NOBRANCH) RTG_KNOB(RTG_EXP_LARTG_RCP64) RTG_KNOB(RTG_EXP_SQRT64) RTG_KNOB(RTG_EXP_SQRT_CALL) RTG_KNOB(RTG_EXP_ACOS_LIBM) RTG_KNOB(RTG_EXP_EULER_SCIPY) RTG_KNOB(RTG_VEL_SEG) RTG_KNOB(RTG_VEL_LDS_MIN) RTG_KNOB(RTG_VEL_ANG_PIPE) RTG_KNOB(RTG_VEL_IEEE_DIV) RTG_KNOB(RTG_FK_NT_STORE) RTG_KNOB(RTG_DOF_NT_STORE) RTG_KNOB(RTG_VEL_NT_STORE) RTG_KNOB(RTG_LINE_NT_STORE) RTG_KNOB(RTG_IN_NT_LOAD) RTG_KNOB(RTG_AOS_NT_LOAD) RTG_KNOB(RTG_VEL_W) RTG_KNOB(RTG_DOF_PF16) RTG_KNOB(RTG_VEL_ANG_NB) RTG_KNOB(RTG_EXP_NO_RARE)
+        RTG_KNOB(RTG_EXP_TIMESTAMPS) RTG_KNOB(RTG_EXP_SKIP_SIGNAL) RTG_KNOB(RTG_EXP_STUB_SVD) RTG_KNOB(RTG_EXP_NO_TABLE) RTG_KNOB(RTG_EXP_FK_COPY) RTG_KNOB(RTG_EXP_FK_NOPOS) RTG_KNOB(RTG_EXP_MULR_NOBRANCH) RTG_KNOB(RTG_EXP_LARTG_RCP64) RTG_KNOB(RTG_EXP_SQRT64) RTG_KNOB(RTG_EXP_SQRT_CALL) RTG_KNOB(RTG_EXP_ACOS_LIBM) RTG_KNOB(RTG_EXP_EULER_SCIPY) RTG_KNOB(RTG_VEL_SEG) RTG_KNOB(RTG_VEL_LDS_MIN) RTG_KNOB(RTG_VEL_IEEE_DIV) RTG_KNOB(RTG_DOF_NT_STORE) RTG_KNOB(RTG_IN_NT_LOAD) RTG_KNOB(RTG_VEL_W) RTG_KNOB(RTG_VEL_ANG_NB) RTG_KNOB(RTG_EXP_NO_RARE)
         "\"RTG_EXP_HOT_INPUTS\":\"" RTG_STR(RTG_EXP_HOT_INPUTS) "\"},\"wrong_answer_knobs\":"
         RTG_STR(RTG_WRONG_ANSWER_KNOBS) "}";
 }

@@ -38,12 +38,12 @@ hipError_t launch_build_ang_tab(uint32_t *tab, hipStream_t s)
 }
 
 template <int KIND>
-static void launch_other(const SolverConsts &C, const float *in0, const float *in1, const float *in2,
-                         const float *in3, int64_t B, int layout, float *dof, float *local_rot, float *body_rot,
-                         hipStream_t s)
+static hipError_t launch_other(const SolverConsts &C, const float *in0, const float *in1, const float *in2,
+                               const float *in3, int64_t B, int layout, float *dof, float *local_rot, float *body_rot,
+                               hipStream_t s)
 {
-    if (layout == RTG_LAYOUT_SOA) launch_kind<KIND, false, true>(C, in0, in1, in2, in3, B, dof, local_rot, body_rot, s);
-    else launch_kind<KIND, false, false>(C, in0, in1, in2, in3, B, dof, local_rot, body_rot, s);
+    if (layout == RTG_LAYOUT_SOA) return launch_kind<KIND, false, true>(C, in0, in1, in2, in3, B, dof, local_rot, body_rot, s);
+    return launch_kind<KIND, false, false>(C, in0, in1, in2, in3, B, dof, local_rot, body_rot, s);
 }
 
 hipError_t launch_retarget(int kind, int precise, const SolverConsts &C, const float *in0, const float *in1,
@@ -55,16 +55,12 @@ hipError_t launch_retarget(int kind, int precise, const SolverConsts &C, const f
         return layout == RTG_LAYOUT_SOA ? launch_fbp_soa(precise, C, in0, in1, in2, B, dof, local_rot, body_rot, s)
                                         : launch_fbp_aos(precise, C, in0, in1, in2, B, dof, local_rot, body_rot, s);
     case RTG_SOLVER_UPPER_BODY:
-        launch_other<RTG_SOLVER_UPPER_BODY>(C, in0, in1, in2, in3, B, layout, dof, local_rot, body_rot, s);
-        break;
+        return launch_other<RTG_SOLVER_UPPER_BODY>(C, in0, in1, in2, in3, B, layout, dof, local_rot, body_rot, s);
     case RTG_SOLVER_FULL_BODY_ROT:
-        launch_other<RTG_SOLVER_FULL_BODY_ROT>(C, in0, in1, in2, in3, B, layout, dof, local_rot, body_rot, s);
-        break;
+        return launch_other<RTG_SOLVER_FULL_BODY_ROT>(C, in0, in1, in2, in3, B, layout, dof, local_rot, body_rot, s);
     default:
-        launch_other<RTG_SOLVER_BODY_ROT>(C, in0, in1, in2, in3, B, layout, dof, local_rot, body_rot, s);
-        break;
+        return launch_other<RTG_SOLVER_BODY_ROT>(C, in0, in1, in2, in3, B, layout, dof, local_rot, body_rot, s);
     }
-    return hipGetLastError();
 }
 
 }  // namespace rtg

@@ -173,14 +173,7 @@ struct FV;
 template <>
 struct FV<false> {
     const float *__restrict__ p;
-    RTG_DEV V p3(int j) const
-    {
-        if (RTG_AOS_NT_LOAD) {   // A/B knob: the AoS rows' points loaded non-temporal
-            const float *a = p + 3 * j;
-            return V{__builtin_nontemporal_load(a), __builtin_nontemporal_load(a + 1), __builtin_nontemporal_load(a + 2)};
-        }
-        return ld3(p + 3 * j);
-    }
+    RTG_DEV V p3(int j) const { return ld3(p + 3 * j); }
     RTG_DEV Q q4(int j) const { return ld4(p + 4 * j); }
 };
 template <>
@@ -450,13 +443,13 @@ __global__ __launch_bounds__(kSideThreads, RTG_SIDES_WAVES) void k_solve_sides(S
     auto view = [&](const float *base, int row_floats) { return frame_view<SOA>(base, fi, row_floats, B); };
 #if RTG_EXP_TIMESTAMPS
     // measurement knob: lane 0 of each wave of every 8th block records the 100 MHz wall clock at the phase
-    // boundaries into the body_rot buffer (tools/side_phases.py): 16 slots per wave, 4 waves per block
+    // boundaries into the body_rot buffer (tools/side_phases.py): 16 slots per wave, 2 * kSideTiles waves per block
     float *const tsb = body_rot;
     body_rot = nullptr;
     auto TS = [&](int k) {
         if (tsb && (blockIdx.x & 7) == 0 && lane == 0) {
             const uint64_t t = wall_clock64();
-            uint32_t *o = reinterpret_cast<uint32_t *>(tsb) + 2 * (((blockIdx.x >> 3) * 4 + w) * 16 + k);
+            uint32_t *o = reinterpret_cast<uint32_t *>(tsb) + 2 * (((blockIdx.x >> 3) * (2 * kSideTiles) + w) * 16 + k);
             o[0] = (uint32_t)t;
             o[1] = (uint32_t)(t >> 32);
         }
@@ -472,8 +465,8 @@ __global__ __launch_bounds__(kSideThreads, RTG_SIDES_WAVES) void k_solve_sides(S
         // Euler split / gripper -- 1.5 SVD-equivalents per wave.  Two per-tile LDS flags hand R10 (left -> right)
         // and the left chain (right -> left) over, so each wave waits only for what it reads; a third counts the
         // waves out, and the second one to finish stores the tile's DOF rows while the first exits.
-        __shared__ int sflag[2][4];   // per tile: [0] R10 ready, [1] left chain ready, [2] waves done, [3] right chain ready
-        if (threadIdx.x < 8) (&sflag[0][0])[threadIdx.x] = 0;
+        __shared__ int sflag[kSideTiles][4];   // per tile: [0] R10 ready, [1] left chain ready, [2] waves done, [3] right chain ready
+        if (threadIdx.x < 4 * kSideTiles) (&sflag[0][0])[threadIdx.x] = 0;
         __syncthreads();
         int *const fl = sflag[w >> 1];
         auto hook1 = [&](int k) { TS(1 + k); };    // 1: first fit's A formed (its points loaded), 2: its SVD + R done
@@ -1227,18 +1220,19 @@ static void launch_fbp_small_kind(const SolverConsts &C, const float *in0, const
                            in0, in1, in2, B, dof, local_rot, body_rot);
     }
 }
+// Returns the launch's status.  launch_fbp_small reads (and so clears) the error state itself, so its result is passed
+// up as it is; a caller must not read hipGetLastError() again after this (a failed small-batch launch was
+// reported as RTG_OK).
 template <int KIND, bool PRECISE, bool SOA>
-static void launch_kind(const SolverConsts &C, const float *in0, const float *in1, const float *in2,
-                        const float *in3, int64_t B, float *dof, float *local_rot, float *body_rot, hipStream_t s)
+static hipError_t launch_kind(const SolverConsts &C, const float *in0, const float *in1, const float *in2,
+                              const float *in3, int64_t B, float *dof, float *local_rot, float *body_rot, hipStream_t s)
 {
     if constexpr (KIND == RTG_SOLVER_FULL_BODY_POS) {
-        if (B <= RTG_LATENCY_MAX_B) {
-            (void)launch_fbp_small(PRECISE, SOA, C, in0, in1, in2, B, dof, local_rot, body_rot, s);   // errors: hipGetLastError
-            return;
-        }
+        if (B <= RTG_LATENCY_MAX_B) return launch_fbp_small(PRECISE, SOA, C, in0, in1, in2, B, dof, local_rot, body_rot, s);
     }
     hipLaunchKernelGGL((k_solve_sides<KIND, PRECISE, SOA>), dim3(grid_for(B, kSideFrames)), dim3(kSideThreads), 0, s, C, in0,
                        in1, in2, in3, B, dof, local_rot, body_rot);
+    return hipGetLastError();
 }
 
 // FULL_BODY_POS launches, one TU per input layout

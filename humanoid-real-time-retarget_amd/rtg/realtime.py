@@ -44,6 +44,39 @@ except ImportError:   # not built: the ctypes path below does the same call
 _F32 = torch.float32
 
 
+# Device inboxes are pooled for the process, not freed per server: hipFree synchronizes the whole device,
+# and dropping one FrameServer while another is resident (its stream busy until it idles out) would stall the caller
+# there.  A released inbox goes back to the pool and is handed to the next server; the pool is freed at exit, after
+# every server has been closed.
+_INBOX_POOL: list = []
+
+
+def _inbox_take():
+    """A device inbox (rtg_server_inbox_alloc) from the pool or a new one, its sequence word 0; None if the device
+    has none (no large BAR): the caller keeps a pinned inbox."""
+    if _INBOX_POOL:
+        p = _INBOX_POOL.pop()
+        lib().rtg_frame_server_signal(p, 0)   # a fresh server's ctl[1] is 0: the word must match it (host store only)
+        return p
+    p = ctypes.c_void_p()
+    if lib().rtg_server_inbox_alloc(ctypes.byref(p)) == 0 and p.value:
+        return p.value
+    return None
+
+
+def _inbox_give(p) -> None:
+    _INBOX_POOL.append(p)
+
+
+@atexit.register
+def _inbox_pool_free() -> None:
+    while _INBOX_POOL:
+        try:
+            lib().rtg_server_inbox_free(_INBOX_POOL.pop())
+        except Exception:
+            break
+
+
 def _host_f32_ptr(x, n: int, tail):
     """(address, owner) of n contiguous float32 values on the host: a CPU tensor or array as it is when it already
     is one, else a float32 copy."""
@@ -182,10 +215,9 @@ class FrameServer:
         from ._lib import SERVER_INBOX_FLOATS
         self.h_in = None
         self._inbox = None
-        p = ctypes.c_void_p()
-        if device_inbox and lib().rtg_server_inbox_alloc(ctypes.byref(p)) == 0 and p.value:
-            self._inbox = p.value
-            self._free_inbox = lib().rtg_server_inbox_free
+        if device_inbox:
+            self._inbox = _inbox_take()
+        if self._inbox:
             in_ptr = self._inbox
         else:
             self.h_in = torch.zeros(SERVER_INBOX_FLOATS, dtype=torch.float32).pin_memory()
@@ -278,9 +310,13 @@ class FrameServer:
             self._atexit = None
 
     def _release(self):
+        """The device inbox back to the process pool -- no hipFree here (a device-wide synchronize).  Only once the
+        server has ended: a resident kernel still polls its inbox."""
+        if getattr(self, "_running", False):
+            return
         inbox, self._inbox = getattr(self, "_inbox", None), None
         if inbox:
-            self._free_inbox(inbox)
+            _inbox_give(inbox)
 
     def __enter__(self):
         return self
@@ -290,8 +326,10 @@ class FrameServer:
 
     def __del__(self):
         try:
-            self.close()
-            self._release()
+            try:
+                self.close()
+            finally:
+                self._release()
         except Exception:
             pass
 

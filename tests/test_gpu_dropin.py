@@ -252,9 +252,11 @@ def test_frame_server_matches_batched(gpu):
     n = 48
     lr_b, dof_b, br_b = hu.retarget_batch(torch.from_numpy(g["body"][:n]), torch.from_numpy(g["lh"][:n]),
                                           torch.from_numpy(g["rh"][:n]), want_body_rot=True)
+    large_bar = _large_bar()
     for device_inbox in (True, False):   # the inbox in device memory through the BAR (MI355X), or pinned
         with FrameServer(hu.solver, want_body_rot=True, idle_ms=20, device_inbox=device_inbox) as fs:
-            assert (fs._inbox is not None) == device_inbox
+            # without a large BAR the library refuses a device inbox and the server keeps a pinned one
+            assert (fs._inbox is not None) == (device_inbox and large_bar)
             for i in range(n):
                 if i == n // 2:
                     time.sleep(0.1)   # past idle_ms: the server has ended; the next call relaunches it
@@ -266,6 +268,59 @@ def test_frame_server_matches_batched(gpu):
         assert not fs._running and fs._ctl[2] == 1
     with pytest.raises(ValueError):
         FrameServer(hu.solver, want_body_rot=True)(g["body"][0], g["lh"][0])
+
+
+def _large_bar() -> bool:
+    """Whether the library can hand out a device inbox here (rtg_server_inbox_alloc refuses without a large BAR)."""
+    import ctypes
+
+    from rtg._lib import lib
+    p = ctypes.c_void_p()
+    if lib().rtg_server_inbox_alloc(ctypes.byref(p)) != 0 or not p.value:
+        return False
+    from rtg import realtime
+    realtime._inbox_give(p.value)   # into the process pool (no hipFree: a device-wide synchronize)
+    return True
+
+
+def test_dropping_a_server_while_another_is_resident_returns_at_once(gpu):
+    """a FrameServer's release must not synchronize the device.  With a second server resident (its
+    stream busy until it idles out, 2 s here), dropping the first one returns in well under that, its device inbox
+    goes back to the process pool and the next server takes it, reset to sequence word 0 and serving exactly."""
+    import gc
+    import time
+
+    from retarget.retarget_solver import VtrdynFullBodyPosRetargeter
+    from robot_kinematics_model import RobotZeroPose
+    from rtg import realtime
+    from rtg.realtime import FrameServer
+    g = golden("full_body_pos_precise")
+    hu = VtrdynFullBodyPosRetargeter(RobotZeroPose.from_asset("vtrdyn_full"), RobotZeroPose.from_asset("hu_v5"),
+                                     precise_gripper=True)
+    _, dof_b, _ = hu.retarget_batch(torch.from_numpy(g["body"][:4]), torch.from_numpy(g["lh"][:4]),
+                                    torch.from_numpy(g["rh"][:4]))
+    resident = FrameServer(hu.solver, idle_ms=2000)
+    resident(g["body"][0], g["lh"][0], g["rh"][0])          # launched, and stays resident for 2 s
+    a = FrameServer(hu.solver, idle_ms=2000)
+    a(g["body"][1], g["lh"][1], g["rh"][1])
+    inbox = a._inbox
+    a.close()                                              # a's own stream only
+    t0 = time.perf_counter()
+    del a
+    gc.collect()
+    dt = time.perf_counter() - t0
+    assert dt < 0.5, dt                                    # a device-wide sync would wait ~2 s for `resident`
+    if inbox:
+        assert inbox in realtime._INBOX_POOL
+        b = FrameServer(hu.solver, idle_ms=50)
+        assert b._inbox == inbox                           # reused, its sequence word reset to 0
+        for i in range(4):
+            _, dof, _ = b(g["body"][i], g["lh"][i], g["rh"][i])
+            np.testing.assert_array_equal(dof.numpy(), dof_b[i].numpy())
+        b.close()
+    _, dof, _ = resident(g["body"][2], g["lh"][2], g["rh"][2])
+    np.testing.assert_array_equal(dof.numpy(), dof_b[2].numpy())
+    resident.close()
 
 
 def test_per_frame_calls_do_not_stall_device_synchronize(gpu):

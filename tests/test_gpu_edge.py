@@ -296,3 +296,41 @@ def test_bench_device_path_two_ranks_on_one_gpu():
     # line names the collective backend and the RCCL build torch carries
     assert [d["rank"] for d in line["devices"]] == [0, 1] and all(d["pci"] for d in line["devices"])
     assert line["comm"]["backend"] == "gloo" and line["comm"]["rccl_version"]
+
+
+_BAD_STREAM_CHILD = r"""
+import ctypes, sys, numpy as np, torch
+sys.path.insert(0, sys.argv[1]); sys.path.insert(0, sys.argv[2])
+from conftest import golden
+from rtg import _lib, assets, ops
+from rtg._lib import lib
+from rtg.runtime import Solver, Topology, ptr
+zp = golden("zero_pose")
+S = Solver(_lib.SOLVER_FULL_BODY_POS, zp["vtrdyn_full_local_t"], zp["vtrdyn_full_global_t"], assets.parents("vtrdyn_full"), True)
+T = Topology(assets.parents("vtrdyn_full"), assets.local_translation("vtrdyn_full"), assets.tree_quat("vtrdyn_full"))
+hip = ctypes.CDLL("libamdhip64.so")
+st = ctypes.c_void_p()
+assert hip.hipStreamCreate(ctypes.byref(st)) == 0 and hip.hipStreamDestroy(st) == 0   # a handle HIP no longer knows
+for B in (1, 16, 4096, 8192, 65536):   # k_fbp_frame1, k_fbp_quad (8 and 16 frames), k_fbp_latency5, k_solve_sides
+    b, l, r = ops.synth_full_body(T, B, seed=5)
+    dof = torch.empty((B, 30), device="cuda")
+    torch.cuda.synchronize()
+    rc = lib().rtg_retarget_f32(S.handle, ptr(b), ptr(l), ptr(r), None, B, _lib.LAYOUT_AOS, ptr(dof), None, None, st.value)
+    print("B", B, "rc", rc, lib().rtg_last_error().decode() if rc else "")
+    sys.stdout.flush()
+"""
+
+
+def test_failed_launch_is_reported_on_every_kernel(gpu):
+    """a launch that fails (here: a stream handle HIP has destroyed) returns a non-OK status from
+    rtg_retarget_f32 on every FULL_BODY_POS kernel, the small-batch ones included -- launch_fbp_small reads the error
+    state itself, and its result is now passed up instead of a second, already cleared hipGetLastError()."""
+    r = subprocess.run([sys.executable, "-c", _BAD_STREAM_CHILD, PKG, os.path.join(REPO, "tests")],
+                       capture_output=True, text=True, timeout=120)
+    if r.returncode < 0:
+        pytest.skip(f"the HIP runtime did not validate the destroyed stream handle (signal {-r.returncode})")
+    assert r.returncode == 0, r.stdout + r.stderr
+    lines = [x for x in r.stdout.splitlines() if x.startswith("B ")]
+    assert len(lines) == 5, r.stdout + r.stderr
+    for x in lines:
+        assert " rc 0 " not in x + " " and "launch" in x, x
