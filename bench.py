@@ -268,11 +268,19 @@ def secondary_configs(solver, sets, stream):
     d = torch.empty((n, 30), device=xb.device)
     for _ in range(10):
         solver.retarget([xb, xl, xr], out_dof=d)
+    # timed through the C ABI with the arguments built once: Solver.retarget's checks cost ~15-20 us of host time
+    # per call, about the kernel's own, so back-to-back Python calls would time the host
+    from rtg import _lib
+    from rtg._lib import lib
+    from rtg.runtime import ptr, stream_handle
+    args = (solver.handle, ptr(xb), ptr(xl), ptr(xr), None, n, _lib.LAYOUT_AOS, ptr(d), None, None,
+            stream_handle(stream))
+    launch = lib().rtg_retarget_f32
     reps = 200
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     e0.record(stream)
     for _ in range(reps):
-        solver.retarget([xb, xl, xr], out_dof=d)
+        launch(*args)
     e1.record(stream)
     e1.synchronize()
     k_ms = e0.elapsed_time(e1) / reps
@@ -297,11 +305,18 @@ def secondary_configs(solver, sets, stream):
         nbytes += 65536 * (J * 16 + 12 + J * 28)        # FK: local rotations + root in, rotations + positions out
         inv.append((t, ops.forward_kinematics(t, lr, torch.zeros((65536, 3), device="cuda"))[0]))
         nbytes += 65536 * (J * 16 + J * 16)             # inverse FK: global rotations in, local rotations out
+    # the segment tables and outputs built once, the launch through the C ABI: ops.kinematics_multi allocates its
+    # outputs per call, and that host time (~0.1 ms) would be what back-to-back calls measure
+    from rtg._lib import check, lib
+    from rtg.runtime import stream_handle
+    fsegs, fkeep, fouts = ops._fk_segments(fk)
+    isegs, ikeep, iouts = ops._inv_segments(inv)
+    launch, sh = lib().rtg_kinematics_multi_f32, stream_handle(stream)
     for _ in range(5):
-        ops.kinematics_multi(fk, inv)
+        check(launch(fsegs, len(fk), isegs, len(inv), sh))
     e0.record(stream)
     for _ in range(50):
-        ops.kinematics_multi(fk, inv)
+        launch(fsegs, len(fk), isegs, len(inv), sh)
     e1.record(stream)
     e1.synchronize()
     ms = e0.elapsed_time(e1) / 50

@@ -11,6 +11,7 @@
 #include <cstring>
 #include <ctime>
 #include <new>
+#include <vector>
 #include <string>
 #include <utility>
 
@@ -25,7 +26,12 @@ struct rtg_topology_s {
     Q *d_tree_quat = nullptr;
     int32_t *d_sched = nullptr;
     int32_t nslots = 0;
-    TopoView view() const { return TopoView{d_parents, d_local_t, d_tree_quat, d_sched, J, nslots}; }
+    GEnt *d_gsched = nullptr;   // lane-group FK schedule (J <= kGroupMaxJ), see fk_group_schedule
+    int32_t gF = 0, gsteps = 0;
+    TopoView view() const
+    {
+        return TopoView{d_parents, d_local_t, d_tree_quat, d_sched, J, nslots, d_gsched, gF, gsteps};
+    }
 };
 
 // HuForwardModel: the topology is borrowed (it must outlive the model); axis / limits are owned.
@@ -145,6 +151,22 @@ int rtg_topology_create(const int32_t *parents, const float *local_t, const floa
     if (rc == RTG_OK) rc = hip_check(hipMalloc(&t->d_sched, sizeof(int32_t) * J), "hipMalloc(sched)");
     if (rc == RTG_OK)
         rc = hip_check(hipMemcpy(t->d_sched, sched, sizeof(int32_t) * J, hipMemcpyHostToDevice), "hipMemcpy");
+    // the lane-group schedule (rtg_fk.hip): J <= kGroupMaxJ, at most J steps
+    const int gF = group_frames(J);
+    if (rc == RTG_OK && gF > 0) {
+        std::vector<V> lt(J);
+        for (int j = 0; j < J; ++j) lt[j] = v3(local_t, j);
+        std::vector<GEnt> gs((size_t)J * (64 / gF));
+        const int steps = fk_group_schedule(parents, lt.data(), tq, J, gF, gs.data(), J);
+        if (steps > 0) {
+            rc = hip_check(hipMalloc(&t->d_gsched, sizeof(GEnt) * steps * (64 / gF)), "hipMalloc(group schedule)");
+            if (rc == RTG_OK)
+                rc = hip_check(hipMemcpy(t->d_gsched, gs.data(), sizeof(GEnt) * steps * (64 / gF), hipMemcpyHostToDevice),
+                               "hipMemcpy");
+            t->gF = gF;
+            t->gsteps = steps;
+        }
+    }
     delete[] tq;
     delete[] sched;
     if (rc != RTG_OK) {
@@ -152,6 +174,7 @@ int rtg_topology_create(const int32_t *parents, const float *local_t, const floa
         (void)hipFree(t->d_local_t);
         (void)hipFree(t->d_tree_quat);
         (void)hipFree(t->d_sched);
+        (void)hipFree(t->d_gsched);
         delete t;
         return rc;
     }
@@ -166,6 +189,7 @@ int rtg_topology_destroy(rtg_topology_t t)
     (void)hipFree(t->d_local_t);
     (void)hipFree(t->d_tree_quat);
     (void)hipFree(t->d_sched);
+    (void)hipFree(t->d_gsched);
     delete t;
     return RTG_OK;
 }
@@ -272,7 +296,7 @@ int rtg_dof_model_create(rtg_topology_t topo, const int32_t *axis, const float *
     if (!out) return fail(RTG_ERR_INVALID_ARGUMENT, "rtg_dof_model_create: out is NULL");
     *out = nullptr;
     if (!topo) return fail(RTG_ERR_INVALID_ARGUMENT, "rtg_dof_model_create: NULL topology");
-    if (topo->nslots > kMaxFkSlots)
+    if (!topo->d_gsched && topo->nslots > kMaxFkSlots)
         return fail(RTG_ERR_UNSUPPORTED, "rtg_dof_model_create: topology needs %d branch slots (max %d)", topo->nslots,
                     kMaxFkSlots);
     const int n = topo->J - 1;

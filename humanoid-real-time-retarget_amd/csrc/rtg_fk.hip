@@ -2,6 +2,9 @@
 // hu_forward_model.py:17-33) and their launchers.
 #include "rtg_device.cuh"
 
+#include <algorithm>
+#include <vector>
+
 namespace rtg {
 
 // ----------------------------------------------------------------------------
@@ -600,10 +603,377 @@ __global__ __launch_bounds__(256) void k_fk_multi(FkMultiArgs A)
     for (int j = 1; j < S.T.J; ++j) st4(l + 4 * j, qmul_norm(qconj(ld4(g + 4 * S.T.parents[j])), ld4(g + 4 * j)));
 }
 
+// ----------------------------------------------------------------------------
+// Lane-group kinematics (round 6): a frame's joints spread over a GROUP of lanes, F frames per wave (F = 16: four
+// lanes per frame for J <= 36; F = 8: eight lanes for J <= 64), so the tile's rows move as whole coalesced pieces.
+// The windowed kernels above keep one frame per lane, and each of their load / store instructions touches 64 rows
+// ~500 bytes apart (FETCH 1.75x, WRITE 1.22x the algorithmic bytes on Hu FK, round 4 PMC; a memory-pattern probe of
+// those pieces alone tops out at 3.45 TB/s).  Here the F frames of a tile are F J consecutive 16-byte records: lane
+// l of load k takes record 64 k + l, so every instruction reads or writes 1 KiB of consecutive bytes, each line of
+// the rows is requested once, and the positions leave as consecutive dwordx4 pieces.  The records go through LDS:
+//   1. every record of the tile is loaded (all loads in flight) and stored into the LDS image of the rows;
+//   2. the joints are composed by a host-built list schedule (fk_group_schedule): at step s, sub-lane u of each
+//      frame's group composes the joint the schedule names, reading its parent's global transform from the image and
+//      writing its own over its local rotation -- a parent is always composed at an earlier step.  Each joint is
+//      composed exactly as in kinematics.py:27-37 / fk_stream_tile (same device functions, same operands, same
+//      order), so the bits are the same whatever the schedule; only which lane does it and when changes.  Hu: 31
+//      joints in 10 steps (its depth + 1) on four lanes;
+//   3. the global rotations and positions leave from the image, record-ordered (coalesced).
+// LDS per wave: F J 28 bytes plus the schedule (Hu: 13.9 + 1.3 KiB).  Inverse FK (kinematics.py:41-63) has no chain:
+// each record's parent is read from the image and its local rotation stored straight from the lane that loaded it.
+// ----------------------------------------------------------------------------
+template <int F>
+struct Grp {
+    static_assert(F == 16 || F == 8, "lane groups of 4 or 8 lanes");
+    static constexpr int L = 64 / F;             // lanes per frame
+    static constexpr int LOG_L = F == 16 ? 2 : 3;
+    static constexpr int NR = F == 16 ? 9 : 8;   // records per lane: F J <= 64 NR (group_frames)
+};
+__host__ __device__ inline size_t pad16f(size_t nfloats) { return (nfloats + 3) & ~(size_t)3; }
+// rot [F J] float4 | pos [F J 3] float | schedule [gsteps L] GEnt | extra floats (kernel-specific tables)
+__host__ __device__ inline size_t group_lds_floats(int J, int F, int steps)
+{
+    return (size_t)F * J * 4 + pad16f((size_t)F * J * 3) + (size_t)steps * (64 / F) * 8;
+}
+
+// the tile's schedule into LDS (float4 copies, in flight with the tile's own loads)
+RTG_DEV void group_sched_fill(const TopoView &T, int L, GEnt *sch)
+{
+    const int n = T.gsteps * L * 2;
+    const f4v *gs = reinterpret_cast<const f4v *>(T.gsched);
+    f4v *d = reinterpret_cast<f4v *>(sch);
+    for (int i = (int)threadIdx.x; i < n; i += 64) d[i] = gs[i];
+}
+
+// The schedule's steps over the tile image (rot: global rotations written over the local ones; pos: positions, the
+// root's preset).  LQ(j, lq) gives joint j's local rotation from its image record (FK: the record itself, with the
+// tree quaternion when STATE; DOF FK: built from the joint angle).
+template <int F, typename LocalQ>
+RTG_DEV void group_compose(const TopoView &T, f4v *rot, float *pos, const GEnt *sch, int nfr, const LocalQ &LQ)
+{
+    using G = Grp<F>;
+    const int J = T.J, lane = (int)threadIdx.x;
+    const int fr = lane >> G::LOG_L, sub = lane & (G::L - 1);
+    const bool live = fr < nfr;
+    const int base = fr * J;
+    for (int s = 0; s < T.gsteps; ++s) {
+        const GEnt e = sch[s * G::L + sub];
+        const int j = e.code & 0xFF, p = (e.code >> 8) & 0xFF;
+        if (live && j != 0xFF) {
+            const f4v lv = rot[base + j];
+            Q ng;
+            V nt;
+            if (j == 0) {   // root: global = local, unnormalised; position = the root translation (kinematics.py:27-29)
+                ng = Q{lv.x, lv.y, lv.z, lv.w};
+                nt = V{pos[3 * base], pos[3 * base + 1], pos[3 * base + 2]};
+            } else {
+                const Q lq = LQ(j, Q{lv.x, lv.y, lv.z, lv.w}, e, fr);
+                const f4v gv = rot[base + p];
+                const Q g{gv.x, gv.y, gv.z, gv.w};
+                const float *tp = pos + 3 * (base + p);
+                const V t{tp[0], tp[1], tp[2]};
+                const V rv = qrotate(g, V{e.lx, e.ly, e.lz});
+                ng = qmul_norm(g, lq);
+                nt = V{rv.x + t.x, rv.y + t.y, rv.z + t.z};
+            }
+            rot[base + j] = f4v{ng.x, ng.y, ng.z, ng.w};
+            float *op = pos + 3 * (base + j);
+            op[0] = nt.x; op[1] = nt.y; op[2] = nt.z;
+        }
+        wave_sync();   // this step's records before the next step's parent reads (other lanes)
+    }
+}
+
+// the tile image out: rotations record-ordered, positions as consecutive dwordx4 pieces (16-byte aligned rows; any
+// other g_pos alignment stores dword by dword)
+template <int F>
+RTG_DEV void group_store(const f4v *rot, const float *pos, int nrec, float *__restrict__ g_rot, float *__restrict__ g_pos)
+{
+    using G = Grp<F>;
+    const int lane = (int)threadIdx.x;
+    f4v *dst = reinterpret_cast<f4v *>(g_rot);
+    f4v o[G::NR];   // every LDS read first (unconditional), then the stores: no wait between two stores
+#pragma unroll
+    for (int k = 0; k < G::NR; ++k) {
+        const int rec = k * 64 + lane;
+        o[k] = rot[rec < nrec ? rec : 0];
+    }
+#pragma unroll
+    for (int k = 0; k < G::NR; ++k) {
+        const int rec = k * 64 + lane;
+        if (rec < nrec) dst[rec] = o[k];
+    }
+    const int npos = 3 * nrec;
+    if ((reinterpret_cast<uintptr_t>(g_pos) & 15u) == 0) {
+        const int n4 = npos >> 2;
+        f4v *pd = reinterpret_cast<f4v *>(g_pos);
+        const f4v *ps = reinterpret_cast<const f4v *>(pos);
+        for (int i = lane; i < n4; i += 64) pd[i] = ps[i];
+        for (int i = 4 * n4 + lane; i < npos; i += 64) g_pos[i] = pos[i];
+    } else {
+        for (int i = lane; i < npos; i += 64) g_pos[i] = pos[i];
+    }
+}
+
+// the tile's NR records per lane, all loads in flight (unconditional: a lane past the tile re-reads record 0, so no
+// branch separates them), then -- after the caller's other loads -- into the LDS image
+template <int F>
+struct GroupRows {
+    f4v v[Grp<F>::NR];
+    RTG_DEV void load(const float *__restrict__ rows, int nrec)
+    {
+        const f4v *src = reinterpret_cast<const f4v *>(rows);
+#pragma unroll
+        for (int k = 0; k < Grp<F>::NR; ++k) {
+            const int rec = k * 64 + (int)threadIdx.x;
+            v[k] = src[rec < nrec ? rec : 0];
+        }
+    }
+    RTG_DEV void to_lds(f4v *rot, int nrec) const
+    {
+#pragma unroll
+        for (int k = 0; k < Grp<F>::NR; ++k) {
+            const int rec = k * 64 + (int)threadIdx.x;
+            if (rec < nrec) rot[rec] = v[k];
+        }
+    }
+};
+
+template <bool STATE, int F>
+RTG_DEV void fk_group_tile(const TopoView &T, const float *__restrict__ local_rot, const float *__restrict__ root_t,
+                           int64_t B, int64_t f0, float *__restrict__ g_rot, float *__restrict__ g_pos, float *lds)
+{
+    const int J = T.J, lane = (int)threadIdx.x;
+    const int nfr = (int)((B - f0) < F ? (B - f0) : F);
+    const int nrec = nfr * J;
+    f4v *rot = reinterpret_cast<f4v *>(lds);
+    float *pos = lds + 4 * F * J;
+    GEnt *sch = reinterpret_cast<GEnt *>(pos + pad16f((size_t)3 * F * J));
+    GroupRows<F> rows;
+    rows.load(local_rot + f0 * J * 4, nrec);
+    const float r = root_t[f0 * 3 + (lane < 3 * nfr ? lane : 0)];
+    group_sched_fill(T, Grp<F>::L, sch);
+    rows.to_lds(rot, nrec);
+    if (lane < 3 * nfr) {
+        const int fr = lane / 3;
+        pos[3 * J * fr + (lane - 3 * fr)] = r;
+    }
+    wave_sync();
+    group_compose<F>(T, rot, pos, sch, nfr, [&](int, Q lq, const GEnt &e, int) {
+        if (STATE) lq = qmul_norm(Q{e.qx, e.qy, e.qz, e.qw}, lq);   // skeleton3d.py:412-418
+        return lq;
+    });
+    group_store<F>(rot, pos, nrec, g_rot + f0 * J * 4, g_pos + f0 * J * 3);
+}
+
+template <bool STATE, int F>
+__global__ __launch_bounds__(64, 4) void k_fk_group(TopoView T, const float *__restrict__ local_rot,
+                                                 const float *__restrict__ root_t, int64_t B, float *__restrict__ g_rot,
+                                                 float *__restrict__ g_pos)
+{
+    extern __shared__ __attribute__((aligned(16))) float fk_lds[];
+    fk_group_tile<STATE, F>(T, local_rot, root_t, B, (int64_t)blockIdx.x * F, g_rot, g_pos, fk_lds);
+}
+
+// inverse FK: LDS = the tile image | parents (J ints) | STATE: normalised conjugate tree quaternions (J float4)
+static inline size_t lrot_group_lds_floats(int J, int F) { return (size_t)F * J * 4 + pad16f((size_t)J) + (size_t)J * 4; }
+template <bool STATE, int F>
+RTG_DEV void lrot_group_tile(const TopoView &T, const float *__restrict__ g_rot, int64_t B, int64_t f0,
+                             float *__restrict__ local_rot, float *lds)
+{
+    using G = Grp<F>;
+    const int J = T.J, lane = (int)threadIdx.x;
+    const int nfr = (int)((B - f0) < F ? (B - f0) : F);
+    const int nrec = nfr * J;
+    f4v *rot = reinterpret_cast<f4v *>(lds);
+    int *par = reinterpret_cast<int *>(lds + 4 * F * J);
+    f4v *tqn = reinterpret_cast<f4v *>(lds + 4 * F * J + pad16f((size_t)J));
+    const f4v *src = reinterpret_cast<const f4v *>(g_rot + f0 * J * 4);
+    f4v v[G::NR];   // unconditional loads (a lane past the tile re-reads record 0): no branch between them
+#pragma unroll
+    for (int k = 0; k < G::NR; ++k) {
+        const int rec = k * 64 + lane;
+        v[k] = src[rec < nrec ? rec : 0];
+    }
+    for (int j = lane; j < J; j += 64) {
+        par[j] = ld_const(T.parents + j);
+        if (STATE) {   // skeleton3d.py:470-478: quat_normalize(quat_conjugate(tree quat)), once per joint
+            const Q c = qnormalize(qconj(ld_const(T.tree_quat + j)));
+            tqn[j] = f4v{c.x, c.y, c.z, c.w};
+        }
+    }
+#pragma unroll
+    for (int k = 0; k < G::NR; ++k) {
+        const int rec = k * 64 + lane;
+        if (rec < nrec) rot[rec] = v[k];
+    }
+    wave_sync();
+    const float rJ = 1.0f / (float)J;   // rec / J as ((rec + 1/2) / J) truncated: exact for rec < 2^12, J <= 64
+    f4v *dst = reinterpret_cast<f4v *>(local_rot + f0 * J * 4);
+#pragma unroll 3
+    for (int k = 0; k < G::NR; ++k) {   // the records from the image: the loaded registers are free by now
+        const int rec = k * 64 + lane;
+        if (rec < nrec) {
+            const int fr = (int)(((float)rec + 0.5f) * rJ), j = rec - fr * J;
+            const f4v gv = rot[rec];
+            const Q gj{gv.x, gv.y, gv.z, gv.w};
+            Q q = gj;   // root copied (kinematics.py:49)
+            if (j > 0) {
+                const f4v pv = rot[fr * J + par[j]];
+                q = qmul_norm(qconj(Q{pv.x, pv.y, pv.z, pv.w}), gj);
+                if (STATE) {
+                    const f4v c = tqn[j];
+                    q = qmul_norm(Q{c.x, c.y, c.z, c.w}, q);
+                }
+            }
+            dst[rec] = f4v{q.x, q.y, q.z, q.w};
+        }
+    }
+}
+
+template <bool STATE, int F>
+__global__ __launch_bounds__(64, 4) void k_lrot_group(TopoView T, const float *__restrict__ g_rot, int64_t B,
+                                                   float *__restrict__ local_rot)
+{
+    extern __shared__ __attribute__((aligned(16))) float fk_lds[];
+    lrot_group_tile<STATE, F>(T, g_rot, B, (int64_t)blockIdx.x * F, local_rot, fk_lds);
+}
+
+// HuForwardModel (hu_forward_model.py:17-33) on the lane groups: LDS = the tile image (root rotation at joint 0) |
+// the tile's DOF rows (F (J - 1) floats) | per-joint {axis, lower, upper}
+static inline size_t dof_group_lds_floats(int J, int F, int steps)
+{
+    return group_lds_floats(J, F, steps) + pad16f((size_t)F * (J - 1)) + (size_t)J * 4;
+}
+template <bool CLIP, int F>
+__global__ __launch_bounds__(64, 4) void k_dof_fk_group(TopoView T, DofView D, const float *__restrict__ dof,
+                                                     const float *__restrict__ root_rot,
+                                                     const float *__restrict__ root_t, int64_t B,
+                                                     float *__restrict__ g_rot, float *__restrict__ g_pos)
+{
+    extern __shared__ __attribute__((aligned(16))) float fk_lds[];
+    using G = Grp<F>;
+    const int J = T.J, lane = (int)threadIdx.x, nd = J - 1;
+    const int64_t f0 = (int64_t)blockIdx.x * F;
+    const int nfr = (int)((B - f0) < F ? (B - f0) : F);
+    const int nrec = nfr * J;
+    f4v *rot = reinterpret_cast<f4v *>(fk_lds);
+    float *pos = fk_lds + 4 * F * J;
+    GEnt *sch = reinterpret_cast<GEnt *>(pos + pad16f((size_t)3 * F * J));
+    float *ang = fk_lds + group_lds_floats(J, F, T.gsteps);
+    f4v *ntab = reinterpret_cast<f4v *>(ang + pad16f((size_t)F * nd));
+    // the tile's DOF rows are nfr * nd consecutive floats: NR dword loads per lane, all in flight
+    const float *drow = dof + f0 * nd;
+    const int nang = nfr * nd;
+    float a[G::NR];   // unconditional loads (a lane past the rows re-reads element 0)
+#pragma unroll
+    for (int k = 0; k < G::NR; ++k) {
+        const int i = k * 64 + lane;
+        a[k] = drow[i < nang ? i : 0];
+    }
+    const f4v rr = reinterpret_cast<const f4v *>(root_rot)[f0 + (lane < nfr ? lane : 0)];
+    const float rt = root_t[f0 * 3 + (lane < 3 * nfr ? lane : 0)];
+    group_sched_fill(T, G::L, sch);
+    for (int j = 1 + lane; j < J; j += 64) {
+        const int ax = ld_const(D.axis + (j - 1));
+        ntab[j] = f4v{__int_as_float(ax), CLIP ? ld_const(D.lower + (j - 1)) : 0.0f,
+                      CLIP ? ld_const(D.upper + (j - 1)) : 0.0f, 0.0f};
+    }
+#pragma unroll
+    for (int k = 0; k < G::NR; ++k) {
+        const int i = k * 64 + lane;
+        if (i < nang) ang[i] = a[k];
+    }
+    if (lane < nfr) rot[lane * J] = rr;   // root: global = the root rotation (hu_forward_model.py:24)
+    if (lane < 3 * nfr) {
+        const int fr = lane / 3;
+        pos[3 * J * fr + (lane - 3 * fr)] = rt;
+    }
+    wave_sync();
+    group_compose<F>(T, rot, pos, sch, nfr, [&](int j, Q, const GEnt &, int fr) {
+        const f4v t = ntab[j];
+        float x = ang[fr * nd + (j - 1)];
+        if (CLIP) {   // torch.clamp (min then max; NaN passes), then the straight-through sum
+            float c = x < t.y ? t.y : x;
+            c = c > t.z ? t.z : c;
+            x = (c - x) + x;
+        }
+        const int ax = __float_as_int(t.x);
+        // the axis is an exact unit vector: quat_from_angle_axis's normalisation is the identity (round 5)
+        return qfrom_angle_unit_axis(x, V{ax == 0 ? 1.0f : 0.0f, ax == 1 ? 1.0f : 0.0f, ax == 2 ? 1.0f : 0.0f});
+    });
+    group_store<F>(rot, pos, nrec, g_rot + f0 * J * 4, g_pos + f0 * J * 3);
+}
+
+// Mixed-target kinematics on the lane groups (config 5): a block is one tile of one segment; the segment's F comes
+// from its topology
+__global__ __launch_bounds__(64, 4) void k_fk_multi_group(FkMultiArgs A)
+{
+    extern __shared__ __attribute__((aligned(16))) float fk_lds[];
+    int s = 0;
+#pragma unroll
+    for (int i = 1; i < RTG_MAX_SEGMENTS; ++i)
+        if (i < A.n && (int64_t)blockIdx.x >= A.block_start[i]) s = i;
+    const FkSeg &S = A.seg[s];
+    const int64_t t = (int64_t)blockIdx.x - A.block_start[s];
+    if (S.T.gF == 16) {
+        if (S.op == 0) fk_group_tile<false, 16>(S.T, S.local_rot, S.root_t, S.B, t * 16, S.g_rot, S.g_pos, fk_lds);
+        else lrot_group_tile<false, 16>(S.T, S.local_rot, S.B, t * 16, S.g_rot, fk_lds);
+    } else {
+        if (S.op == 0) fk_group_tile<false, 8>(S.T, S.local_rot, S.root_t, S.B, t * 8, S.g_rot, S.g_pos, fk_lds);
+        else lrot_group_tile<false, 8>(S.T, S.local_rot, S.B, t * 8, S.g_rot, fk_lds);
+    }
+}
+
+// Host: the lane-group list schedule.  Joints become ready once their parent's step is past; each step takes up to L
+// ready joints, longest remaining chain (height) first, ties by index -- for a tree that is the critical-path bound
+// (depth + 1 steps) whenever L covers the widest level the chains keep busy (Hu on 4 lanes: 10 steps for 31 joints).
+// The bits do not depend on it (group_compose).  Returns the step count, or -1 if it would exceed max_steps.
+int32_t fk_group_schedule(const int32_t *parents, const V *local_t, const Q *tree_quat, int32_t J, int32_t F,
+                          GEnt *out, int32_t max_steps)
+{
+    const int L = 64 / F;
+    std::vector<int> h(J, 1), done(J, -1);
+    for (int j = J - 1; j > 0; --j) h[parents[j]] = std::max(h[parents[j]], h[j] + 1);
+    int steps = 0, placed = 0;
+    std::vector<int> ready;
+    while (placed < J) {
+        if (steps >= max_steps) return -1;
+        ready.clear();
+        for (int j = 0; j < J; ++j)
+            if (done[j] < 0 && (j == 0 || (done[parents[j]] >= 0 && done[parents[j]] < steps))) ready.push_back(j);
+        std::stable_sort(ready.begin(), ready.end(), [&](int a, int b) { return h[a] > h[b]; });
+        for (int u = 0; u < L; ++u) {
+            GEnt &e = out[steps * L + u];
+            e = GEnt{0.f, 0.f, 0.f, 0xFFFF, 0.f, 0.f, 0.f, 1.f};
+            if (u < (int)ready.size()) {
+                const int j = ready[u];
+                done[j] = steps;
+                ++placed;
+                e = GEnt{local_t[j].x, local_t[j].y, local_t[j].z, j | ((j ? parents[j] : 0xFF) << 8),
+                         tree_quat[j].x, tree_quat[j].y, tree_quat[j].z, tree_quat[j].w};
+            }
+        }
+        ++steps;
+    }
+    return steps;
+}
+
 hipError_t launch_fk(const TopoView &T, bool state, const float *lr, const float *rt, int64_t B, float *gr, float *gp,
                      hipStream_t s)
 {
-    if (T.nslots <= kMaxFkSlots) {
+    if (RTG_FK_GROUP && T.gsched) {
+        const int F = T.gF;
+        const size_t lds = sizeof(float) * group_lds_floats(T.J, F, T.gsteps);
+        const dim3 g(grid_for(B, F)), b(64);
+        if (F == 16) {
+            if (state) hipLaunchKernelGGL((k_fk_group<true, 16>), g, b, lds, s, T, lr, rt, B, gr, gp);
+            else hipLaunchKernelGGL((k_fk_group<false, 16>), g, b, lds, s, T, lr, rt, B, gr, gp);
+        } else {
+            if (state) hipLaunchKernelGGL((k_fk_group<true, 8>), g, b, lds, s, T, lr, rt, B, gr, gp);
+            else hipLaunchKernelGGL((k_fk_group<false, 8>), g, b, lds, s, T, lr, rt, B, gr, gp);
+        }
+    } else if (T.nslots <= kMaxFkSlots) {
         const dim3 g(grid_for(B, kFkTile)), b(kFkTile);
         const size_t lds = fk_stream_lds_bytes(T.nslots);
         if (state) hipLaunchKernelGGL(k_fk_stream<true>, g, b, lds, s, T, lr, rt, B, gr, gp);
@@ -618,7 +988,18 @@ hipError_t launch_fk(const TopoView &T, bool state, const float *lr, const float
 
 hipError_t launch_local_rotation(const TopoView &T, bool state, const float *g, int64_t B, float *l, hipStream_t s)
 {
-    if (T.nslots <= kMaxFkSlots) {
+    if (RTG_FK_GROUP && T.gsched) {
+        const int F = T.gF;
+        const size_t lds = sizeof(float) * lrot_group_lds_floats(T.J, F);
+        const dim3 gd(grid_for(B, F)), b(64);
+        if (F == 16) {
+            if (state) hipLaunchKernelGGL((k_lrot_group<true, 16>), gd, b, lds, s, T, g, B, l);
+            else hipLaunchKernelGGL((k_lrot_group<false, 16>), gd, b, lds, s, T, g, B, l);
+        } else {
+            if (state) hipLaunchKernelGGL((k_lrot_group<true, 8>), gd, b, lds, s, T, g, B, l);
+            else hipLaunchKernelGGL((k_lrot_group<false, 8>), gd, b, lds, s, T, g, B, l);
+        }
+    } else if (T.nslots <= kMaxFkSlots) {
         const dim3 gd(grid_for(B, kFkTile)), b(kFkTile);
         const size_t lds = fk_line_lds_bytes(T.J, T.nslots);
         if (state) hipLaunchKernelGGL(k_local_rotation_line<true>, gd, b, lds, s, T, g, B, l);
@@ -633,6 +1014,23 @@ hipError_t launch_local_rotation(const TopoView &T, bool state, const float *g, 
 
 hipError_t launch_fk_multi(FkMultiArgs &A, hipStream_t s)
 {
+    bool group = RTG_FK_GROUP != 0;
+    for (int i = 0; i < A.n; ++i) group = group && A.seg[i].T.gsched != nullptr;
+    if (group) {   // every segment on the lane groups: one block per F-frame tile of its segment
+        int64_t blocks = 0;
+        size_t lds = 0;
+        for (int i = 0; i < A.n; ++i) {
+            const TopoView &T = A.seg[i].T;
+            A.block_start[i] = blocks;
+            blocks += grid_for(A.seg[i].B, T.gF);
+            const size_t need = A.seg[i].op == 0 ? group_lds_floats(T.J, T.gF, T.gsteps) : lrot_group_lds_floats(T.J, T.gF);
+            lds = need > lds ? need : lds;
+        }
+        for (int i = A.n; i < RTG_MAX_SEGMENTS; ++i) A.block_start[i] = blocks;
+        if (blocks == 0) return hipSuccess;
+        hipLaunchKernelGGL(k_fk_multi_group, dim3((unsigned)blocks), dim3(64), sizeof(float) * lds, s, A);
+        return hipGetLastError();
+    }
     int maxS = 0;
     for (int i = 0; i < A.n; ++i) maxS = A.seg[i].T.nslots > maxS ? A.seg[i].T.nslots : maxS;
     const bool stream = maxS <= kMaxFkSlots;
@@ -658,6 +1056,19 @@ hipError_t launch_fk_multi(FkMultiArgs &A, hipStream_t s)
 hipError_t launch_dof_fk(const TopoView &T, const DofView &D, bool clip, const float *dof, const float *root_rot,
                          const float *root_t, int64_t B, float *gr, float *gp, hipStream_t s)
 {
+    if (RTG_FK_GROUP && T.gsched) {
+        const int F = T.gF;
+        const size_t lds = sizeof(float) * dof_group_lds_floats(T.J, F, T.gsteps);
+        const dim3 g(grid_for(B, F)), b(64);
+        if (F == 16) {
+            if (clip) hipLaunchKernelGGL((k_dof_fk_group<true, 16>), g, b, lds, s, T, D, dof, root_rot, root_t, B, gr, gp);
+            else hipLaunchKernelGGL((k_dof_fk_group<false, 16>), g, b, lds, s, T, D, dof, root_rot, root_t, B, gr, gp);
+        } else {
+            if (clip) hipLaunchKernelGGL((k_dof_fk_group<true, 8>), g, b, lds, s, T, D, dof, root_rot, root_t, B, gr, gp);
+            else hipLaunchKernelGGL((k_dof_fk_group<false, 8>), g, b, lds, s, T, D, dof, root_rot, root_t, B, gr, gp);
+        }
+        return hipGetLastError();
+    }
     if (T.nslots > kMaxFkSlots) return hipErrorInvalidValue;   // rejected at rtg_dof_model_create
     const dim3 g(grid_for(B, kFkTile)), b(kFkTile);
     const size_t lds = dof_fk_lds_bytes(T.nslots);

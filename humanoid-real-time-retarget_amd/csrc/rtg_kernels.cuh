@@ -5,6 +5,16 @@
 
 namespace rtg {
 
+// One (step, sub-lane) entry of the lane-group FK schedule (fk_group_schedule, rtg_fk.hip): at step s, sub-lane u of
+// every frame's lane group composes joint `code & 0xFF` (0xFF: idle) from its parent `(code >> 8) & 0xFF`, with that
+// joint's zero-pose local translation and tree quaternion alongside (two ds_read_b128 per step).
+struct alignas(16) GEnt {
+    float lx, ly, lz;
+    int32_t code;
+    float qx, qy, qz, qw;
+};
+constexpr int kGroupMaxJ = 64;   // the lane-group kernels serve J <= 64 (every shipped skeleton); larger: lane walks
+
 // Device view of a topology (all pointers device memory, uniform per launch).
 struct TopoView {
     const int32_t *parents;   // (J)   parents[j] < j, root -1
@@ -13,7 +23,15 @@ struct TopoView {
     const int32_t *sched;     // (J)   streaming-FK parent schedule, see fk_schedule()
     int32_t J;
     int32_t nslots;           // branch-parent slots the schedule needs
+    const GEnt *gsched;       // (gsteps * 64 / gF) lane-group schedule, or nullptr (J > kGroupMaxJ)
+    int32_t gF;               // frames per wave of the lane-group kernels (16: J <= 36, 8: J <= 64)
+    int32_t gsteps;           // steps of the lane-group schedule
 };
+// the lane-group frames per wave for J joints (0: J too large, the lane-walk kernels run); F J <= 64 * 9 records
+inline int group_frames(int J) { return J <= 36 ? 16 : (J <= kGroupMaxJ ? 8 : 0); }
+// fills `out` (steps x (64 / F) entries) and returns the step count
+int32_t fk_group_schedule(const int32_t *parents, const V *local_t, const Q *tree_quat, int32_t J, int32_t F,
+                          GEnt *out, int32_t max_steps);
 
 // Streaming-FK schedule.  Joints are visited in index order and a lane keeps
 // the previous joint's global transform in registers, so only a parent that

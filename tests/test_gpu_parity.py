@@ -137,7 +137,9 @@ def _random_tree(rng, J, kind):
     return par
 
 
-@pytest.mark.parametrize("kind,J", [("bushy", 31), ("bushy", 97), ("star", 81), ("chain", 17), ("chain", 1)])
+@pytest.mark.parametrize("kind,J", [("bushy", 31), ("bushy", 97), ("star", 81), ("chain", 17), ("chain", 1),
+                                    ("bushy", 36), ("bushy", 37), ("bushy", 64), ("chain", 64), ("star", 60),
+                                    ("bushy", 65)])
 def test_fk_random_topologies_vs_oracle(gpu, kind, J):
     """Any parent-indexed tree (parents[j] < j): FK, inverse FK and the state
     variants agree bit for bit with the oracle, on ragged batch sizes."""
@@ -166,6 +168,32 @@ def test_fk_random_topologies_vs_oracle(gpu, kind, J):
         ng = _np(ops.quat_normalize(osgr))
         np.testing.assert_array_equal(_np(ops.local_rotation(T, ng, state=True)),
                                       orc.state_local_rotation(par, tq, ng))
+
+
+def test_fk_positions_at_any_alignment(gpu):
+    """The lane-group FK stores a tile's positions as dwordx4 pieces when the position rows are 16-byte aligned and
+    dword by dword otherwise: a g_pos 4 bytes into its buffer (a (B, J, 3) view at an odd row offset) gives the same
+    bits, and the floats around the rows stay untouched."""
+    import ctypes
+
+    import oracle as orc
+    from rtg import assets, synth
+    from rtg._lib import check, lib
+    from rtg.runtime import ptr, stream_handle
+    T = _topo("hu_v5")
+    for B in (16, 1000):
+        lr = torch.from_numpy(synth.random_local_quats(B, 31, 12)).cuda()
+        rt = torch.from_numpy(np.random.default_rng(4).normal(0, 0.3, (B, 3)).astype(np.float32)).cuda()
+        gr = torch.empty((B, 31, 4), device="cuda")
+        buf = torch.full((B * 31 * 3 + 2,), 7.0, device="cuda")
+        check(lib().rtg_fk_f32(T.handle, ptr(lr), ptr(rt), B, ptr(gr), ctypes.c_void_p(buf.data_ptr() + 4),
+                               stream_handle()))
+        torch.cuda.synchronize()
+        ogr, ogp = orc.fk(assets.parents("hu_v5"), assets.local_translation("hu_v5"), lr.cpu().numpy(), rt.cpu().numpy())
+        b = buf.cpu().numpy()
+        assert b[0] == 7.0 and b[-1] == 7.0
+        np.testing.assert_array_equal(b[1:-1].reshape(B, 31, 3), ogp)
+        np.testing.assert_array_equal(_np(gr), ogr)
 
 
 DOF_FK_CASES = [("hu_clip", "hu"), ("hu_noclip", "hu"), ("hu_v5_noclip", "hu_v5")]

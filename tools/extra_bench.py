@@ -147,27 +147,45 @@ def teleop_gaps():
 
 
 def fk():
+    """Kinematics kernels through the C ABI with every output preallocated and the ctypes arguments built once: a
+    Python-level call (ops.*) allocates its outputs and costs 30-130 us of host time, above some of these kernels'
+    own time, so back-to-back ops.* calls timed the host (round 5's 'k_dof_fk 128 us' was that)."""
+    from rtg._lib import check, lib
+    from rtg.runtime import DofModel, ptr, stream_handle
+    import importlib
     res = {}
     B = 262144
+    sh = stream_handle()
     T = topo("hu_v5")
     lr = torch.from_numpy(synth.random_local_quats(B, 31, 5)).cuda()
     rt = torch.zeros((B, 3), device="cuda")
-    ms = time_events(lambda: ops.forward_kinematics(T, lr, rt))
+    gr = torch.empty((B, 31, 4), device="cuda")
+    gp = torch.empty((B, 31, 3), device="cuda")
+    fk_args = (T.handle, ptr(lr), ptr(rt), B, ptr(gr), ptr(gp), sh)
+    f = lib().rtg_fk_f32
+    ms = time_events(lambda: f(*fk_args))
+    check(f(*fk_args))
     res["hu_fk_262144"] = {"ms": ms, "frames_per_s": B / (ms * 1e-3),
                            "GBs_algorithmic": 1376 * B / (ms * 1e-3) / 1e9}
-    g = ops.forward_kinematics(T, lr, rt)[0]
-    ms = time_events(lambda: ops.local_rotation(T, g))
+    lo = torch.empty((B, 31, 4), device="cuda")
+    inv_args = (T.handle, ptr(gr), B, ptr(lo), sh)
+    f = lib().rtg_local_rotation_f32
+    ms = time_events(lambda: f(*inv_args))
+    check(f(*inv_args))
     res["hu_inverse_fk_262144"] = {"ms": ms, "frames_per_s": B / (ms * 1e-3),
                                    "GBs_algorithmic": 31 * 32 * B / (ms * 1e-3) / 1e9}
     # HuForwardModel: joint angles -> FK (33-link Hu, clip on): (J-1)*4 + 16 + 12 in, J*28 out per frame
-    from rtg.runtime import DofModel
-    import importlib
     hu = importlib.import_module("retarget.robot_config.Hu")
     Th = topo("hu")
     M = DofModel(Th, hu.Hu_DOF_AXIS, hu.Hu_DOF_LOWER.numpy(), hu.Hu_DOF_UPPER.numpy())
     dof = (torch.rand((B, 32), device="cuda") - 0.5) * 4
     rr = torch.nn.functional.normalize(torch.randn((B, 4), device="cuda"), dim=-1)
-    ms = time_events(lambda: ops.dof_forward_kinematics(M, dof, rr, rt, clip=True))
+    dgr = torch.empty((B, 33, 4), device="cuda")
+    dgp = torch.empty((B, 33, 3), device="cuda")
+    dof_args = (M.handle, ptr(dof), ptr(rr), ptr(rt), B, 1, ptr(dgr), ptr(dgp), sh)
+    f = lib().rtg_dof_fk_f32
+    ms = time_events(lambda: f(*dof_args))
+    check(f(*dof_args))
     res["hu_dof_fk_262144"] = {"ms": ms, "frames_per_s": B / (ms * 1e-3),
                                "GBs_algorithmic": (32 * 4 + 28 + 33 * 28) * B / (ms * 1e-3) / 1e9}
     segs = []
@@ -178,8 +196,19 @@ def fk():
         segs.append((t, torch.from_numpy(synth.random_local_quats(65536, J, 10 + i)).cuda(),
                      torch.zeros((65536, 3), device="cuda")))
         nbytes += 65536 * (J * 16 + 12 + J * 28)
-    ms = time_events(lambda: ops.forward_kinematics_multi(segs))
+    fsegs, keep, outs = ops._fk_segments(segs)
+    f = lib().rtg_fk_multi_f32
+    ms = time_events(lambda: f(fsegs, len(segs), sh))
+    check(f(fsegs, len(segs), sh))
     res["mixed_4x65536"] = {"ms": ms, "frames_per_s": 4 * 65536 / (ms * 1e-3), "GBs_algorithmic": nbytes / (ms * 1e-3) / 1e9}
+    inv = [(t, ops.forward_kinematics(t, lr4, rt4)[0]) for t, lr4, rt4 in segs]
+    isegs, ikeep, iouts = ops._inv_segments(inv)
+    nb5 = nbytes + sum(65536 * t.num_joints * 32 for t, _ in inv)
+    f = lib().rtg_kinematics_multi_f32
+    ms = time_events(lambda: f(fsegs, len(segs), isegs, len(inv), sh))
+    check(f(fsegs, len(segs), isegs, len(inv), sh))
+    res["config5_fk_and_inverse_4x65536"] = {"ms": ms, "frames_per_s": 4 * 65536 / (ms * 1e-3),
+                                             "GBs_algorithmic": nb5 / (ms * 1e-3) / 1e9}
     return res
 
 
