@@ -24,13 +24,11 @@ struct rtg_topology_s {
     int32_t *d_parents = nullptr;
     V *d_local_t = nullptr;
     Q *d_tree_quat = nullptr;
-    int32_t *d_sched = nullptr;
-    int32_t nslots = 0;
     GEnt *d_gsched = nullptr;   // lane-group FK schedule (J <= kGroupMaxJ), see fk_group_schedule
     int32_t gF = 0, gsteps = 0;
     TopoView view() const
     {
-        return TopoView{d_parents, d_local_t, d_tree_quat, d_sched, J, nslots, d_gsched, gF, gsteps};
+        return TopoView{d_parents, d_local_t, d_tree_quat, J, d_gsched, gF, gsteps};
     }
 };
 
@@ -129,14 +127,10 @@ int rtg_topology_create(const int32_t *parents, const float *local_t, const floa
     if (!t) return fail(RTG_ERR_OUT_OF_MEMORY, "rtg_topology_create: host allocation failed");
     t->J = J;
     Q *tq = new (std::nothrow) Q[J];
-    int32_t *sched = new (std::nothrow) int32_t[J];
-    if (!tq || !sched) {
-        delete[] tq;
-        delete[] sched;
+    if (!tq) {
         delete t;
         return fail(RTG_ERR_OUT_OF_MEMORY, "rtg_topology_create: host allocation failed");
     }
-    t->nslots = fk_schedule(parents, J, sched);
     for (int j = 0; j < J; ++j)
         tq[j] = tree_quat ? Q{tree_quat[4 * j], tree_quat[4 * j + 1], tree_quat[4 * j + 2], tree_quat[4 * j + 3]}
                           : Q{0.f, 0.f, 0.f, 1.f};
@@ -148,9 +142,6 @@ int rtg_topology_create(const int32_t *parents, const float *local_t, const floa
     if (rc == RTG_OK)
         rc = hip_check(hipMemcpy(t->d_local_t, local_t, sizeof(V) * J, hipMemcpyHostToDevice), "hipMemcpy");
     if (rc == RTG_OK) rc = hip_check(hipMemcpy(t->d_tree_quat, tq, sizeof(Q) * J, hipMemcpyHostToDevice), "hipMemcpy");
-    if (rc == RTG_OK) rc = hip_check(hipMalloc(&t->d_sched, sizeof(int32_t) * J), "hipMalloc(sched)");
-    if (rc == RTG_OK)
-        rc = hip_check(hipMemcpy(t->d_sched, sched, sizeof(int32_t) * J, hipMemcpyHostToDevice), "hipMemcpy");
     // the lane-group schedule (rtg_fk.hip): J <= kGroupMaxJ, at most J steps
     const int gF = group_frames(J);
     if (rc == RTG_OK && gF > 0) {
@@ -168,12 +159,10 @@ int rtg_topology_create(const int32_t *parents, const float *local_t, const floa
         }
     }
     delete[] tq;
-    delete[] sched;
     if (rc != RTG_OK) {
         (void)hipFree(t->d_parents);
         (void)hipFree(t->d_local_t);
         (void)hipFree(t->d_tree_quat);
-        (void)hipFree(t->d_sched);
         (void)hipFree(t->d_gsched);
         delete t;
         return rc;
@@ -188,7 +177,6 @@ int rtg_topology_destroy(rtg_topology_t t)
     (void)hipFree(t->d_parents);
     (void)hipFree(t->d_local_t);
     (void)hipFree(t->d_tree_quat);
-    (void)hipFree(t->d_sched);
     (void)hipFree(t->d_gsched);
     delete t;
     return RTG_OK;
@@ -296,9 +284,6 @@ int rtg_dof_model_create(rtg_topology_t topo, const int32_t *axis, const float *
     if (!out) return fail(RTG_ERR_INVALID_ARGUMENT, "rtg_dof_model_create: out is NULL");
     *out = nullptr;
     if (!topo) return fail(RTG_ERR_INVALID_ARGUMENT, "rtg_dof_model_create: NULL topology");
-    if (!topo->d_gsched && topo->nslots > kMaxFkSlots)
-        return fail(RTG_ERR_UNSUPPORTED, "rtg_dof_model_create: topology needs %d branch slots (max %d)", topo->nslots,
-                    kMaxFkSlots);
     const int n = topo->J - 1;
     if (n > 0 && !axis) return fail(RTG_ERR_INVALID_ARGUMENT, "rtg_dof_model_create: NULL axis");
     for (int k = 0; k < n; ++k)

@@ -20,10 +20,8 @@ struct TopoView {
     const int32_t *parents;   // (J)   parents[j] < j, root -1
     const V *local_t;         // (J)   zero-pose local translation
     const Q *tree_quat;       // (J)   SkeletonTree pre-rotation
-    const int32_t *sched;     // (J)   streaming-FK parent schedule, see fk_schedule()
     int32_t J;
-    int32_t nslots;           // branch-parent slots the schedule needs
-    const GEnt *gsched;       // (gsteps * 64 / gF) lane-group schedule, or nullptr (J > kGroupMaxJ)
+    const GEnt *gsched;       // (gsteps * 64 / gF) lane-group schedule, or nullptr (J > kGroupMaxJ: lane walks)
     int32_t gF;               // frames per wave of the lane-group kernels (16: J <= 36, 8: J <= 64)
     int32_t gsteps;           // steps of the lane-group schedule
 };
@@ -32,18 +30,6 @@ inline int group_frames(int J) { return J <= 36 ? 16 : (J <= kGroupMaxJ ? 8 : 0)
 // fills `out` (steps x (64 / F) entries) and returns the step count
 int32_t fk_group_schedule(const int32_t *parents, const V *local_t, const Q *tree_quat, int32_t J, int32_t F,
                           GEnt *out, int32_t max_steps);
-
-// Streaming-FK schedule.  Joints are visited in index order and a lane keeps
-// the previous joint's global transform in registers, so only a parent that
-// is NOT j-1 (a branch point: pelvis, chest, wrists, hands) must be kept
-// elsewhere -- in one of a few LDS "slots".  sched[j] packs
-//   bits 0-7  slot to read joint j's parent from (kNoSlot: parent is j-1 / root)
-//   bits 8-15 slot to save joint j's own transform to (kNoSlot: not a branch parent)
-// Slots are reused once a branch parent's last non-consecutive child is done
-// (interval colouring), so the shipped skeletons need at most 2.
-constexpr int32_t kNoSlot = 0xFF;
-constexpr int32_t kMaxFkSlots = 16;
-int32_t fk_schedule(const int32_t *parents, int32_t J, int32_t *sched);   // returns nslots
 
 // Per-solver constants, passed by value (kernel argument -> SGPRs).
 struct SolverConsts {

@@ -41,15 +41,6 @@
 #define RTG_VEL_LDS_MIN 0   // A/B knob: the velocity tile's LDS request raised to this many bytes (blocks per CU)
 #endif
 // ---- used by rtg_fk.hip
-#ifndef RTG_FK_GROUP
-#define RTG_FK_GROUP 1   // FK / inverse FK / DOF FK / the mixed launch on the lane-group kernels (J <= 64; round 6)
-#endif
-#ifndef RTG_EXP_FK_COPY
-#define RTG_EXP_FK_COPY 0   // measurement knob: k_fk_stream copies its windows out without the chain (wrong answers)
-#endif
-#ifndef RTG_EXP_FK_NOPOS
-#define RTG_EXP_FK_NOPOS 0   // measurement knob: k_fk_stream writes no position rows (wrong answers)
-#endif
 // ---- used by rtg_math.cuh
 #ifndef RTG_EXP_MULR_NOBRANCH
 #define RTG_EXP_MULR_NOBRANCH 0   // measurement knob: mulr without its subnormal-quotient branch (wrong answers on rare inputs)

@@ -1079,8 +1079,14 @@ RTG_DEV void la_bdsqr3(float &d1, float &d2, float &d3, float e1, float e2, Svd3
         }
     }
 }
+// Stage marks for the timestamp measurement builds (RTG_EXP_TIMESTAMPS): hook(k) at a stage boundary, a no-op otherwise.
+// cal_joint_quat: 0 A formed, 1 rotation done; la_gesdd3: 10 bidiagonal form (SGEBD2) done, 11 SBDSQR done.
+struct NoHook {
+    RTG_DEV void operator()(int) const {}
+};
 // SGESDD(JOBZ='A') of a 3x3 (column-major a, overwritten): U and VT (column-major) in z
-RTG_DEV void la_gesdd3(float a[9], Svd3 &z)
+template <typename Hook = NoHook>
+RTG_DEV void la_gesdd3(float a[9], Svd3 &z, const Hook &hook = Hook{})
 {
     const float smlnum = 9.09494702e-13f, bignum = 1.0f / smlnum;   // sqrt(slamch('S')) / slamch('P') = 2^-40
     float anrm = 0.0f;
@@ -1127,11 +1133,13 @@ RTG_DEV void la_gesdd3(float a[9], Svd3 &z)
     }
     const float e2 = a[7];
     const float d3 = a[8];   // i = 2: H_2 = I
+    hook(10);
     // SBDSDC('U','I') -> SLASDQ -> SBDSQR with U = VT = I
 #pragma unroll
     for (int i = 0; i < 9; ++i) { z.u[i] = (i % 4 == 0) ? 1.0f : 0.0f; z.vt[i] = z.u[i]; }
     float s1 = d1, s2 = d2, s3 = d3;
     la_bdsqr3(s1, s2, s3, e1, e2, z);
+    hook(11);
     // SORMBR('Q','L','N'): U := H_0 H_1 U (H_1 first), the unit row fused as fma(-tau, w, c)
     if (tq1 != 0.0f) {
 #pragma unroll
@@ -1165,7 +1173,8 @@ RTG_DEV void la_gesdd3(float a[9], Svd3 &z)
 }
 // transform3d.py:40-45: R = U Vt ((p0 + p1) + p2, torch's bmm order); det(R) < 0 -> Vt[-1,:] *= -1; R = U Vt.
 // A and R row-major.  det only decides a sign (|det| = 1 up to rounding), taken in float64.
-RTG_DEV void kabsch_rot(const float A[9], float R[9])
+template <typename Hook = NoHook>
+RTG_DEV void kabsch_rot(const float A[9], float R[9], const Hook &hook = Hook{})
 {
 #if RTG_EXP_STUB_SVD
 #pragma unroll
@@ -1178,7 +1187,7 @@ RTG_DEV void kabsch_rot(const float A[9], float R[9])
 #pragma unroll
         for (int k = 0; k < 3; ++k) a[i + 3 * k] = A[i * 3 + k];
     Svd3 z;
-    la_gesdd3(a, z);
+    la_gesdd3(a, z, hook);
 #pragma unroll
     for (int i = 0; i < 3; ++i)
 #pragma unroll
@@ -1200,10 +1209,7 @@ RTG_DEV void kabsch_rot(const float A[9], float R[9])
 }
 
 // cal_joint_quat (transform3d.py:31-50): A = M^T Z by einsum (sequential in j, no FMA).  `hook(k)` marks the
-// stages (0: A formed, 1: rotation) for the latency-phase measurement knob; a no-op otherwise.
-struct NoHook {
-    RTG_DEV void operator()(int) const {}
-};
+// stages (NoHook above) for the latency-phase measurement knob; a no-op otherwise.
 // `svd_nan` is set when A has a NaN entry: torch.linalg.svd refuses such a matrix (LAPACK sgesdd returns info = -4
 // on a NaN norm and torch raises "linalg.svd: ... contained non-finite values", transform3d.py:40), so the reference
 // frame raises there (an inf entry alone does not raise).
@@ -1231,7 +1237,7 @@ RTG_DEV Q cal_joint_quat(const V (&Z)[N], const V (&M)[N], bool &svd_nan, const 
     svd_nan = nan;
     hook(0);
     float R[9];
-    kabsch_rot(A, R);
+    kabsch_rot(A, R, hook);
     hook(1);
     return qfrom_rotmat(R);
 }

@@ -242,39 +242,6 @@ __global__ __launch_bounds__(256) void k_ingest_vtrdyn(const float *__restrict__
     for (int e = tid; e < nfr; e += 256) valid[f0 + e] = sdata[e] ? 1 : 0;
 }
 
-int32_t fk_schedule(const int32_t *parents, int32_t J, int32_t *sched)
-{
-    // last non-consecutive child of every branch parent
-    int32_t *last = new int32_t[J];
-    int32_t *slot_of = new int32_t[J];
-    for (int j = 0; j < J; ++j) last[j] = slot_of[j] = -1;
-    for (int k = 1; k < J; ++k)
-        if (parents[k] != k - 1) last[parents[k]] = k;
-    uint32_t used = 0;   // bitmask of live slots (the schedule is only used when nslots <= kMaxFkSlots)
-    int32_t nslots = 0, overflow = 0;
-    for (int j = 0; j < J; ++j) {
-        int32_t ld = kNoSlot, sv = kNoSlot;
-        const int p = j > 0 ? parents[j] : -1;
-        if (j > 0 && p != j - 1) {
-            ld = slot_of[p];
-            if (last[p] == j && ld >= 0 && ld < 32) used &= ~(1u << ld);   // free after this read
-        }
-        if (last[j] >= 0) {
-            int s = 0;
-            while (s < 32 && (used >> s) & 1u) ++s;
-            if (s >= 32) { overflow = 1; s = 31; }
-            used |= 1u << s;
-            slot_of[j] = s;
-            sv = s;
-            nslots = s + 1 > nslots ? s + 1 : nslots;
-        }
-        sched[j] = (ld & 0xFF) | ((sv & 0xFF) << 8);
-    }
-    delete[] last;
-    delete[] slot_of;
-    return overflow ? 1 << 30 : nslots;
-}
-
 
 // ----------------------------------------------------------------------------
 // elementwise primitives
@@ -1034,7 +1001,7 @@ int probe_valu_iters() { return kProbeIters; }
 // ----------------------------------------------------------------------------
 // build configuration (rtg.h rtg_build_info): every RTG_* knob as compiled into this library
 // ----------------------------------------------------------------------------
-#if RTG_EXP_STUB_SVD + RTG_EXP_NO_TABLE + RTG_EXP_HOT_INPUTS + RTG_EXP_FK_COPY + RTG_EXP_FK_NOPOS + RTG_EXP_MULR_NOBRANCH + RTG_EXP_NO_RARE + \
+#if RTG_EXP_STUB_SVD + RTG_EXP_NO_TABLE + RTG_EXP_HOT_INPUTS + RTG_EXP_MULR_NOBRANCH + RTG_EXP_NO_RARE + \
     RTG_EXP_TIMESTAMPS + RTG_EXP_SKIP_SIGNAL == 0
 #define RTG_WRONG_ANSWER_KNOBS 0
 #else
@@ -1047,7 +1014,7 @@ extern "C" const char *rtg_build_info(void)
 {
     return "{\"abi\":" RTG_STR(RTG_ABI_VERSION) ",\"arch\":\"gfx950\",\"knobs\":{"
         RTG_KNOB(RTG_SIDES_WAVES) RTG_KNOB(RTG_SIDES_TILES) RTG_KNOB(RTG_SIDES_SPLIT_READOUT) RTG_KNOB(RTG_QUAD8_MAX_B) RTG_KNOB(RTG_QUAD_MAX_B) RTG_KNOB(RTG_LATENCY_MAX_B)
-        RTG_KNOB(RTG_EXP_TIMESTAMPS) RTG_KNOB(RTG_EXP_SKIP_SIGNAL) RTG_KNOB(RTG_EXP_STUB_SVD) RTG_KNOB(RTG_EXP_NO_TABLE) RTG_KNOB(RTG_FK_GROUP) RTG_KNOB(RTG_EXP_FK_COPY) RTG_KNOB(RTG_EXP_FK_NOPOS) RTG_KNOB(RTG_EXP_MULR_NOBRANCH) RTG_KNOB(RTG_EXP_LARTG_RCP64) RTG_KNOB(RTG_EXP_SQRT64) RTG_KNOB(RTG_EXP_SQRT_CALL) RTG_KNOB(RTG_EXP_ACOS_LIBM) RTG_KNOB(RTG_EXP_EULER_SCIPY) RTG_KNOB(RTG_VEL_SEG) RTG_KNOB(RTG_VEL_LDS_MIN) RTG_KNOB(RTG_VEL_IEEE_DIV) RTG_KNOB(RTG_DOF_NT_STORE) RTG_KNOB(RTG_IN_NT_LOAD) RTG_KNOB(RTG_VEL_W) RTG_KNOB(RTG_VEL_ANG_NB) RTG_KNOB(RTG_EXP_NO_RARE)
+        RTG_KNOB(RTG_EXP_TIMESTAMPS) RTG_KNOB(RTG_EXP_SKIP_SIGNAL) RTG_KNOB(RTG_EXP_STUB_SVD) RTG_KNOB(RTG_EXP_NO_TABLE) RTG_KNOB(RTG_EXP_MULR_NOBRANCH) RTG_KNOB(RTG_EXP_LARTG_RCP64) RTG_KNOB(RTG_EXP_SQRT64) RTG_KNOB(RTG_EXP_SQRT_CALL) RTG_KNOB(RTG_EXP_ACOS_LIBM) RTG_KNOB(RTG_EXP_EULER_SCIPY) RTG_KNOB(RTG_VEL_SEG) RTG_KNOB(RTG_VEL_LDS_MIN) RTG_KNOB(RTG_VEL_IEEE_DIV) RTG_KNOB(RTG_DOF_NT_STORE) RTG_KNOB(RTG_IN_NT_LOAD) RTG_KNOB(RTG_VEL_W) RTG_KNOB(RTG_VEL_ANG_NB) RTG_KNOB(RTG_EXP_NO_RARE)
         "\"RTG_EXP_HOT_INPUTS\":\"" RTG_STR(RTG_EXP_HOT_INPUTS) "\"},\"wrong_answer_knobs\":"
         RTG_STR(RTG_WRONG_ANSWER_KNOBS) "}";
 }

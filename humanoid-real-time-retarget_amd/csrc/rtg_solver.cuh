@@ -469,8 +469,8 @@ __global__ __launch_bounds__(kSideThreads, RTG_SIDES_WAVES) void k_solve_sides(S
         if (threadIdx.x < 4 * kSideTiles) (&sflag[0][0])[threadIdx.x] = 0;
         __syncthreads();
         int *const fl = sflag[w >> 1];
-        auto hook1 = [&](int k) { TS(1 + k); };    // 1: first fit's A formed (its points loaded), 2: its SVD + R done
-        auto hook2 = [&](int k) { TS(10 + k); };   // 10 / 11: the same for the left wave's second fit
+        auto hook1 = [&](int k) { if (k < 2) TS(1 + k); };    // 1: first fit's A formed (its points loaded), 2: its SVD + R done
+        auto hook2 = [&](int k) { if (k < 2) TS(10 + k); };   // 10 / 11: the same for the left wave's second fit
         TS(0);
         const auto b = view(in0, 63);
         Q R10 = qident(), W = qident();
@@ -673,7 +673,7 @@ RTG_DEV void fbp_latency5_tile(const SolverConsts &C, const float *__restrict__ 
 #else
     auto TS = [](int) {};
 #endif
-    auto hook = [&](int k) { TS(8 + k); };
+    auto hook = [&](int k) { if (k < 2) TS(8 + k); };
     TS(0);
     float *const lrow = live && local_rot ? local_rot + f * 124 : nullptr;
     const Emit E{sdof + lane * kDofStride, lrow, C.ang_tab, sst + lane, kLatFrames};
@@ -941,6 +941,26 @@ RTG_DEV uint32_t fbp_frame1_tile(const SolverConsts &C, const float *rows, float
     __shared__ uint32_t sstat[3];  // status bits of the torso wave and the two wrist waves
     const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const bool w0 = lane == 0;
+#if RTG_EXP_TIMESTAMPS
+    // measurement knob: lane 0 of each wave records the 100 MHz wall clock at its stage boundaries into body_rot
+    // (16 u32 pairs per wave; tools/latency_phases.py frame1): 0 start; fits (waves 0-2): 1 A formed, 2 SGEBD2 done,
+    // 3 SBDSQR done, 4 rotation done; wave 0: 5 R10 signalled; waves 1 / 2: 5 gripper done, 6 arm chain received,
+    // 7 Euler split done, 8 read-out done; waves 3 / 4: 1 points loaded, 6 R10 received, 7 arm chain done, 8 read-out
+    // done; every wave: 14 at the final barrier, 15 past it
+    float *const tsb = body_rot;
+    body_rot = nullptr;
+    auto TS = [&](int k) {
+        if (tsb && lane == 0) {
+            const uint64_t t = wall_clock64();
+            reinterpret_cast<uint32_t *>(tsb)[2 * (16 * w + k)] = (uint32_t)t;
+            reinterpret_cast<uint32_t *>(tsb)[2 * (16 * w + k) + 1] = (uint32_t)(t >> 32);
+        }
+    };
+#else
+    auto TS = [](int) {};
+#endif
+    auto hook = [&](int k) { TS(k == 0 ? 1 : (k == 10 ? 2 : (k == 11 ? 3 : 4))); };
+    TS(0);
     if (threadIdx.x < 3) sflag[threadIdx.x] = 0;
     __syncthreads();
     const Emit E{sdof, local_rot, C.ang_tab, sst, 1};
@@ -949,16 +969,19 @@ RTG_DEV uint32_t fbp_frame1_tile(const SolverConsts &C, const float *rows, float
     if (w == 0) {
         if (w0) {
             bool nan = false;
-            const Q q = fbp_torso(C, b, nan);
+            const Q q = fbp_torso(C, b, nan, hook);
             sfit = make_float4(q.x, q.y, q.z, q.w);
             st = nan ? kStTorsoSvd : 0u;
         }
         lds_signal(&sflag[0]);
+        TS(5);
         if (w0) emit_fixed_links(E, const_rows);
     } else if (w >= 3) {
         const int side = w - 3;
         const ArmPts ap = side ? load_arm<1>(b) : load_arm<0>(b);
+        TS(1);
         lds_wait(&sflag[0], C.err);
+        TS(6);
         const float4 t = sfit;
         const Q R10{t.x, t.y, t.z, t.w};
         const V up = vsub(ap.el, ap.sh), fo = vsub(ap.wr, ap.el);
@@ -966,7 +989,9 @@ RTG_DEV uint32_t fbp_frame1_tile(const SolverConsts &C, const float *rows, float
                           : solve_arm_lanes<12>(E, up, fo, C.lsh, C.lel, R10);
         if (w0) schain[side] = make_float4(ch.x, ch.y, ch.z, ch.w);
         lds_signal(&sflag[1 + side]);
+        TS(7);
         finalize_lanes(E, side ? 7 : 0, 4);
+        TS(8);
     } else {
         const int side = w - 1;
         const FV<false> H{rows + (side ? 123 : 63)};
@@ -974,13 +999,15 @@ RTG_DEV uint32_t fbp_frame1_tile(const SolverConsts &C, const float *rows, float
         float a = 0.0f;
         if (w0) {
             bool nan = false;
-            W = side ? fbp_wrist_fit<1>(C, H, nan) : fbp_wrist_fit<0>(C, H, nan);
+            W = side ? fbp_wrist_fit<1>(C, H, nan, hook) : fbp_wrist_fit<0>(C, H, nan, hook);
             st = nan ? (side ? kStRightSvd : kStLeftSvd) : 0u;
             const TipPts tp = load_tips(H);
             a = hand_x_mean(qconj(W), tp.h0, tp.t);   // the gripper needs only W (:142-158 / :165-175)
         }
         W = gbc<64, 0>(W);
+        TS(5);
         lds_wait(&sflag[1 + side], C.err);   // the arm waited for R10 first: both are visible (release / acquire chain)
+        TS(6);
         const float4 t = sfit, c = schain[side];
         const Q R10{t.x, t.y, t.z, t.w}, chain{c.x, c.y, c.z, c.w};
         if (w0) {
@@ -993,10 +1020,14 @@ RTG_DEV uint32_t fbp_frame1_tile(const SolverConsts &C, const float *rows, float
         const Q loc = qmul_norm(qconj(qmul_norm(R10, chain)), W);
         const bool refused = side ? emit_euler_xyz_lanes<25>(E, loc) : emit_euler_xyz_lanes<16>(E, loc);
         st |= refused ? (side ? kStRightEuler : kStLeftEuler) : 0u;
+        TS(7);
         finalize_lanes(E, side ? 11 : 4, 3);
+        TS(8);
     }
     if (w < 3 && w0) sstat[w] = st;
+    TS(14);
     __syncthreads();
+    TS(15);
     const uint32_t bits = sstat[0] | sstat[1] | sstat[2];   // block-uniform
     if (bits) {   // rare: the reference raises on this frame
         if (threadIdx.x == 0) poison_frame(sdof, local_rot, body_rot, bits);

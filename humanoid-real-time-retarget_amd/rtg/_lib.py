@@ -163,7 +163,7 @@ def lib() -> ctypes.CDLL:
     return _lib
 
 
-WRONG_ANSWER_KNOBS = ("RTG_EXP_STUB_SVD", "RTG_EXP_NO_TABLE", "RTG_EXP_HOT_INPUTS", "RTG_EXP_FK_COPY", "RTG_EXP_FK_NOPOS",
+WRONG_ANSWER_KNOBS = ("RTG_EXP_STUB_SVD", "RTG_EXP_NO_TABLE", "RTG_EXP_HOT_INPUTS",
                       "RTG_EXP_MULR_NOBRANCH", "RTG_EXP_TIMESTAMPS", "RTG_EXP_SKIP_SIGNAL", "RTG_EXP_NO_RARE")
 
 

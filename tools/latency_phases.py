@@ -4,6 +4,8 @@
                the five-wave latency kernel (k_fbp_latency5; B = 1 runs k_fbp_frame1, which records no stages, so use B >= 2) records the
                100 MHz wall clock at its stage boundaries; prints the median stage times (us) per wave at B=1 and
                B=4096
+  frame1    -- needs the RTG_EXP_TIMESTAMPS build too: the B = 1 kernel k_fbp_frame1's critical path, per wave the
+               median end time of each stage (fits split into SGEBD2 / SBDSQR / the rotation and quaternion)
   zerocopy  -- the B=1 call with the inputs and outputs in pinned host memory that the kernel reads / writes
                directly (no copy nodes), as a direct launch and as a one-node graph, next to the FrameGraph path
 """
@@ -98,6 +100,53 @@ def phases():
                 d["end"] = float(r[w, 7])
             res[f"wave{w}"] = d
         out[str(B)] = {"kernel_waves": nw, **res}
+    return out
+
+
+F1 = {0: {1: "A_formed", 2: "gebrd", 3: "bdsqr", 4: "rotation_quat", 5: "R10_signalled"},
+      1: {1: "A_formed", 2: "gebrd", 3: "bdsqr", 4: "rotation_quat", 5: "gripper", 6: "chain_received",
+          7: "euler", 8: "readout"},
+      3: {1: "points_loaded", 6: "R10_received", 7: "arm_chain", 8: "readout"}}
+F1[2] = F1[1]
+F1[4] = F1[3]
+
+
+def frame1(reps=200):
+    """The B = 1 kernel's critical path (k_fbp_frame1; RTG_EXP_TIMESTAMPS build): per wave, the median time (us from
+    the block's first timestamp) at which each stage ENDS, over `reps` launches on one frame; the golden frames
+    cycle so every stage sees varied inputs (the SVD's sweep count varies per frame)."""
+    S = solver()
+    g = np.load(os.path.join(G, "full_body_pos_precise.npz"))
+    dof = torch.empty((1, 30), device="cuda")
+    ts = torch.zeros((236,), device="cuda")
+    rows = []
+    for rep in range(reps + 10):
+        i = rep % len(g["body"])
+        ins = [torch.from_numpy(np.ascontiguousarray(g[k][i:i + 1])).cuda() for k in ("body", "lh", "rh")]
+        ts.zero_()
+        check(lib().rtg_retarget_f32(S.handle, ptr(ins[0]), ptr(ins[1]), ptr(ins[2]), None, 1, 0, ptr(dof), None,
+                                     ptr(ts), stream_handle()))
+        torch.cuda.synchronize()
+        t = ts[:160].cpu().numpy().view(np.uint32).astype(np.uint64)
+        t = (t[0::2] | (t[1::2] << np.uint64(32))).reshape(5, 16).astype(np.int64)
+        if rep >= 10:
+            rows.append(t)
+    T = np.stack(rows).astype(np.float64)
+    T = np.where(T == 0, np.nan, T)
+    T = (T - np.nanmin(T[:, :, 0], axis=1)[:, None, None]) * 0.01
+    med = np.nanmedian(T, axis=0)
+    p90 = np.nanpercentile(T, 90, axis=0)
+    out = {}
+    for w in range(5):
+        d = {"start": float(med[w, 0])}
+        for k, name in F1[w].items():
+            d[name] = float(med[w, k])
+            d[name + "_p90"] = float(p90[w, k])
+        d["barrier_in"] = float(med[w, 14])
+        d["barrier_out"] = float(med[w, 15])
+        out[f"wave{w}"] = d
+    # the critical path: the later of the two Euler / read-out ends
+    out["critical_path_end_us"] = float(np.nanmedian(np.nanmax(T[:, :, 15], axis=1)))
     return out
 
 
