@@ -372,11 +372,15 @@ __global__ __launch_bounds__(64, 4) void k_lrot_group(TopoView T, const float *_
     lrot_group_tile<STATE, F>(T, g_rot, B, (int64_t)blockIdx.x * F, local_rot, fk_lds);
 }
 
-// HuForwardModel (hu_forward_model.py:17-33) on the lane groups: LDS = the tile image (root rotation at joint 0) |
-// the tile's DOF rows (F (J - 1) floats) | per-joint {axis, lower, upper}
-static inline size_t dof_group_lds_floats(int J, int F, int steps)
+// HuForwardModel (hu_forward_model.py:17-33) on the lane groups.  The local rotations do not depend on the chain, so
+// they are built first, all at once: each lane turns the DOFs it loaded (the tile's rows are nfr (J - 1) consecutive
+// floats, NR loads per lane) into joint rotations -- quat_from_angle_axis of the clipped angle about the joint's unit
+// axis -- and writes them into the tile image where FK's local rotations would be; then FK's compose runs as is.  (A
+// first version built each joint's rotation inside its compose step: the f64 sincos sat on the chain's critical path
+// and the kernel took 128 us against FK's 88, profiles/r06/fk/.)  LDS = the tile image | per-joint {axis, lower, upper}
+__host__ __device__ inline size_t dof_group_lds_floats(int J, int F, int steps)
 {
-    return group_lds_floats(J, F, steps) + pad16f((size_t)F * (J - 1)) + (size_t)J * 4;
+    return group_lds_floats(J, F, steps) + (size_t)J * 4;
 }
 template <bool CLIP, int F>
 __global__ __launch_bounds__(64, 4) void k_dof_fk_group(TopoView T, DofView D, const float *__restrict__ dof,
@@ -393,9 +397,7 @@ __global__ __launch_bounds__(64, 4) void k_dof_fk_group(TopoView T, DofView D, c
     f4v *rot = reinterpret_cast<f4v *>(fk_lds);
     float *pos = fk_lds + 4 * F * J;
     GEnt *sch = reinterpret_cast<GEnt *>(pos + pad16f((size_t)3 * F * J));
-    float *ang = fk_lds + group_lds_floats(J, F, T.gsteps);
-    f4v *ntab = reinterpret_cast<f4v *>(ang + pad16f((size_t)F * nd));
-    // the tile's DOF rows are nfr * nd consecutive floats: NR dword loads per lane, all in flight
+    f4v *ntab = reinterpret_cast<f4v *>(fk_lds + group_lds_floats(J, F, T.gsteps));
     const float *drow = dof + f0 * nd;
     const int nang = nfr * nd;
     float a[G::NR];   // unconditional loads (a lane past the rows re-reads element 0)
@@ -412,29 +414,35 @@ __global__ __launch_bounds__(64, 4) void k_dof_fk_group(TopoView T, DofView D, c
         ntab[j] = f4v{__int_as_float(ax), CLIP ? ld_const(D.lower + (j - 1)) : 0.0f,
                       CLIP ? ld_const(D.upper + (j - 1)) : 0.0f, 0.0f};
     }
-#pragma unroll
-    for (int k = 0; k < G::NR; ++k) {
-        const int i = k * 64 + lane;
-        if (i < nang) ang[i] = a[k];
-    }
     if (lane < nfr) rot[lane * J] = rr;   // root: global = the root rotation (hu_forward_model.py:24)
     if (lane < 3 * nfr) {
         const int fr = lane / 3;
         pos[3 * J * fr + (lane - 3 * fr)] = rt;
     }
     wave_sync();
-    group_compose<F>(T, rot, pos, sch, nfr, [&](int j, Q, const GEnt &, int fr) {
-        const f4v t = ntab[j];
-        float x = ang[fr * nd + (j - 1)];
-        if (CLIP) {   // torch.clamp (min then max; NaN passes), then the straight-through sum
-            float c = x < t.y ? t.y : x;
-            c = c > t.z ? t.z : c;
-            x = (c - x) + x;
+    // angle i = (frame fr, joint i mod nd + 1): its rotation into record fr J + j (i / nd as ((i + 1/2) / nd)
+    // truncated: exact for i < 2^12)
+    const float rnd = 1.0f / (float)(nd > 0 ? nd : 1);
+#pragma unroll
+    for (int k = 0; k < G::NR; ++k) {
+        const int i = k * 64 + lane;
+        if (i < nang) {
+            const int fr = (int)(((float)i + 0.5f) * rnd), j = i - fr * nd + 1;
+            const f4v t = ntab[j];
+            float x = a[k];
+            if (CLIP) {   // torch.clamp (min then max; NaN passes), then the straight-through sum
+                float c = x < t.y ? t.y : x;
+                c = c > t.z ? t.z : c;
+                x = (c - x) + x;
+            }
+            const int ax = __float_as_int(t.x);
+            // the axis is an exact unit vector: quat_from_angle_axis's normalisation is the identity (round 5)
+            const Q q = qfrom_angle_unit_axis(x, V{ax == 0 ? 1.0f : 0.0f, ax == 1 ? 1.0f : 0.0f, ax == 2 ? 1.0f : 0.0f});
+            rot[fr * J + j] = f4v{q.x, q.y, q.z, q.w};
         }
-        const int ax = __float_as_int(t.x);
-        // the axis is an exact unit vector: quat_from_angle_axis's normalisation is the identity (round 5)
-        return qfrom_angle_unit_axis(x, V{ax == 0 ? 1.0f : 0.0f, ax == 1 ? 1.0f : 0.0f, ax == 2 ? 1.0f : 0.0f});
-    });
+    }
+    wave_sync();
+    group_compose<F>(T, rot, pos, sch, nfr, [&](int, Q lq, const GEnt &, int) { return lq; });
     group_store<F>(rot, pos, nrec, g_rot + f0 * J * 4, g_pos + f0 * J * 3);
 }
 

@@ -26,7 +26,7 @@ struct TopoView {
     int32_t gsteps;           // steps of the lane-group schedule
 };
 // the lane-group frames per wave for J joints (0: J too large, the lane-walk kernels run); F J <= 64 * 9 records
-inline int group_frames(int J) { return J <= 36 ? 16 : (J <= kGroupMaxJ ? 8 : 0); }
+inline int group_frames(int J) { return J <= RTG_FK_F16_MAXJ ? 16 : (J <= kGroupMaxJ ? 8 : 0); }
 // fills `out` (steps x (64 / F) entries) and returns the step count
 int32_t fk_group_schedule(const int32_t *parents, const V *local_t, const Q *tree_quat, int32_t J, int32_t F,
                           GEnt *out, int32_t max_steps);

@@ -41,6 +41,9 @@
 #define RTG_VEL_LDS_MIN 0   // A/B knob: the velocity tile's LDS request raised to this many bytes (blocks per CU)
 #endif
 // ---- used by rtg_fk.hip
+#ifndef RTG_FK_F16_MAXJ
+#define RTG_FK_F16_MAXJ 36   // lane-group kinematics: 16 frames per wave (4 lanes each) up to this J, else 8 (8 lanes)
+#endif
 // ---- used by rtg_math.cuh
 #ifndef RTG_EXP_MULR_NOBRANCH
 #define RTG_EXP_MULR_NOBRANCH 0   // measurement knob: mulr without its subnormal-quotient branch (wrong answers on rare inputs)
