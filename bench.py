@@ -223,7 +223,7 @@ def cpu_baseline(body, lh, rh, zl, zg, seconds):
     return out
 
 
-PMC_JSON = os.path.join(REPO, "profiles", "pmc_r05.json")
+PMC_JSON = os.path.join(REPO, "profiles", "pmc_r06.json")
 PMC_KERNELS = {"soa": "rtg::k_solve_sides<0, true, true>", "aos": "rtg::k_solve_sides<0, true, false>"}
 VALU_PEAK_LANE_OPS = 256 * 4 * 32 * 2.4e9   # MI355X: CUs x SIMDs x lanes issued per cycle x 2.4 GHz (78.6 T/s)
 

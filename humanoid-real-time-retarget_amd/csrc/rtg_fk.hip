@@ -309,6 +309,7 @@ __global__ __launch_bounds__(64, 4) void k_fk_group(TopoView T, const float *__r
 }
 
 // inverse FK: LDS = the tile image | parents (J ints) | STATE: normalised conjugate tree quaternions (J float4)
+constexpr int kLrotFrames = 8;   // frames per wave of the inverse tiles (any J <= kGroupMaxJ)
 static inline size_t lrot_group_lds_floats(int J, int F) { return (size_t)F * J * 4 + pad16f((size_t)J) + (size_t)J * 4; }
 template <bool STATE, int F>
 RTG_DEV void lrot_group_tile(const TopoView &T, const float *__restrict__ g_rot, int64_t B, int64_t f0,
@@ -457,13 +458,9 @@ __global__ __launch_bounds__(64, 4) void k_fk_multi_group(FkMultiArgs A)
         if (i < A.n && (int64_t)blockIdx.x >= A.block_start[i]) s = i;
     const FkSeg &S = A.seg[s];
     const int64_t t = (int64_t)blockIdx.x - A.block_start[s];
-    if (S.T.gF == 16) {
-        if (S.op == 0) fk_group_tile<false, 16>(S.T, S.local_rot, S.root_t, S.B, t * 16, S.g_rot, S.g_pos, fk_lds);
-        else lrot_group_tile<false, 16>(S.T, S.local_rot, S.B, t * 16, S.g_rot, fk_lds);
-    } else {
-        if (S.op == 0) fk_group_tile<false, 8>(S.T, S.local_rot, S.root_t, S.B, t * 8, S.g_rot, S.g_pos, fk_lds);
-        else lrot_group_tile<false, 8>(S.T, S.local_rot, S.B, t * 8, S.g_rot, fk_lds);
-    }
+    if (S.op == 1) lrot_group_tile<false, kLrotFrames>(S.T, S.local_rot, S.B, t * kLrotFrames, S.g_rot, fk_lds);
+    else if (S.T.gF == 16) fk_group_tile<false, 16>(S.T, S.local_rot, S.root_t, S.B, t * 16, S.g_rot, S.g_pos, fk_lds);
+    else fk_group_tile<false, 8>(S.T, S.local_rot, S.root_t, S.B, t * 8, S.g_rot, S.g_pos, fk_lds);
 }
 
 // Host: the lane-group list schedule.  Joints become ready once their parent's step is past; each step takes up to L
@@ -524,17 +521,12 @@ hipError_t launch_fk(const TopoView &T, bool state, const float *lr, const float
 
 hipError_t launch_local_rotation(const TopoView &T, bool state, const float *g, int64_t B, float *l, hipStream_t s)
 {
-    if (T.gsched) {
-        const int F = T.gF;
-        const size_t lds = sizeof(float) * lrot_group_lds_floats(T.J, F);
-        const dim3 gd(grid_for(B, F)), b(64);
-        if (F == 16) {
-            if (state) hipLaunchKernelGGL((k_lrot_group<true, 16>), gd, b, lds, s, T, g, B, l);
-            else hipLaunchKernelGGL((k_lrot_group<false, 16>), gd, b, lds, s, T, g, B, l);
-        } else {
-            if (state) hipLaunchKernelGGL((k_lrot_group<true, 8>), gd, b, lds, s, T, g, B, l);
-            else hipLaunchKernelGGL((k_lrot_group<false, 8>), gd, b, lds, s, T, g, B, l);
-        }
+    if (T.gsched) {   // 8 frames per wave whatever J: no chain here, so the smallest tile -- the most waves per CU --
+                      // wins (Hu: 41.4 vs 46.8 us at 16 frames, profiles/r06/fk/)
+        const size_t lds = sizeof(float) * lrot_group_lds_floats(T.J, kLrotFrames);
+        const dim3 gd(grid_for(B, kLrotFrames)), b(64);
+        if (state) hipLaunchKernelGGL((k_lrot_group<true, kLrotFrames>), gd, b, lds, s, T, g, B, l);
+        else hipLaunchKernelGGL((k_lrot_group<false, kLrotFrames>), gd, b, lds, s, T, g, B, l);
     } else if (state) {   // J > kGroupMaxJ: lane walk
         hipLaunchKernelGGL(k_local_rotation<true>, dim3(grid_for(B, 256)), dim3(256), 0, s, T, g, B, l);
     } else {
@@ -553,9 +545,10 @@ hipError_t launch_fk_multi(FkMultiArgs &A, hipStream_t s)
     for (int i = 0; i < A.n; ++i) {
         const TopoView &T = A.seg[i].T;
         A.block_start[i] = blocks;
-        blocks += grid_for(A.seg[i].B, group ? T.gF : 256);
+        blocks += grid_for(A.seg[i].B, group ? (A.seg[i].op == 0 ? T.gF : kLrotFrames) : 256);
         if (group) {
-            const size_t need = A.seg[i].op == 0 ? group_lds_floats(T.J, T.gF, T.gsteps) : lrot_group_lds_floats(T.J, T.gF);
+            const size_t need =
+                A.seg[i].op == 0 ? group_lds_floats(T.J, T.gF, T.gsteps) : lrot_group_lds_floats(T.J, kLrotFrames);
             lds = need > lds ? need : lds;
         }
     }
