@@ -135,6 +135,13 @@ RTG_DEV void wave_sync()
 }
 
 typedef float f4v __attribute__((ext_vector_type(4)));
+// the lane-group tiles' output pieces (whole 1 KiB wave stores): non-temporal (RTG_FK_NT_OUT): never read back here,
+// they would only evict the rows still to be read from the L2
+RTG_DEV void st_out(f4v *p, f4v v)
+{
+    if (RTG_FK_NT_OUT) __builtin_nontemporal_store(v, p);
+    else *p = v;
+}
 
 // ----------------------------------------------------------------------------
 // Lane-group kinematics (round 6): a frame's joints spread over a GROUP of lanes, F frames per wave (F = 16: four
@@ -234,14 +241,14 @@ RTG_DEV void group_store(const f4v *rot, const float *pos, int nrec, float *__re
 #pragma unroll
     for (int k = 0; k < G::NR; ++k) {
         const int rec = k * 64 + lane;
-        if (rec < nrec) dst[rec] = o[k];
+        if (rec < nrec) st_out(dst + rec, o[k]);
     }
     const int npos = 3 * nrec;
     if ((reinterpret_cast<uintptr_t>(g_pos) & 15u) == 0) {
         const int n4 = npos >> 2;
         f4v *pd = reinterpret_cast<f4v *>(g_pos);
         const f4v *ps = reinterpret_cast<const f4v *>(pos);
-        for (int i = lane; i < n4; i += 64) pd[i] = ps[i];
+        for (int i = lane; i < n4; i += 64) st_out(pd + i, ps[i]);
         for (int i = 4 * n4 + lane; i < npos; i += 64) g_pos[i] = pos[i];
     } else {
         for (int i = lane; i < npos; i += 64) g_pos[i] = pos[i];
@@ -360,7 +367,7 @@ RTG_DEV void lrot_group_tile(const TopoView &T, const float *__restrict__ g_rot,
                     q = qmul_norm(Q{c.x, c.y, c.z, c.w}, q);
                 }
             }
-            dst[rec] = f4v{q.x, q.y, q.z, q.w};
+            st_out(dst + rec, f4v{q.x, q.y, q.z, q.w});
         }
     }
 }

@@ -41,6 +41,10 @@
 #define RTG_VEL_LDS_MIN 0   // A/B knob: the velocity tile's LDS request raised to this many bytes (blocks per CU)
 #endif
 // ---- used by rtg_fk.hip
+#ifndef RTG_FK_NT_OUT
+#define RTG_FK_NT_OUT 1   // the lane-group kinematics' output rows stored non-temporal (whole 1 KiB wave stores;
+                          // Hu FK 88 -> 80 us, mixed 112 -> 101 us, profiles/r06/fk/nt/)
+#endif
 #ifndef RTG_FK_F16_MAXJ
 #define RTG_FK_F16_MAXJ 36   // lane-group kinematics: 16 frames per wave (4 lanes each) up to this J, else 8 (8 lanes)
 #endif

@@ -674,6 +674,7 @@ static uint32_t vel_tile_frames(int64_t C, int R)
 {
     // measured at 64 x 4096 x 31 (profiles/r04/aux/vel_tiles.log): 64 / 32 / 16 frames linear 79 / 90 / 108 us,
     // angular 125 / 140 / 169 us (the halo's share grows faster than the extra blocks per CU help)
+    // (128-frame tiles in 64 KB: linear 72 vs 56 us, angular 117 vs 113 us, profiles/r06/aux/vel128_*)
     for (uint32_t T = 64; T >= 16; T /= 2)
         if ((int64_t)vel_lds_stride(T, R) * C * 4 <= 48 * 1024) return T;
     return 0;
@@ -1014,7 +1015,7 @@ extern "C" const char *rtg_build_info(void)
 {
     return "{\"abi\":" RTG_STR(RTG_ABI_VERSION) ",\"arch\":\"gfx950\",\"knobs\":{"
         RTG_KNOB(RTG_SIDES_WAVES) RTG_KNOB(RTG_SIDES_TILES) RTG_KNOB(RTG_SIDES_SPLIT_READOUT) RTG_KNOB(RTG_QUAD8_MAX_B) RTG_KNOB(RTG_QUAD_MAX_B) RTG_KNOB(RTG_LATENCY_MAX_B)
-        RTG_KNOB(RTG_EXP_TIMESTAMPS) RTG_KNOB(RTG_EXP_SKIP_SIGNAL) RTG_KNOB(RTG_EXP_STUB_SVD) RTG_KNOB(RTG_EXP_NO_TABLE) RTG_KNOB(RTG_EXP_MULR_NOBRANCH) RTG_KNOB(RTG_FK_F16_MAXJ) RTG_KNOB(RTG_EXP_LARTG_RCP64) RTG_KNOB(RTG_EXP_SQRT64) RTG_KNOB(RTG_EXP_SQRT_CALL) RTG_KNOB(RTG_EXP_ACOS_LIBM) RTG_KNOB(RTG_EXP_EULER_SCIPY) RTG_KNOB(RTG_VEL_SEG) RTG_KNOB(RTG_VEL_LDS_MIN) RTG_KNOB(RTG_VEL_IEEE_DIV) RTG_KNOB(RTG_DOF_NT_STORE) RTG_KNOB(RTG_IN_NT_LOAD) RTG_KNOB(RTG_VEL_W) RTG_KNOB(RTG_VEL_ANG_NB) RTG_KNOB(RTG_EXP_NO_RARE)
+        RTG_KNOB(RTG_EXP_TIMESTAMPS) RTG_KNOB(RTG_EXP_SKIP_SIGNAL) RTG_KNOB(RTG_EXP_STUB_SVD) RTG_KNOB(RTG_EXP_NO_TABLE) RTG_KNOB(RTG_EXP_MULR_NOBRANCH) RTG_KNOB(RTG_FK_F16_MAXJ) RTG_KNOB(RTG_FK_NT_OUT) RTG_KNOB(RTG_EXP_LARTG_RCP64) RTG_KNOB(RTG_EXP_SQRT64) RTG_KNOB(RTG_EXP_SQRT_CALL) RTG_KNOB(RTG_EXP_ACOS_LIBM) RTG_KNOB(RTG_EXP_EULER_SCIPY) RTG_KNOB(RTG_VEL_SEG) RTG_KNOB(RTG_VEL_LDS_MIN) RTG_KNOB(RTG_VEL_IEEE_DIV) RTG_KNOB(RTG_DOF_NT_STORE) RTG_KNOB(RTG_IN_NT_LOAD) RTG_KNOB(RTG_VEL_W) RTG_KNOB(RTG_VEL_ANG_NB) RTG_KNOB(RTG_EXP_NO_RARE)
         "\"RTG_EXP_HOT_INPUTS\":\"" RTG_STR(RTG_EXP_HOT_INPUTS) "\"},\"wrong_answer_knobs\":"
         RTG_STR(RTG_WRONG_ANSWER_KNOBS) "}";
 }
