@@ -813,8 +813,8 @@ template <int G>
 RTG_DEV int sublane() { return (int)(threadIdx.x & (G - 1)); }
 
 // shoulder_pr (SHOULDER) / elbow_py of the frame: sub-lane 0 the first angle's quaternion, sub-lane 1 the second's
-template <bool SHOULDER, int G = 64>
-RTG_DEV void arm_pair_lanes(V v1, ArmZero z0, Q parent, Q &first, Q &second)
+template <bool SHOULDER, int G = 64, typename Hook = NoHook>
+RTG_DEV void arm_pair_lanes(V v1, ArmZero z0, Q parent, Q &first, Q &second, const Hook &hook = Hook{})
 {
     const int sub = sublane<G>();
     Q q = qident();
@@ -822,15 +822,19 @@ RTG_DEV void arm_pair_lanes(V v1, ArmZero z0, Q parent, Q &first, Q &second)
         const V ex{1.f, 0.f, 0.f}, ey{0.f, 1.f, 0.f}, ez{0.f, 0.f, 1.f};
         const V pn = SHOULDER ? ey : ez;   // the plane of the first angle
         const V v1r = qrotate(qconj(parent), v1);
+        hook(0);
         const V v1p = proj_in_plane(v1r, pn);
+        hook(1);
         const bool l0 = sub == 0;
         const V a{l0 ? 1.f : v1p.x, l0 ? 0.f : v1p.y, l0 ? 0.f : v1p.z};
         const V b = l0 ? v1p : v1r;
         const V c = SHOULDER ? cross3(v1p, ey) : cross3(ez, v1p);
         const V n = l0 ? pn : c;
         const float ang = radians_between(a, b, n);
+        hook(2);
         const V ax = l0 ? pn : (SHOULDER ? ex : ey);
         q = qfrom_angle_unit_axis(ang - (l0 ? z0.th0 : z0.ph0), ax);
+        hook(3);
     }
     first = gbc<G, 0>(q);
     second = gbc<G, 1>(q);
@@ -842,14 +846,14 @@ RTG_DEV void link_rt(const Emit &E, int link, Q q)
     E.st[(link <= 18 ? link - 12 : link - 14) * E.sst] = make_float2(q.w, k == 0 ? q.x : (k == 1 ? q.y : q.z));
     if (E.lr) st4(E.lr + 4 * link, q);
 }
-template <int L0, int G = 64>
-RTG_DEV Q solve_arm_lanes(const Emit &E, V upper, V fore, ArmZero zs, ArmZero ze, Q parent)
+template <int L0, int G = 64, typename Hook = NoHook>
+RTG_DEV Q solve_arm_lanes(const Emit &E, V upper, V fore, ArmZero zs, ArmZero ze, Q parent, const Hook &hook = Hook{})
 {
     const bool w0 = sublane<G>() == 0;
     Q p, r, y, e;
-    arm_pair_lanes<true, G>(upper, zs, parent, p, r);
+    arm_pair_lanes<true, G>(upper, zs, parent, p, r, [&](int k) { hook(k); });
     if (w0) { E.link<L0>(p); E.link<L0 + 1>(r); }
-    arm_pair_lanes<false, G>(fore, ze, qmul(qmul(parent, p), r), y, e);
+    arm_pair_lanes<false, G>(fore, ze, qmul(qmul(parent, p), r), y, e, [&](int k) { hook(4 + k); });
     if (w0) { E.link<L0 + 2>(y); E.link<L0 + 3>(e); }
     return qmul(qmul(qmul(p, r), y), e);
 }
@@ -945,8 +949,9 @@ RTG_DEV uint32_t fbp_frame1_tile(const SolverConsts &C, const float *rows, float
     // measurement knob: lane 0 of each wave records the 100 MHz wall clock at its stage boundaries into body_rot
     // (16 u32 pairs per wave; tools/latency_phases.py frame1): 0 start; fits (waves 0-2): 1 A formed, 2 SGEBD2 done,
     // 3 SBDSQR done, 4 rotation done; wave 0: 5 R10 signalled; waves 1 / 2: 5 gripper done, 6 arm chain received,
-    // 7 Euler split done, 8 read-out done; waves 3 / 4: 1 points loaded, 6 R10 received, 7 arm chain done, 8 read-out
-    // done; every wave: 14 at the final barrier, 15 past it
+    // 7 Euler split done, 8 read-out done; waves 3 / 4: 1 points loaded, 6 R10 received, 8-11 the shoulder pair (parent
+    // rotated, projected, angle, quaternion), 12 the elbow pair's quaternion, 7 arm chain done, 13 read-out done; every
+    // wave: 14 at the final barrier, 15 past it
     float *const tsb = body_rot;
     body_rot = nullptr;
     auto TS = [&](int k) {
@@ -985,13 +990,17 @@ RTG_DEV uint32_t fbp_frame1_tile(const SolverConsts &C, const float *rows, float
         const float4 t = sfit;
         const Q R10{t.x, t.y, t.z, t.w};
         const V up = vsub(ap.el, ap.sh), fo = vsub(ap.wr, ap.el);
-        const Q ch = side ? solve_arm_lanes<21>(E, up, fo, C.rsh, C.rel, R10)
-                          : solve_arm_lanes<12>(E, up, fo, C.lsh, C.lel, R10);
+        auto ahook = [&](int k) {   // arm stages: 8 + (0 rotated, 1 projected, 2 angle, 3 quaternion); 12 the elbow's quaternion
+            if (k < 4) TS(8 + k);
+            else if (k == 7) TS(12);
+        };
+        const Q ch = side ? solve_arm_lanes<21>(E, up, fo, C.rsh, C.rel, R10, ahook)
+                          : solve_arm_lanes<12>(E, up, fo, C.lsh, C.lel, R10, ahook);
         if (w0) schain[side] = make_float4(ch.x, ch.y, ch.z, ch.w);
         lds_signal(&sflag[1 + side]);
         TS(7);
         finalize_lanes(E, side ? 7 : 0, 4);
-        TS(8);
+        TS(13);
     } else {
         const int side = w - 1;
         const FV<false> H{rows + (side ? 123 : 63)};

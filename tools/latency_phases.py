@@ -106,7 +106,8 @@ def phases():
 F1 = {0: {1: "A_formed", 2: "gebrd", 3: "bdsqr", 4: "rotation_quat", 5: "R10_signalled"},
       1: {1: "A_formed", 2: "gebrd", 3: "bdsqr", 4: "rotation_quat", 5: "gripper", 6: "chain_received",
           7: "euler", 8: "readout"},
-      3: {1: "points_loaded", 6: "R10_received", 7: "arm_chain", 8: "readout"}}
+      3: {1: "points_loaded", 6: "R10_received", 8: "sh_rotated", 9: "sh_projected", 10: "sh_angle", 11: "sh_quat",
+          12: "el_quat", 7: "arm_chain", 13: "readout"}}
 F1[2] = F1[1]
 F1[4] = F1[3]
 
