@@ -10,8 +10,16 @@
 #define RTG_SIDES_TILES 2   // 64-frame tiles (two waves each) per k_solve_sides block
 #endif
 #ifndef RTG_SIDES_SPLIT_READOUT
-#define RTG_SIDES_SPLIT_READOUT 1   // FULL_BODY_POS side kernel: the left wave also reads out the right chain's slots
-                                    // (medians 101.8 / 103.3 vs 102.9 / 104.0 us SoA, 115.1 / 116.2 vs 117.0 / 118.2 AoS)
+#define RTG_SIDES_SPLIT_READOUT 0   // FULL_BODY_POS side kernel: the left wave also reads out the right chain's slots
+                                    // (round 5: medians 101.8 / 103.3 vs 102.9 / 104.0 us SoA; off since round 6's
+                                    // RTG_SIDES_ARMS2 shortened the right wave: 99.3 vs 100.6 us, profiles/r06/arms2/)
+#endif
+#ifndef RTG_SIDES_ARMS2
+#define RTG_SIDES_ARMS2 1   // FULL_BODY_POS side kernel: both arm chains in one instruction stream (fbp_arms2)
+#endif
+#ifndef RTG_AOS_PRELOAD_TIPS
+#define RTG_AOS_PRELOAD_TIPS 1   // AoS inputs: the gripper's hand points loaded with the wrist fit's (125 VGPRs, still
+                                 // 4 waves/SIMD; AoS 111.2 vs 113.5 us, SoA unchanged, profiles/r06/arms2/)
 #endif
 #ifndef RTG_SIDES_WAVES
 #define RTG_SIDES_WAVES 1   // min waves per SIMD for the side kernel (1: the compiler picks; measured best)

@@ -251,10 +251,9 @@ struct NormRcp {
     float n;
     Rcp r;
 };
-RTG_DEV NormRcp sqrt_clamp_rcp(float s, float lo)
+// the fast path of sqrt_clamp_rcp; `ok` false where its value must be replaced by sqrt_clamp_rcp_exact's
+RTG_DEV NormRcp sqrt_clamp_rcp_fast(float s, float lo, bool &ok)
 {
-    // the fast path runs unconditionally (on s <= 0 / inf / NaN its values are discarded) and ONE rare-case branch
-    // takes the cr_sqrt + rcp64 path when s is not a positive finite number or n needs the clamp
     const double d = (double)s;
     const double y = __builtin_amdgcn_rsq(d);
     double g = d * y, h = 0.5 * y;
@@ -269,11 +268,21 @@ RTG_DEV NormRcp sqrt_clamp_rcp(float s, float lo)
     const double e0 = __builtin_fma(-dn, r0, 1.0);
     const double r1 = __builtin_fma(r0, e0, r0);
     const double e1 = __builtin_fma(-dn, r1, 1.0);
-    NormRcp out{n, Rcp{__builtin_fma(r1, e1, r1), n}};
-    if (!(RTG_EXP_NO_RARE & 16) && __builtin_expect(!((d > 0.0) & (d < __builtin_inf()) & (n >= lo)), 0)) {
-        const float nc = clamp_lo(cr_sqrt(s), lo);
-        out = NormRcp{nc, rcp64(nc)};
-    }
+    ok = (d > 0.0) & (d < __builtin_inf()) & (n >= lo);
+    return NormRcp{n, Rcp{__builtin_fma(r1, e1, r1), n}};
+}
+RTG_DEV NormRcp sqrt_clamp_rcp_exact(float s, float lo)
+{
+    const float nc = clamp_lo(cr_sqrt(s), lo);
+    return NormRcp{nc, rcp64(nc)};
+}
+RTG_DEV NormRcp sqrt_clamp_rcp(float s, float lo)
+{
+    // the fast path runs unconditionally (on s <= 0 / inf / NaN its values are discarded) and ONE rare-case branch
+    // takes the cr_sqrt + rcp64 path when s is not a positive finite number or n needs the clamp
+    bool ok;
+    NormRcp out = sqrt_clamp_rcp_fast(s, lo, ok);
+    if (!(RTG_EXP_NO_RARE & 16) && __builtin_expect(!ok, 0)) out = sqrt_clamp_rcp_exact(s, lo);
     return out;
 }
 
@@ -430,6 +439,145 @@ RTG_DEV Q qfrom_angle_unit_axis(float angle, V axis)
     const float theta = angle / 2.0f;
     const SC t = cr_sincos((double)theta);
     return qnormalize(Q{axis.x * t.s, axis.y * t.s, axis.z * t.s, t.c});
+}
+
+// ------------------------------------------------ N-way forms of the leaf math (round 6)
+// Element by element the same values as the scalar functions above (each element's fast path, and its exact path
+// where that one declines), but the fast paths of all N elements run first and the whole group shares ONE rare-case
+// branch.  A rare-case branch ends a basic block, and the scheduler does not move instructions across it: in the
+// scalar forms two independent chains (the two arms of a frame) could not interleave, ~17 branches per arm map.
+template <int N>
+RTG_DEV void sqrt_clamp_rcp_n(const float (&s)[N], float lo, NormRcp (&out)[N])
+{
+    bool ok[N], all = true;
+#pragma unroll
+    for (int i = 0; i < N; ++i) {
+        out[i] = sqrt_clamp_rcp_fast(s[i], lo, ok[i]);
+        all &= ok[i];
+    }
+    if (!(RTG_EXP_NO_RARE & 16) && __builtin_expect(!all, 0)) {
+#pragma unroll
+        for (int i = 0; i < N; ++i)
+            if (!ok[i]) out[i] = sqrt_clamp_rcp_exact(s[i], lo);
+    }
+}
+// v_i * 1/n_i for N vectors: mulr_v's products; a vector with a nonzero subnormal product takes IEEE divisions
+// (the same quotients: mulr_k)
+template <int N>
+RTG_DEV void mulr_v_n(const V (&v)[N], const NormRcp (&r)[N], V (&out)[N])
+{
+    bool sub[N], any = false;
+#pragma unroll
+    for (int i = 0; i < N; ++i) {
+        const double p[3] = {(double)v[i].x * r[i].r.r, (double)v[i].y * r[i].r.r, (double)v[i].z * r[i].r.r};
+        out[i] = V{(float)p[0], (float)p[1], (float)p[2]};
+        sub[i] = false;
+#pragma unroll
+        for (int k = 0; k < 3; ++k) sub[i] |= (__builtin_fabs(p[k]) < 0x1p-126) & (p[k] != 0.0);
+        any |= sub[i];
+    }
+#if !RTG_EXP_MULR_NOBRANCH
+    if (!(RTG_EXP_NO_RARE & 8) && __builtin_expect(any, 0)) {
+#pragma unroll
+        for (int i = 0; i < N; ++i)
+            if (sub[i]) out[i] = V{v[i].x / r[i].r.n, v[i].y / r[i].r.n, v[i].z / r[i].r.n};
+    }
+#endif
+}
+template <int N>
+RTG_DEV void mulr_q_n(const Q (&v)[N], const NormRcp (&r)[N], Q (&out)[N])
+{
+    bool sub[N], any = false;
+#pragma unroll
+    for (int i = 0; i < N; ++i) {
+        const double p[4] = {(double)v[i].x * r[i].r.r, (double)v[i].y * r[i].r.r, (double)v[i].z * r[i].r.r,
+                             (double)v[i].w * r[i].r.r};
+        out[i] = Q{(float)p[0], (float)p[1], (float)p[2], (float)p[3]};
+        sub[i] = false;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) sub[i] |= (__builtin_fabs(p[k]) < 0x1p-126) & (p[k] != 0.0);
+        any |= sub[i];
+    }
+#if !RTG_EXP_MULR_NOBRANCH
+    if (!(RTG_EXP_NO_RARE & 8) && __builtin_expect(any, 0)) {
+#pragma unroll
+        for (int i = 0; i < N; ++i)
+            if (sub[i]) out[i] = div_q_call(v[i], r[i].r.n);
+    }
+#endif
+}
+template <int N>
+RTG_DEV void cr_acos_n(const float (&x)[N], float (&out)[N])
+{
+    bool ok[N], all = true;
+#pragma unroll
+    for (int i = 0; i < N; ++i) {
+        out[i] = acos_fast(x[i], ok[i]);
+        all &= ok[i];
+    }
+    if (!(RTG_EXP_NO_RARE & 2) && __builtin_expect(!all, 0)) {
+#pragma unroll
+        for (int i = 0; i < N; ++i)
+            if (!ok[i]) out[i] = acos_libm_call(x[i]);
+    }
+}
+template <int N>
+RTG_DEV void cr_sincos_n(const double (&x)[N], SC (&out)[N])
+{
+    bool sok[N], cok[N], all = true;
+#pragma unroll
+    for (int i = 0; i < N; ++i) {
+        const crm::SinCos r = crm::crm_sincos(x[i]);
+        out[i] = SC{r.s, r.c};
+        sok[i] = r.s_ok;
+        cok[i] = r.c_ok;
+        all &= r.s_ok & r.c_ok;
+    }
+    if (!(RTG_EXP_NO_RARE & 4) && __builtin_expect(!all, 0)) {
+#pragma unroll
+        for (int i = 0; i < N; ++i) {
+            if (!sok[i]) out[i].s = sin_libm_call(x[i]);
+            if (!cok[i]) out[i].c = cos_libm_call(x[i]);
+        }
+    }
+}
+template <int N>
+RTG_DEV void vunit_n(const V (&a)[N], V (&u)[N])   // vunit
+{
+    float s[N];
+#pragma unroll
+    for (int i = 0; i < N; ++i) s[i] = __builtin_fmaf(a[i].z, a[i].z, __builtin_fmaf(a[i].y, a[i].y, a[i].x * a[i].x));
+    NormRcp r[N];
+    sqrt_clamp_rcp_n<N>(s, 0.0f, r);
+    mulr_v_n<N>(a, r, u);
+}
+template <int N>
+RTG_DEV void qnormalize_n(const Q (&q0)[N], Q (&out)[N])   // qnormalize
+{
+    Q q[N];
+    float s[N];
+#pragma unroll
+    for (int i = 0; i < N; ++i) {
+        const float f = 1.0f - 2.0f * (q0[i].w < 0.0f ? 1.0f : 0.0f);
+        q[i] = Q{f * q0[i].x, f * q0[i].y, f * q0[i].z, f * q0[i].w};
+        s[i] = ((q[i].x * q[i].x + q[i].y * q[i].y) + q[i].z * q[i].z) + q[i].w * q[i].w;
+    }
+    NormRcp r[N];
+    sqrt_clamp_rcp_n<N>(s, 1e-9f, r);
+    mulr_q_n<N>(q, r, out);
+}
+template <int N>
+RTG_DEV void qfrom_angle_unit_axis_n(const float (&angle)[N], const V (&axis)[N], Q (&out)[N])
+{
+    double th[N];
+#pragma unroll
+    for (int i = 0; i < N; ++i) th[i] = (double)(angle[i] / 2.0f);
+    SC t[N];
+    cr_sincos_n<N>(th, t);
+    Q q[N];
+#pragma unroll
+    for (int i = 0; i < N; ++i) q[i] = Q{axis[i].x * t[i].s, axis[i].y * t[i].s, axis[i].z * t[i].s, t[i].c};
+    qnormalize_n<N>(q, out);
 }
 
 RTG_DEV Q qfrom_rotmat(const float m[9])  // :146-193 (the four overlapping branches, in order)
@@ -626,14 +774,7 @@ RTG_DEV V proj_in_plane(V v, V n)  // :61-75
     return vsub(v, vmul(n, dot3(v, n) / (nn * nn)));
 }
 
-RTG_DEV float radians_between(V v1, V v2, V n)  // :77-100
-{
-    v1 = vunit(v1);
-    v2 = vunit(v2);
-    const V nrm = vunit(n);
-    const float c = clamp_lohi(dot3(v1, v2), -1.0f, 1.0f);
-    return cr_acos(c) * tsign(dot3(nrm, cross3(v1, v2)));
-}
+RTG_DEV float radians_between(V v1, V v2, V n);   // :77-100 (after the N-way leaf math below)
 // radians_between with v1 and n exact unit axes (the arm maps' ex / ey / ez): their normalisation is the
 // identity (lnorm3 = sqrt(1) = 1, x * RN(1/1) = x), so only v2 is normalised -- the same bits, 2/3 fewer divides.
 RTG_DEV float radians_between_axes(V v1, V v2, V n)
@@ -1440,6 +1581,61 @@ RTG_DEV void elbow_py(V v1, ArmZero z0, Q parent, Q &yaw, Q &elbow)
     yaw = qfrom_angle_unit_axis(th1 - z0.th0, ez);
     const float ph1 = radians_between(v1p, v1r, cross3(ez, v1p));
     elbow = qfrom_angle_unit_axis(ph1 - z0.ph0, ey);
+}
+
+// the three unit vectors through one vunit_n (one rare-case branch instead of three; the same values)
+RTG_DEV float radians_between(V v1, V v2, V n)  // :77-100
+{
+    const V in[3] = {v1, v2, n};
+    V u[3];
+    vunit_n<3>(in, u);
+    const float c = clamp_lohi(dot3(u[0], u[1]), -1.0f, 1.0f);
+    return cr_acos(c) * tsign(dot3(u[2], cross3(u[0], u[1])));
+}
+
+// shoulder_pr (SHOULDER) / elbow_py of NA arms at once, on the N-way leaf math: per arm the same operations on the
+// same operands as the scalar forms above (vunit(v1p) serves both angles, as CSE made it there), so the same bits
+template <bool SHOULDER, int NA>
+RTG_DEV void arm_pair_n(const V (&v1)[NA], const ArmZero (&z0)[NA], const Q (&parent)[NA], Q (&first)[NA],
+                        Q (&second)[NA])
+{
+    const V ex{1.f, 0.f, 0.f}, ey{0.f, 1.f, 0.f}, ez{0.f, 0.f, 1.f};
+    const V pn = SHOULDER ? ey : ez;   // the plane of the first angle
+    V vec[3 * NA];
+#pragma unroll
+    for (int a = 0; a < NA; ++a) {
+        const V v1r = qrotate(qconj(parent[a]), v1[a]);
+        const V v1p = proj_in_plane(v1r, pn);
+        vec[3 * a] = v1p;
+        vec[3 * a + 1] = v1r;
+        vec[3 * a + 2] = SHOULDER ? cross3(v1p, ey) : cross3(ez, v1p);
+    }
+    V u[3 * NA];
+    vunit_n<3 * NA>(vec, u);
+    float c[2 * NA];
+#pragma unroll
+    for (int a = 0; a < NA; ++a) {
+        c[2 * a] = clamp_lohi(dot3(ex, u[3 * a]), -1.0f, 1.0f);                  // radians_between_axes(ex, v1p, pn)
+        c[2 * a + 1] = clamp_lohi(dot3(u[3 * a], u[3 * a + 1]), -1.0f, 1.0f);    // radians_between(v1p, v1r, n)
+    }
+    float ac[2 * NA];
+    cr_acos_n<2 * NA>(c, ac);
+    float ang[2 * NA];
+    V ax[2 * NA];
+#pragma unroll
+    for (int a = 0; a < NA; ++a) {
+        ang[2 * a] = ac[2 * a] * tsign(dot3(pn, cross3(ex, u[3 * a]))) - z0[a].th0;
+        ax[2 * a] = pn;
+        ang[2 * a + 1] = ac[2 * a + 1] * tsign(dot3(u[3 * a + 2], cross3(u[3 * a], u[3 * a + 1]))) - z0[a].ph0;
+        ax[2 * a + 1] = SHOULDER ? ex : ey;
+    }
+    Q q[2 * NA];
+    qfrom_angle_unit_axis_n<2 * NA>(ang, ax, q);
+#pragma unroll
+    for (int a = 0; a < NA; ++a) {
+        first[a] = q[2 * a];
+        second[a] = q[2 * a + 1];
+    }
 }
 
 // torch sum of 5 elements (cascade reduce order, measured) / 5

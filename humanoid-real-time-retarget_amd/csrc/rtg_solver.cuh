@@ -134,14 +134,32 @@ RTG_DEV void report_device_error(uint32_t *err, uint32_t code)
 
 // one arm: shoulder pitch/roll then shoulder yaw / elbow pitch (full_body_pos_retargeter.py:75-93);
 // returns quat_mul_four of the four link rotations (the wrist parent chain, :128-136)
+// (round 6: on arm_pair_n, the two angles of each map in one instruction stream with shared rare-case branches; the
+// same values as shoulder_pr / elbow_py)
 template <int L0>
 RTG_DEV Q solve_arm(const Emit &E, V upper, V fore, ArmZero zs, ArmZero ze, Q parent)
 {
     Q p, r, y, e;
-    shoulder_pr(upper, zs, parent, p, r);
+    {
+        const V v[1] = {upper};
+        const ArmZero z[1] = {zs};
+        const Q par[1] = {parent};
+        Q a[1], b[1];
+        arm_pair_n<true, 1>(v, z, par, a, b);
+        p = a[0];
+        r = b[0];
+    }
     E.link<L0>(p);
     E.link<L0 + 1>(r);
-    elbow_py(fore, ze, qmul(qmul(parent, p), r), y, e);
+    {
+        const V v[1] = {fore};
+        const ArmZero z[1] = {ze};
+        const Q par[1] = {qmul(qmul(parent, p), r)};
+        Q a[1], b[1];
+        arm_pair_n<false, 1>(v, z, par, a, b);
+        y = a[0];
+        e = b[0];
+    }
     E.link<L0 + 2>(y);
     E.link<L0 + 3>(e);
     return qmul(qmul(qmul(p, r), y), e);
@@ -293,6 +311,30 @@ RTG_DEV Q fbp_arm(const SolverConsts &C, const ArmPts &ap, Q R10, const Emit &E)
 {
     return solve_arm<SIDE ? 21 : 12>(E, vsub(ap.el, ap.sh), vsub(ap.wr, ap.el), SIDE ? C.rsh : C.lsh,
                                      SIDE ? C.rel : C.lel, R10);
+}
+// Both arms' chains at once (round 6): solve_arm for the left and the right arm on the N-way leaf math, so the two
+// independent chains interleave in one instruction stream (the same values: arm_pair_n).  Returns the chains.
+RTG_DEV void fbp_arms2(const SolverConsts &C, const ArmPts &apL, const ArmPts &apR, Q R10, const Emit &E, Q &chL,
+                       Q &chR)
+{
+    const V up[2] = {vsub(apL.el, apL.sh), vsub(apR.el, apR.sh)};
+    const V fo[2] = {vsub(apL.wr, apL.el), vsub(apR.wr, apR.el)};
+    const ArmZero zs[2] = {C.lsh, C.rsh}, ze[2] = {C.lel, C.rel};
+    const Q par[2] = {R10, R10};
+    Q p[2], r[2], y[2], e[2];
+    arm_pair_n<true, 2>(up, zs, par, p, r);
+    E.link<12>(p[0]);
+    E.link<13>(r[0]);
+    E.link<21>(p[1]);
+    E.link<22>(r[1]);
+    const Q par2[2] = {qmul(qmul(R10, p[0]), r[0]), qmul(qmul(R10, p[1]), r[1])};
+    arm_pair_n<false, 2>(fo, ze, par2, y, e);
+    E.link<14>(y[0]);
+    E.link<15>(e[0]);
+    E.link<23>(y[1]);
+    E.link<24>(e[1]);
+    chL = qmul(qmul(qmul(p[0], r[0]), y[0]), e[0]);
+    chR = qmul(qmul(qmul(p[1], r[1]), y[1]), e[1]);
 }
 // the gripper DOFs of one side from its x-spread a (full_body_pos_retargeter.py:199-215)
 template <bool PRECISE>
@@ -475,6 +517,10 @@ __global__ __launch_bounds__(kSideThreads, RTG_SIDES_WAVES) void k_solve_sides(S
         const auto b = view(in0, 63);
         Q R10 = qident(), W = qident();
         ArmPts apL{}, apR{};
+        // AoS (RTG_AOS_PRELOAD_TIPS): the gripper's hand points load with the wrist fit's, while the hand row's lines
+        // are in the L2 -- loaded after the arm chains they come back from the MALL or HBM (AoS fetch 1.57x the rows)
+        constexpr bool kPreTips = RTG_AOS_PRELOAD_TIPS && !SOA;
+        TipPts tpre{};
         if (live) {
             bool nan = false;
             if (!side) {
@@ -484,6 +530,7 @@ __global__ __launch_bounds__(kSideThreads, RTG_SIDES_WAVES) void k_solve_sides(S
             } else {
                 apL = load_arm<0>(b);
                 apR = load_arm<1>(b);
+                if (kPreTips) tpre = load_tips(view(in2, 60));
                 W = fbp_wrist_fit<1>(C, view(in2, 60), nan, hook1);
                 fit1_nan = nan;
             }
@@ -499,6 +546,18 @@ __global__ __launch_bounds__(kSideThreads, RTG_SIDES_WAVES) void k_solve_sides(S
         TS(4);
         Q chain = qident();
         if (side) {
+#if RTG_SIDES_ARMS2
+            // both arm chains in one instruction stream (fbp_arms2), then both hand-overs
+            if (live) {
+                const float4 t = storso[r];   // read R10 before the same lane overwrites the slot with the chain
+                R10 = Q{t.x, t.y, t.z, t.w};
+                Q cl;
+                fbp_arms2(C, apL, apR, R10, E, cl, chain);
+                storso[r] = make_float4(cl.x, cl.y, cl.z, cl.w);
+            }
+            lds_signal(&fl[1]);   // the left chain and its exp-map slots 0-3 are in LDS
+            if (RTG_SIDES_SPLIT_READOUT) lds_signal(&fl[3]);   // the right chain's exp-map slots 7-10 are in LDS
+#else
             if (live) {
                 const float4 t = storso[r];   // read R10 before the same lane overwrites the slot with the chain
                 R10 = Q{t.x, t.y, t.z, t.w};
@@ -508,9 +567,11 @@ __global__ __launch_bounds__(kSideThreads, RTG_SIDES_WAVES) void k_solve_sides(S
             lds_signal(&fl[1]);   // the left chain and its exp-map slots 0-3 are in LDS
             if (live) chain = fbp_arm<1>(C, apR, R10, E);
             if (RTG_SIDES_SPLIT_READOUT) lds_signal(&fl[3]);   // the right chain's exp-map slots 7-10 are in LDS
+#endif
         } else if (live) {
             emit_fixed_links(E);
             bool nan = false;
+            if (kPreTips) tpre = load_tips(view(in1, 60));
             W = fbp_wrist_fit<0>(C, view(in1, 60), nan, hook2);
             fit2_nan = nan;
         }
@@ -519,7 +580,7 @@ __global__ __launch_bounds__(kSideThreads, RTG_SIDES_WAVES) void k_solve_sides(S
         TS(6);
         if (live) {
             float *brow = body_rot ? body_rot + f * 236 : nullptr;
-            const TipPts tp = load_tips(view(side ? in2 : in1, 60));
+            const TipPts tp = kPreTips ? tpre : load_tips(view(side ? in2 : in1, 60));
             if (side) {
                 euler_refused = fbp_side_after_arm<PRECISE, 1>(C, tp, R10, chain, W, E, brow);
             } else {
