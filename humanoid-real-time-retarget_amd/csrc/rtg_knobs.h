@@ -17,6 +17,10 @@
 #ifndef RTG_SIDES_ARMS2
 #define RTG_SIDES_ARMS2 1   // FULL_BODY_POS side kernel: both arm chains in one instruction stream (fbp_arms2)
 #endif
+#ifndef RTG_SIDES_EARLY_WORDS
+#define RTG_SIDES_EARLY_WORDS 1   // FULL_BODY_POS side kernel, AoS inputs: each read-out's table word loaded into LDS
+                                  // when its link is emitted (global_load_lds), not in the read-out's batch
+#endif
 #ifndef RTG_AOS_PRELOAD_TIPS
 #define RTG_AOS_PRELOAD_TIPS 1   // AoS inputs: the gripper's hand points loaded with the wrist fit's (125 VGPRs, still
                                  // 4 waves/SIMD; AoS 111.2 vs 113.5 us, SoA unchanged, profiles/r06/arms2/)
@@ -90,6 +94,9 @@
 #endif
 #ifndef RTG_VEL_W
 #define RTG_VEL_W 8   // velocity tiles: consecutive smoothed outputs per thread (8 vs 4: linear 61.2 vs 65.1 us, angular 110.5 vs 113.1)
+#endif
+#ifndef RTG_VEL_ANG_NWAY
+#define RTG_VEL_ANG_NWAY 1   // angular velocity tile: a batch's NB elements on the N-way leaf math (rtg_math.cuh)
 #endif
 #ifndef RTG_VEL_ANG_NB
 #define RTG_VEL_ANG_NB 2   // angular velocity tile: raw elements per thread per load batch (1-4 measured alike, ~110 us)

@@ -715,15 +715,30 @@ struct ExpDof {
     float angle, sin_theta;
     bool mask, exact;
 };
+// the table word a read-out of w needs (word 0 when w is outside the table: its code is not used)
+RTG_DEV uint32_t ang_tab_word_of(float w)
+{
+    const uint32_t i = __float_as_uint(w) - kAngTabLo;
+    return i < kAngTabEntries ? ang_tab_word(i) : 0u;
+}
+RTG_DEV ExpDof exp_dof_word_part(float w, uint32_t word);
 RTG_DEV ExpDof exp_dof_table_part(float w, const uint32_t *__restrict__ tab)
+{
+#if RTG_EXP_NO_TABLE
+    const uint32_t word = 0x24924924u + 0u * tab[0];
+#else
+    const uint32_t word = tab[ang_tab_word_of(w)];
+#endif
+    return exp_dof_word_part(w, word);
+}
+// the read-out of w from its table word (loaded by the caller: exp_dof_table_part, or early into LDS, Emit::wd)
+RTG_DEV ExpDof exp_dof_word_part(float w, uint32_t word)
 {
     const uint32_t i = __float_as_uint(w) - kAngTabLo;
     const bool in = i < kAngTabEntries;
     const uint32_t wd = ang_tab_word(i);
 #if RTG_EXP_NO_TABLE
-    const uint32_t word = 0x24924924u + 0u * tab[0];
-#else
-    const uint32_t word = tab[in ? wd : 0u];
+    word = 0x24924924u;
 #endif
     const float sin_theta = cr_sqrt(1.0f - w * w);
     const bool mask = fabsf(sin_theta) > 1e-5f;

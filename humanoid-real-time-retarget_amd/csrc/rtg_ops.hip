@@ -620,6 +620,45 @@ __global__ __launch_bounds__(256) void k_velocity_tile(const float *__restrict__
             uint32_t cat[NB];
 #pragma unroll
             for (int k = 0; k < NB; ++k) { ca[k] = qa[k]; cb[k] = qb[k]; cl[k] = last[k]; cat[k] = at[k]; }
+#if RTG_VEL_ANG_NWAY && !RTG_VEL_IEEE_DIV
+            // round 6: the NB elements on the N-way leaf math (one rare-case branch per step for all of them, so
+            // their instruction streams interleave); every element's value as below.  Elements past the rows and
+            // last frames compute on whatever they hold and are replaced / not stored.
+            {
+                Q prod[NB], dn[NB], d[NB];
+#pragma unroll
+                for (int k = 0; k < NB; ++k) prod[k] = qmul(ca[k], qconj(cb[k]));
+                qnormalize_n<NB>(prod, dn);
+                float c[NB], s3[NB];
+                V xyz[NB];
+#pragma unroll
+                for (int k = 0; k < NB; ++k) {   // quat_angle_axis (rotation3d.py:230-240), qangle_axis_abs
+                    d[k] = cl[k] ? qident() : dn[k];
+                    c[k] = clamp_lohi(2.0f * (d[k].w * d[k].w) - 1.0f, -1.0f, 1.0f);
+                    s3[k] = (d[k].x * d[k].x + d[k].y * d[k].y) + d[k].z * d[k].z;
+                    xyz[k] = V{d[k].x, d[k].y, d[k].z};
+                }
+                float ang[NB];
+                cr_acos_n<NB>(c, ang);
+                NormRcp nr[NB], rdt[NB];
+                sqrt_clamp_rcp_n<NB>(s3, 1e-9f, nr);
+                V ax[NB], prod3[NB], av[NB];
+                mulr_v_n<NB>(xyz, nr, ax);
+#pragma unroll
+                for (int k = 0; k < NB; ++k) {
+                    prod3[k] = V{ax[k].x * ang[k], ax[k].y * ang[k], ax[k].z * ang[k]};
+                    rdt[k] = NormRcp{dt, Rcp{vt.rdt, dt}};
+                }
+                mulr_v_n<NB>(prod3, rdt, av);
+#pragma unroll
+                for (int k = 0; k < NB; ++k)
+                    if (e0 + 256u * k < n) {
+                        sg[cat[k]] = av[k].x;
+                        sg[cat[k] + NS] = av[k].y;
+                        sg[cat[k] + 2 * NS] = av[k].z;
+                    }
+            }
+#else
 #pragma unroll
             for (int k = 0; k < NB; ++k) {
                 if (e0 + 256u * k >= n) continue;
@@ -637,6 +676,7 @@ __global__ __launch_bounds__(256) void k_velocity_tile(const float *__restrict__
                 sg[cat[k] + 2 * NS] = av.z;
 #endif
             }
+#endif
             if (e0 + 256 * NB < n) fetch(e0 + 256 * NB);
         }
     }
@@ -1014,8 +1054,8 @@ int probe_valu_iters() { return kProbeIters; }
 extern "C" const char *rtg_build_info(void)
 {
     return "{\"abi\":" RTG_STR(RTG_ABI_VERSION) ",\"arch\":\"gfx950\",\"knobs\":{"
-        RTG_KNOB(RTG_SIDES_WAVES) RTG_KNOB(RTG_SIDES_TILES) RTG_KNOB(RTG_SIDES_SPLIT_READOUT) RTG_KNOB(RTG_SIDES_ARMS2) RTG_KNOB(RTG_AOS_PRELOAD_TIPS) RTG_KNOB(RTG_QUAD8_MAX_B) RTG_KNOB(RTG_QUAD_MAX_B) RTG_KNOB(RTG_LATENCY_MAX_B)
-        RTG_KNOB(RTG_EXP_TIMESTAMPS) RTG_KNOB(RTG_EXP_SKIP_SIGNAL) RTG_KNOB(RTG_EXP_STUB_SVD) RTG_KNOB(RTG_EXP_NO_TABLE) RTG_KNOB(RTG_EXP_MULR_NOBRANCH) RTG_KNOB(RTG_FK_F16_MAXJ) RTG_KNOB(RTG_FK_NT_OUT) RTG_KNOB(RTG_EXP_LARTG_RCP64) RTG_KNOB(RTG_EXP_SQRT64) RTG_KNOB(RTG_EXP_SQRT_CALL) RTG_KNOB(RTG_EXP_ACOS_LIBM) RTG_KNOB(RTG_EXP_EULER_SCIPY) RTG_KNOB(RTG_VEL_SEG) RTG_KNOB(RTG_VEL_LDS_MIN) RTG_KNOB(RTG_VEL_IEEE_DIV) RTG_KNOB(RTG_DOF_NT_STORE) RTG_KNOB(RTG_IN_NT_LOAD) RTG_KNOB(RTG_VEL_W) RTG_KNOB(RTG_VEL_ANG_NB) RTG_KNOB(RTG_EXP_NO_RARE)
+        RTG_KNOB(RTG_SIDES_WAVES) RTG_KNOB(RTG_SIDES_TILES) RTG_KNOB(RTG_SIDES_SPLIT_READOUT) RTG_KNOB(RTG_SIDES_ARMS2) RTG_KNOB(RTG_SIDES_EARLY_WORDS) RTG_KNOB(RTG_AOS_PRELOAD_TIPS) RTG_KNOB(RTG_QUAD8_MAX_B) RTG_KNOB(RTG_QUAD_MAX_B) RTG_KNOB(RTG_LATENCY_MAX_B)
+        RTG_KNOB(RTG_EXP_TIMESTAMPS) RTG_KNOB(RTG_EXP_SKIP_SIGNAL) RTG_KNOB(RTG_EXP_STUB_SVD) RTG_KNOB(RTG_EXP_NO_TABLE) RTG_KNOB(RTG_EXP_MULR_NOBRANCH) RTG_KNOB(RTG_FK_F16_MAXJ) RTG_KNOB(RTG_FK_NT_OUT) RTG_KNOB(RTG_EXP_LARTG_RCP64) RTG_KNOB(RTG_EXP_SQRT64) RTG_KNOB(RTG_EXP_SQRT_CALL) RTG_KNOB(RTG_EXP_ACOS_LIBM) RTG_KNOB(RTG_EXP_EULER_SCIPY) RTG_KNOB(RTG_VEL_SEG) RTG_KNOB(RTG_VEL_LDS_MIN) RTG_KNOB(RTG_VEL_IEEE_DIV) RTG_KNOB(RTG_DOF_NT_STORE) RTG_KNOB(RTG_IN_NT_LOAD) RTG_KNOB(RTG_VEL_W) RTG_KNOB(RTG_VEL_ANG_NB) RTG_KNOB(RTG_VEL_ANG_NWAY) RTG_KNOB(RTG_EXP_NO_RARE)
         "\"RTG_EXP_HOT_INPUTS\":\"" RTG_STR(RTG_EXP_HOT_INPUTS) "\"},\"wrong_answer_knobs\":"
         RTG_STR(RTG_WRONG_ANSWER_KNOBS) "}";
 }

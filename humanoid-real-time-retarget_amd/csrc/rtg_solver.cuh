@@ -35,14 +35,27 @@ struct Emit {
     const uint32_t *__restrict__ ang;   // exp-map angle table (SolverConsts::ang_tab)
     float2 *st;                  // LDS stash of this lane: (w, Hu_DOF_AXIS component) per DOF link, stride sst
     int sst;
+    // k_solve_sides FULL_BODY_POS (round 6): the wave's LDS block of table words, [slot][lane] (stride 64, the same
+    // slots as st).  link() starts the load of its read-out's table word straight into it (global_load_lds: no VGPR,
+    // asynchronous), so the word is there long before the read-out; finalize reads it from LDS after a vmcnt wait.
+    // nullptr: finalize loads the words itself.
+    uint32_t *wd = nullptr;
     // links 12..18 and 21..27 (DOFs 11..17, 20..26) -> stash slots 0..13
     template <int LINK>
     static constexpr int slot() { return LINK <= 18 ? LINK - 12 : LINK - 14; }
+    RTG_DEV void load_word(int s, float w) const
+    {
+#if !RTG_EXP_NO_TABLE
+        __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void *)(ang + ang_tab_word_of(w)),
+                                         (__attribute__((address_space(3))) void *)(wd + s * 64), 4, 0, 0);
+#endif
+    }
     template <int LINK>
     RTG_DEV void link(Q q) const
     {
         constexpr int k = hu_dof_axis(LINK - 1);
         st[slot<LINK>() * sst] = make_float2(q.w, k == 0 ? q.x : (k == 1 ? q.y : q.z));
+        if (wd) load_word(slot<LINK>(), q.w);
         if (lr) st4(lr + 4 * LINK, q);
     }
     template <int LINK>
@@ -58,11 +71,12 @@ struct Emit {
     RTG_DEV void finalize(int s0, int n) const
     {
         uint32_t exact = 0;
+        if (wd) wait_words();
 #pragma unroll
         for (int j = 0; j < 14; ++j)
             if (j >= s0 && j < s0 + n) {
                 const float2 v = st[j * sst];
-                const ExpDof e = exp_dof_table_part(v.x, ang);
+                const ExpDof e = wd ? exp_dof_word_part(v.x, wd[j * 64 + (threadIdx.x & 63)]) : exp_dof_table_part(v.x, ang);
                 exact |= (uint32_t)e.exact << j;
                 row[j < 7 ? 11 + j : 13 + j] = exp_dof_finish(e, v.y);
             }
@@ -75,6 +89,8 @@ struct Emit {
                 }
         }
     }
+    // this wave's table-word loads into LDS have landed (vmcnt 0; expcnt / lgkmcnt not waited on)
+    static RTG_DEV void wait_words() { __builtin_amdgcn_s_waitcnt(0x0F70); }
 };
 
 RTG_DEV void emit_fixed_links(const Emit &E, bool write_lr = true)
@@ -476,7 +492,14 @@ __global__ __launch_bounds__(kSideThreads, RTG_SIDES_WAVES) void k_solve_sides(S
     const int64_t f0 = (int64_t)blockIdx.x * kSideFrames, f = f0 + r;
     const bool live = f < B;
     float *const lrow = live && local_rot ? local_rot + f * 124 : nullptr;
-    const Emit E{sdof + r * kDofStride, lrow, C.ang_tab, sst + (w >> 1) * 14 * 64 + lane, 64};
+#if RTG_SIDES_EARLY_WORDS
+    __shared__ uint32_t swd[kSideTiles * 14 * 64];   // FULL_BODY_POS: the read-outs' table words, [tile][slot][lane]
+    // AoS only: SoA 99.5-102.8 vs 99.9-100.9 us without, AoS 110.1-111.2 vs 110.7-113.4 (profiles/r06/early_words/)
+    uint32_t *const wds = KIND == RTG_SOLVER_FULL_BODY_POS && !SOA ? swd + (w >> 1) * 14 * 64 : nullptr;
+#else
+    uint32_t *const wds = nullptr;
+#endif
+    const Emit E{sdof + r * kDofStride, lrow, C.ang_tab, sst + (w >> 1) * 14 * 64 + lane, 64, wds};
 #if RTG_EXP_HOT_INPUTS   // measurement knob (tools/build_variants.sh): every tile reads the first block's rows
     const int64_t fi = f & (kSideFrames - 1);
 #else
@@ -555,6 +578,7 @@ __global__ __launch_bounds__(kSideThreads, RTG_SIDES_WAVES) void k_solve_sides(S
                 fbp_arms2(C, apL, apR, R10, E, cl, chain);
                 storso[r] = make_float4(cl.x, cl.y, cl.z, cl.w);
             }
+            if (wds) Emit::wait_words();   // the left chain's table words (slots 0-3) have landed in LDS
             lds_signal(&fl[1]);   // the left chain and its exp-map slots 0-3 are in LDS
             if (RTG_SIDES_SPLIT_READOUT) lds_signal(&fl[3]);   // the right chain's exp-map slots 7-10 are in LDS
 #else
