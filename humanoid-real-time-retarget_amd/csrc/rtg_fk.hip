@@ -4,6 +4,7 @@
 #include "rtg_device.cuh"
 
 #include <algorithm>
+#include <type_traits>
 #include <vector>
 
 namespace rtg {
@@ -386,9 +387,62 @@ __global__ __launch_bounds__(64, 4) void k_lrot_group(TopoView T, const float *_
 // axis -- and writes them into the tile image where FK's local rotations would be; then FK's compose runs as is.  (A
 // first version built each joint's rotation inside its compose step: the f64 sincos sat on the chain's critical path
 // and the kernel took 128 us against FK's 88, profiles/r06/fk/.)  LDS = the tile image | per-joint {axis, lower, upper}
+//
+// The joint rotations' normalisation (round 6).  q = {e_ax sin, cos} from a correctly rounded sin / cos pair has
+// |q|^2 = RN(RN(s s) + RN(c c)) within a few f32 codes of 1.0f, so sqrt_clamp_rcp's (n, 1/n) come from a table of
+// the 2K + 1 codes around 1.0f, filled by each wave with sqrt_clamp_rcp_exact itself (its loads are in flight by
+// then): a lookup returns exactly that function's values.
+constexpr int kUnitTabK = 16;
+struct UnitEnt {
+    double r;
+    float n, pad;
+};
+RTG_DEV void unit_tab_fill(UnitEnt *tab)
+{
+    const int l = (int)threadIdx.x;
+    if (l <= 2 * kUnitTabK) {
+        const NormRcp e = sqrt_clamp_rcp_exact(__int_as_float(0x3F800000 - kUnitTabK + l), 1e-9f);
+        tab[l] = UnitEnt{e.r.r, e.n, 0.0f};
+    }
+}
+// qfrom_angle_unit_axis(angle, e_ax) for N joints, element by element the same values: qnormalize's sign flip f
+// (on cos), its |q|^2 in any component order (the zero components add +0 exactly), (n, 1/n) from the table, the two
+// nonzero components' products by 1/n, and the zero components keep the sign of f sin (0 sin, times f, times 1/n > 0).
+// A |q|^2 outside the table (NaN / inf angles) or a subnormal product: the scalar path, one rare-case branch per group.
+template <int N>
+RTG_DEV void joint_rot_n(const float (&angle)[N], const int (&ax)[N], const UnitEnt *tab, Q (&out)[N])
+{
+    double th[N];
+#pragma unroll
+    for (int i = 0; i < N; ++i) th[i] = (double)(angle[i] / 2.0f);
+    SC t[N];
+    cr_sincos_n<N>(th, t);
+    bool ok[N], all = true;
+#pragma unroll
+    for (int i = 0; i < N; ++i) {
+        const float f = 1.0f - 2.0f * (t[i].c < 0.0f ? 1.0f : 0.0f);
+        const float s = f * t[i].s, c = f * t[i].c;
+        const float n2 = s * s + c * c;
+        const uint32_t idx = (uint32_t)(__float_as_int(n2) - (0x3F800000 - kUnitTabK));
+        const bool in = idx <= 2u * kUnitTabK;
+        const double r = tab[in ? idx : 0u].r;
+        const double ps = (double)s * r, pc = (double)c * r;
+        const float qs = (float)ps, z = __builtin_copysignf(0.0f, s);
+        out[i] = Q{ax[i] == 0 ? qs : z, ax[i] == 1 ? qs : z, ax[i] == 2 ? qs : z, (float)pc};
+        ok[i] = in & !((__builtin_fabs(ps) < 0x1p-126) & (ps != 0.0)) & !((__builtin_fabs(pc) < 0x1p-126) & (pc != 0.0));
+        all &= ok[i];
+    }
+    if (__builtin_expect(!all, 0)) {
+#pragma unroll
+        for (int i = 0; i < N; ++i)
+            if (!ok[i])
+                out[i] = qfrom_angle_unit_axis(angle[i], V{ax[i] == 0 ? 1.0f : 0.0f, ax[i] == 1 ? 1.0f : 0.0f,
+                                                           ax[i] == 2 ? 1.0f : 0.0f});
+    }
+}
 __host__ __device__ inline size_t dof_group_lds_floats(int J, int F, int steps)
 {
-    return group_lds_floats(J, F, steps) + (size_t)J * 4;
+    return group_lds_floats(J, F, steps) + (size_t)J * 4 + (RTG_DOF_UNIT_TAB ? 4 * (2 * kUnitTabK + 1) : 0);
 }
 template <bool CLIP, int F>
 __global__ __launch_bounds__(64, 4) void k_dof_fk_group(TopoView T, DofView D, const float *__restrict__ dof,
@@ -417,6 +471,8 @@ __global__ __launch_bounds__(64, 4) void k_dof_fk_group(TopoView T, DofView D, c
     const f4v rr = reinterpret_cast<const f4v *>(root_rot)[f0 + (lane < nfr ? lane : 0)];
     const float rt = root_t[f0 * 3 + (lane < 3 * nfr ? lane : 0)];
     group_sched_fill(T, G::L, sch);
+    UnitEnt *utab = reinterpret_cast<UnitEnt *>(ntab + J);
+    if (RTG_DOF_UNIT_TAB) unit_tab_fill(utab);
     for (int j = 1 + lane; j < J; j += 64) {
         const int ax = ld_const(D.axis + (j - 1));
         ntab[j] = f4v{__int_as_float(ax), CLIP ? ld_const(D.lower + (j - 1)) : 0.0f,
@@ -431,24 +487,47 @@ __global__ __launch_bounds__(64, 4) void k_dof_fk_group(TopoView T, DofView D, c
     // angle i = (frame fr, joint i mod nd + 1): its rotation into record fr J + j (i / nd as ((i + 1/2) / nd)
     // truncated: exact for i < 2^12)
     const float rnd = 1.0f / (float)(nd > 0 ? nd : 1);
+    // NW loads' rotations at a time on the N-way leaf math (one rare-case branch per group, the same bits); a lane
+    // past the angles computes a dummy rotation (its j is still a joint) and does not store it
+    auto rotations = [&](auto nw, int k0) {
+        constexpr int NW = decltype(nw)::value;
+        if (k0 * 64 >= nang) return;   // wave-uniform: no lane has an angle in this group
+        float x[NW];
+        int axi[NW], rec[NW];
 #pragma unroll
-    for (int k = 0; k < G::NR; ++k) {
-        const int i = k * 64 + lane;
-        if (i < nang) {
+        for (int w = 0; w < NW; ++w) {
+            const int i = (k0 + w) * 64 + lane;
             const int fr = (int)(((float)i + 0.5f) * rnd), j = i - fr * nd + 1;
             const f4v t = ntab[j];
-            float x = a[k];
+            x[w] = a[k0 + w];
             if (CLIP) {   // torch.clamp (min then max; NaN passes), then the straight-through sum
-                float c = x < t.y ? t.y : x;
+                float c = x[w] < t.y ? t.y : x[w];
                 c = c > t.z ? t.z : c;
-                x = (c - x) + x;
+                x[w] = (c - x[w]) + x[w];
             }
-            const int ax = __float_as_int(t.x);
             // the axis is an exact unit vector: quat_from_angle_axis's normalisation is the identity (round 5)
-            const Q q = qfrom_angle_unit_axis(x, V{ax == 0 ? 1.0f : 0.0f, ax == 1 ? 1.0f : 0.0f, ax == 2 ? 1.0f : 0.0f});
-            rot[fr * J + j] = f4v{q.x, q.y, q.z, q.w};
+            axi[w] = __float_as_int(t.x);
+            rec[w] = i < nang ? fr * J + j : -1;
         }
-    }
+        Q q[NW];
+#if RTG_DOF_UNIT_TAB
+        joint_rot_n<NW>(x, axi, utab, q);
+#else
+        V axv[NW];
+#pragma unroll
+        for (int w = 0; w < NW; ++w)
+            axv[w] = V{axi[w] == 0 ? 1.0f : 0.0f, axi[w] == 1 ? 1.0f : 0.0f, axi[w] == 2 ? 1.0f : 0.0f};
+        qfrom_angle_unit_axis_n<NW>(x, axv, q);
+#endif
+#pragma unroll
+        for (int w = 0; w < NW; ++w)
+            if (rec[w] >= 0) rot[rec[w]] = f4v{q[w].x, q[w].y, q[w].z, q[w].w};
+    };
+    constexpr int NW = RTG_DOF_NWAY, NFULL = G::NR - G::NR % NW;
+#pragma unroll
+    for (int k = 0; k < NFULL; k += NW) rotations(std::integral_constant<int, NW>{}, k);
+#pragma unroll
+    for (int k = NFULL; k < G::NR; ++k) rotations(std::integral_constant<int, 1>{}, k);
     wave_sync();
     group_compose<F>(T, rot, pos, sch, nfr, [&](int, Q lq, const GEnt &, int) { return lq; });
     group_store<F>(rot, pos, nrec, g_rot + f0 * J * 4, g_pos + f0 * J * 3);

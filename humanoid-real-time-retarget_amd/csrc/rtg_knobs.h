@@ -98,6 +98,12 @@
 #ifndef RTG_VEL_ANG_NWAY
 #define RTG_VEL_ANG_NWAY 1   // angular velocity tile: a batch's NB elements on the N-way leaf math (rtg_math.cuh)
 #endif
+#ifndef RTG_DOF_NWAY
+#define RTG_DOF_NWAY 4   // HuForwardModel lane groups: joint rotations per N-way group (one rare-case branch each)
+#endif
+#ifndef RTG_DOF_UNIT_TAB
+#define RTG_DOF_UNIT_TAB 1   // HuForwardModel: joint rotations normalised through the near-1.0f (n, 1/n) table
+#endif
 #ifndef RTG_VEL_ANG_NB
 #define RTG_VEL_ANG_NB 2   // angular velocity tile: raw elements per thread per load batch (1-4 measured alike, ~110 us)
 #endif

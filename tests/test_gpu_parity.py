@@ -234,6 +234,38 @@ def test_dof_fk_vs_oracle_and_reference(gpu, tag, name):
     np.testing.assert_array_equal(_np(gp), ogp)
 
 
+def test_dof_fk_edge_angles(gpu):
+    """The joint rotations' fast path (N-way groups, the near-1.0f normalisation table) against the oracle on the
+    angles that leave it: +-0, subnormal and tiny angles (subnormal sin products), +-pi and odd multiples (cos near
+    0, the sign flip), huge, +-inf and NaN, mixed into random frames so every group has some; clip off and on."""
+    import oracle as orc
+    from rtg import assets, ops
+    from rtg.runtime import DofModel
+    from retarget.robot_config import Hu_v5
+    T = _topo("hu_v5")
+    par, lt = assets.parents("hu_v5"), assets.local_translation("hu_v5")
+    n = T.num_joints - 1
+    edge = np.array([0.0, -0.0, 1e-45, -1e-45, 1e-38, 3e-39, -2e-30, 1e-7, np.pi, -np.pi, 3 * np.pi, 2 * np.pi,
+                     np.float32(np.pi) * np.float32(1 + 2 ** -23), 1e5, -3e7, 1e30, np.inf, -np.inf, np.nan,
+                     4.0, -4.0], np.float32)
+    rng = np.random.default_rng(23)
+    B = 4099
+    dof = rng.uniform(-4, 4, (B, n)).astype(np.float32)
+    mask = rng.random((B, n)) < 0.15
+    dof[mask] = rng.choice(edge, mask.sum())
+    dof[:len(edge)] = edge[:, None]   # whole frames of one edge value
+    rr = rng.normal(size=(B, 4)).astype(np.float32)
+    rt = rng.normal(0, 0.3, (B, 3)).astype(np.float32)
+    lo = np.full(n, -2.5, np.float32)
+    hi = np.full(n, 2.5, np.float32)
+    for lim in (None, (lo, hi)):
+        model = DofModel(T, Hu_v5.Hu_DOF_AXIS, *(lim or (None, None)))
+        gr, gp = ops.dof_forward_kinematics(model, dof, rr, rt, clip=lim is not None)
+        ogr, ogp = orc.dof_fk(par, lt, np.asarray(Hu_v5.Hu_DOF_AXIS), dof, rr, rt, *(lim or (None, None)))
+        np.testing.assert_array_equal(_np(gr), ogr)
+        np.testing.assert_array_equal(_np(gp), ogp)
+
+
 def test_dof_fk_roundtrip_with_retargeted_dofs(gpu):
     """Closing the loop: the retargeted Hu v5 DOFs of the golden frames, driven through the
     joint-angle model, reproduce FK of the solver's own local rotations (identity root)."""
