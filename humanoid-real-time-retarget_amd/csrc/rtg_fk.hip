@@ -145,6 +145,53 @@ RTG_DEV void st_out(f4v *p, f4v v)
 }
 
 // ----------------------------------------------------------------------------
+// Near-unit normalisation (round 6).  Every quaternion these kernels normalise is a product of unit quaternions
+// (FK's compose, inverse FK) or {e_ax sin, cos} from a correctly rounded pair (HuForwardModel's joints), so its
+// |q|^2 lands within a few f32 codes of 1.0f.  sqrt_clamp_rcp's (n, 1/n) for the 2K + 1 codes around 1.0f are a
+// table, filled by each wave with sqrt_clamp_rcp_exact itself while its loads are in flight: a lookup returns exactly
+// that function's values, and a |q|^2 outside it (a non-unit root rotation or input row) takes qnormalize itself.
+constexpr int kUnitTabK = 16;
+struct UnitEnt {
+    double r;
+    float n, pad;
+};
+constexpr bool kUnitTab = RTG_FK_UNIT_TAB || RTG_DOF_UNIT_TAB;
+constexpr size_t kUnitTabFloats = kUnitTab ? 4 * (2 * kUnitTabK + 1) : 0;
+RTG_DEV void unit_tab_fill(UnitEnt *tab)
+{
+    const int l = (int)threadIdx.x;
+    if (l <= 2 * kUnitTabK) {
+        const NormRcp e = sqrt_clamp_rcp_exact(__int_as_float(0x3F800000 - kUnitTabK + l), 1e-9f);
+        tab[l] = UnitEnt{e.r.r, e.n, 0.0f};
+    }
+}
+RTG_DEV bool unit_tab_index(float s, uint32_t &idx)
+{
+    idx = (uint32_t)(__float_as_int(s) - (0x3F800000 - kUnitTabK));
+    const bool in = idx <= 2u * kUnitTabK;
+    idx = in ? idx : 0u;
+    return in;
+}
+// qnormalize (quat_unit(quat_pos(q))) with the table: the same sign flip, sum, products and subnormal test
+RTG_DEV Q qnormalize_tab(Q q0, const UnitEnt *tab)
+{
+    if (!RTG_FK_UNIT_TAB) return qnormalize(q0);
+    const float f = 1.0f - 2.0f * (q0.w < 0.0f ? 1.0f : 0.0f);
+    const Q q{f * q0.x, f * q0.y, f * q0.z, f * q0.w};
+    uint32_t idx;
+    const bool in = unit_tab_index(((q.x * q.x + q.y * q.y) + q.z * q.z) + q.w * q.w, idx);
+    const double r = tab[idx].r;
+    const double p[4] = {(double)q.x * r, (double)q.y * r, (double)q.z * r, (double)q.w * r};
+    bool sub = false;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) sub |= (__builtin_fabs(p[i]) < 0x1p-126) & (p[i] != 0.0);
+    Q out{(float)p[0], (float)p[1], (float)p[2], (float)p[3]};
+    if (__builtin_expect(!in | sub, 0)) out = qnormalize(q0);
+    return out;
+}
+RTG_DEV Q qmul_norm_tab(Q a, Q b, const UnitEnt *tab) { return qnormalize_tab(qmul(a, b), tab); }
+
+// ----------------------------------------------------------------------------
 // Lane-group kinematics (round 6): a frame's joints spread over a GROUP of lanes, F frames per wave (F = 16: four
 // lanes per frame for J <= 36; F = 8: eight lanes for J <= 64), so the tile's rows move as whole coalesced pieces.
 // The windowed kernels above keep one frame per lane, and each of their load / store instructions touches 64 rows
@@ -172,9 +219,14 @@ struct Grp {
 };
 __host__ __device__ inline size_t pad16f(size_t nfloats) { return (nfloats + 3) & ~(size_t)3; }
 // rot [F J] float4 | pos [F J 3] float | schedule [gsteps L] GEnt | extra floats (kernel-specific tables)
-__host__ __device__ inline size_t group_lds_floats(int J, int F, int steps)
+// ... | the near-unit table (kUnitTabFloats)
+__host__ __device__ inline size_t group_core_floats(int J, int F, int steps)
 {
     return (size_t)F * J * 4 + pad16f((size_t)F * J * 3) + (size_t)steps * (64 / F) * 8;
+}
+__host__ __device__ inline size_t group_lds_floats(int J, int F, int steps)
+{
+    return group_core_floats(J, F, steps) + kUnitTabFloats;
 }
 
 // the tile's schedule into LDS (float4 copies, in flight with the tile's own loads)
@@ -190,7 +242,8 @@ RTG_DEV void group_sched_fill(const TopoView &T, int L, GEnt *sch)
 // root's preset).  LQ(j, lq) gives joint j's local rotation from its image record (FK: the record itself, with the
 // tree quaternion when STATE; DOF FK: built from the joint angle).
 template <int F, typename LocalQ>
-RTG_DEV void group_compose(const TopoView &T, f4v *rot, float *pos, const GEnt *sch, int nfr, const LocalQ &LQ)
+RTG_DEV void group_compose(const TopoView &T, f4v *rot, float *pos, const GEnt *sch, int nfr, const UnitEnt *utab,
+                           const LocalQ &LQ)
 {
     using G = Grp<F>;
     const int J = T.J, lane = (int)threadIdx.x;
@@ -214,7 +267,7 @@ RTG_DEV void group_compose(const TopoView &T, f4v *rot, float *pos, const GEnt *
                 const float *tp = pos + 3 * (base + p);
                 const V t{tp[0], tp[1], tp[2]};
                 const V rv = qrotate(g, V{e.lx, e.ly, e.lz});
-                ng = qmul_norm(g, lq);
+                ng = qmul_norm_tab(g, lq, utab);
                 nt = V{rv.x + t.x, rv.y + t.y, rv.z + t.z};
             }
             rot[base + j] = f4v{ng.x, ng.y, ng.z, ng.w};
@@ -294,14 +347,16 @@ RTG_DEV void fk_group_tile(const TopoView &T, const float *__restrict__ local_ro
     rows.load(local_rot + f0 * J * 4, nrec);
     const float r = root_t[f0 * 3 + (lane < 3 * nfr ? lane : 0)];
     group_sched_fill(T, Grp<F>::L, sch);
+    UnitEnt *utab = reinterpret_cast<UnitEnt *>(lds + group_core_floats(J, F, T.gsteps));
+    if (RTG_FK_UNIT_TAB) unit_tab_fill(utab);
     rows.to_lds(rot, nrec);
     if (lane < 3 * nfr) {
         const int fr = lane / 3;
         pos[3 * J * fr + (lane - 3 * fr)] = r;
     }
     wave_sync();
-    group_compose<F>(T, rot, pos, sch, nfr, [&](int, Q lq, const GEnt &e, int) {
-        if (STATE) lq = qmul_norm(Q{e.qx, e.qy, e.qz, e.qw}, lq);   // skeleton3d.py:412-418
+    group_compose<F>(T, rot, pos, sch, nfr, utab, [&](int, Q lq, const GEnt &e, int) {
+        if (STATE) lq = qmul_norm_tab(Q{e.qx, e.qy, e.qz, e.qw}, lq, utab);   // skeleton3d.py:412-418
         return lq;
     });
     group_store<F>(rot, pos, nrec, g_rot + f0 * J * 4, g_pos + f0 * J * 3);
@@ -318,7 +373,8 @@ __global__ __launch_bounds__(64, 4) void k_fk_group(TopoView T, const float *__r
 
 // inverse FK: LDS = the tile image | parents (J ints) | STATE: normalised conjugate tree quaternions (J float4)
 constexpr int kLrotFrames = 8;   // frames per wave of the inverse tiles (any J <= kGroupMaxJ)
-static inline size_t lrot_group_lds_floats(int J, int F) { return (size_t)F * J * 4 + pad16f((size_t)J) + (size_t)J * 4; }
+__host__ __device__ inline size_t lrot_core_floats(int J, int F) { return (size_t)F * J * 4 + pad16f((size_t)J) + (size_t)J * 4; }
+__host__ __device__ inline size_t lrot_group_lds_floats(int J, int F) { return lrot_core_floats(J, F) + kUnitTabFloats; }
 template <bool STATE, int F>
 RTG_DEV void lrot_group_tile(const TopoView &T, const float *__restrict__ g_rot, int64_t B, int64_t f0,
                              float *__restrict__ local_rot, float *lds)
@@ -337,6 +393,8 @@ RTG_DEV void lrot_group_tile(const TopoView &T, const float *__restrict__ g_rot,
         const int rec = k * 64 + lane;
         v[k] = src[rec < nrec ? rec : 0];
     }
+    UnitEnt *utab = reinterpret_cast<UnitEnt *>(lds + lrot_core_floats(J, F));
+    if (RTG_FK_UNIT_TAB) unit_tab_fill(utab);
     for (int j = lane; j < J; j += 64) {
         par[j] = ld_const(T.parents + j);
         if (STATE) {   // skeleton3d.py:470-478: quat_normalize(quat_conjugate(tree quat)), once per joint
@@ -362,10 +420,10 @@ RTG_DEV void lrot_group_tile(const TopoView &T, const float *__restrict__ g_rot,
             Q q = gj;   // root copied (kinematics.py:49)
             if (j > 0) {
                 const f4v pv = rot[fr * J + par[j]];
-                q = qmul_norm(qconj(Q{pv.x, pv.y, pv.z, pv.w}), gj);
+                q = qmul_norm_tab(qconj(Q{pv.x, pv.y, pv.z, pv.w}), gj, utab);
                 if (STATE) {
                     const f4v c = tqn[j];
-                    q = qmul_norm(Q{c.x, c.y, c.z, c.w}, q);
+                    q = qmul_norm_tab(Q{c.x, c.y, c.z, c.w}, q, utab);
                 }
             }
             st_out(dst + rec, f4v{q.x, q.y, q.z, q.w});
@@ -387,24 +445,6 @@ __global__ __launch_bounds__(64, 4) void k_lrot_group(TopoView T, const float *_
 // axis -- and writes them into the tile image where FK's local rotations would be; then FK's compose runs as is.  (A
 // first version built each joint's rotation inside its compose step: the f64 sincos sat on the chain's critical path
 // and the kernel took 128 us against FK's 88, profiles/r06/fk/.)  LDS = the tile image | per-joint {axis, lower, upper}
-//
-// The joint rotations' normalisation (round 6).  q = {e_ax sin, cos} from a correctly rounded sin / cos pair has
-// |q|^2 = RN(RN(s s) + RN(c c)) within a few f32 codes of 1.0f, so sqrt_clamp_rcp's (n, 1/n) come from a table of
-// the 2K + 1 codes around 1.0f, filled by each wave with sqrt_clamp_rcp_exact itself (its loads are in flight by
-// then): a lookup returns exactly that function's values.
-constexpr int kUnitTabK = 16;
-struct UnitEnt {
-    double r;
-    float n, pad;
-};
-RTG_DEV void unit_tab_fill(UnitEnt *tab)
-{
-    const int l = (int)threadIdx.x;
-    if (l <= 2 * kUnitTabK) {
-        const NormRcp e = sqrt_clamp_rcp_exact(__int_as_float(0x3F800000 - kUnitTabK + l), 1e-9f);
-        tab[l] = UnitEnt{e.r.r, e.n, 0.0f};
-    }
-}
 // qfrom_angle_unit_axis(angle, e_ax) for N joints, element by element the same values: qnormalize's sign flip f
 // (on cos), its |q|^2 in any component order (the zero components add +0 exactly), (n, 1/n) from the table, the two
 // nonzero components' products by 1/n, and the zero components keep the sign of f sin (0 sin, times f, times 1/n > 0).
@@ -423,9 +463,9 @@ RTG_DEV void joint_rot_n(const float (&angle)[N], const int (&ax)[N], const Unit
         const float f = 1.0f - 2.0f * (t[i].c < 0.0f ? 1.0f : 0.0f);
         const float s = f * t[i].s, c = f * t[i].c;
         const float n2 = s * s + c * c;
-        const uint32_t idx = (uint32_t)(__float_as_int(n2) - (0x3F800000 - kUnitTabK));
-        const bool in = idx <= 2u * kUnitTabK;
-        const double r = tab[in ? idx : 0u].r;
+        uint32_t idx;
+        const bool in = unit_tab_index(n2, idx);
+        const double r = tab[idx].r;
         const double ps = (double)s * r, pc = (double)c * r;
         const float qs = (float)ps, z = __builtin_copysignf(0.0f, s);
         out[i] = Q{ax[i] == 0 ? qs : z, ax[i] == 1 ? qs : z, ax[i] == 2 ? qs : z, (float)pc};
@@ -442,7 +482,7 @@ RTG_DEV void joint_rot_n(const float (&angle)[N], const int (&ax)[N], const Unit
 }
 __host__ __device__ inline size_t dof_group_lds_floats(int J, int F, int steps)
 {
-    return group_lds_floats(J, F, steps) + (size_t)J * 4 + (RTG_DOF_UNIT_TAB ? 4 * (2 * kUnitTabK + 1) : 0);
+    return group_lds_floats(J, F, steps) + (size_t)J * 4;
 }
 template <bool CLIP, int F>
 __global__ __launch_bounds__(64, 4) void k_dof_fk_group(TopoView T, DofView D, const float *__restrict__ dof,
@@ -471,8 +511,8 @@ __global__ __launch_bounds__(64, 4) void k_dof_fk_group(TopoView T, DofView D, c
     const f4v rr = reinterpret_cast<const f4v *>(root_rot)[f0 + (lane < nfr ? lane : 0)];
     const float rt = root_t[f0 * 3 + (lane < 3 * nfr ? lane : 0)];
     group_sched_fill(T, G::L, sch);
-    UnitEnt *utab = reinterpret_cast<UnitEnt *>(ntab + J);
-    if (RTG_DOF_UNIT_TAB) unit_tab_fill(utab);
+    UnitEnt *utab = reinterpret_cast<UnitEnt *>(fk_lds + group_core_floats(J, F, T.gsteps));
+    if (kUnitTab) unit_tab_fill(utab);
     for (int j = 1 + lane; j < J; j += 64) {
         const int ax = ld_const(D.axis + (j - 1));
         ntab[j] = f4v{__int_as_float(ax), CLIP ? ld_const(D.lower + (j - 1)) : 0.0f,
@@ -529,7 +569,7 @@ __global__ __launch_bounds__(64, 4) void k_dof_fk_group(TopoView T, DofView D, c
 #pragma unroll
     for (int k = NFULL; k < G::NR; ++k) rotations(std::integral_constant<int, 1>{}, k);
     wave_sync();
-    group_compose<F>(T, rot, pos, sch, nfr, [&](int, Q lq, const GEnt &, int) { return lq; });
+    group_compose<F>(T, rot, pos, sch, nfr, utab, [&](int, Q lq, const GEnt &, int) { return lq; });
     group_store<F>(rot, pos, nrec, g_rot + f0 * J * 4, g_pos + f0 * J * 3);
 }
 

@@ -101,6 +101,9 @@
 #ifndef RTG_DOF_NWAY
 #define RTG_DOF_NWAY 4   // HuForwardModel lane groups: joint rotations per N-way group (one rare-case branch each)
 #endif
+#ifndef RTG_FK_UNIT_TAB
+#define RTG_FK_UNIT_TAB 1   // lane-group FK / inverse FK / HuForwardModel compose: qmul_norm through the near-1.0f table
+#endif
 #ifndef RTG_DOF_UNIT_TAB
 #define RTG_DOF_UNIT_TAB 1   // HuForwardModel: joint rotations normalised through the near-1.0f (n, 1/n) table
 #endif
