@@ -144,52 +144,16 @@ RTG_DEV void st_out(f4v *p, f4v v)
     else *p = v;
 }
 
-// ----------------------------------------------------------------------------
-// Near-unit normalisation (round 6).  Every quaternion these kernels normalise is a product of unit quaternions
-// (FK's compose, inverse FK) or {e_ax sin, cos} from a correctly rounded pair (HuForwardModel's joints), so its
-// |q|^2 lands within a few f32 codes of 1.0f.  sqrt_clamp_rcp's (n, 1/n) for the 2K + 1 codes around 1.0f are a
-// table, filled by each wave with sqrt_clamp_rcp_exact itself while its loads are in flight: a lookup returns exactly
-// that function's values, and a |q|^2 outside it (a non-unit root rotation or input row) takes qnormalize itself.
-constexpr int kUnitTabK = 16;
-struct UnitEnt {
-    double r;
-    float n, pad;
-};
+// the near-unit normalisation table (rtg_math.cuh) in the lane-group tiles' LDS, when any of them uses it
 constexpr bool kUnitTab = RTG_FK_UNIT_TAB || RTG_DOF_UNIT_TAB;
 constexpr size_t kUnitTabFloats = kUnitTab ? 4 * (2 * kUnitTabK + 1) : 0;
-RTG_DEV void unit_tab_fill(UnitEnt *tab)
+RTG_DEV Q qmul_norm_tab(Q a, Q b, const UnitEnt *tab)
 {
-    const int l = (int)threadIdx.x;
-    if (l <= 2 * kUnitTabK) {
-        const NormRcp e = sqrt_clamp_rcp_exact(__int_as_float(0x3F800000 - kUnitTabK + l), 1e-9f);
-        tab[l] = UnitEnt{e.r.r, e.n, 0.0f};
-    }
+    if (!RTG_FK_UNIT_TAB) return qmul_norm(a, b);
+    Q q[1] = {qmul(a, b)}, o[1];
+    qnormalize_tab_n<1>(q, tab, o);
+    return o[0];
 }
-RTG_DEV bool unit_tab_index(float s, uint32_t &idx)
-{
-    idx = (uint32_t)(__float_as_int(s) - (0x3F800000 - kUnitTabK));
-    const bool in = idx <= 2u * kUnitTabK;
-    idx = in ? idx : 0u;
-    return in;
-}
-// qnormalize (quat_unit(quat_pos(q))) with the table: the same sign flip, sum, products and subnormal test
-RTG_DEV Q qnormalize_tab(Q q0, const UnitEnt *tab)
-{
-    if (!RTG_FK_UNIT_TAB) return qnormalize(q0);
-    const float f = 1.0f - 2.0f * (q0.w < 0.0f ? 1.0f : 0.0f);
-    const Q q{f * q0.x, f * q0.y, f * q0.z, f * q0.w};
-    uint32_t idx;
-    const bool in = unit_tab_index(((q.x * q.x + q.y * q.y) + q.z * q.z) + q.w * q.w, idx);
-    const double r = tab[idx].r;
-    const double p[4] = {(double)q.x * r, (double)q.y * r, (double)q.z * r, (double)q.w * r};
-    bool sub = false;
-#pragma unroll
-    for (int i = 0; i < 4; ++i) sub |= (__builtin_fabs(p[i]) < 0x1p-126) & (p[i] != 0.0);
-    Q out{(float)p[0], (float)p[1], (float)p[2], (float)p[3]};
-    if (__builtin_expect(!in | sub, 0)) out = qnormalize(q0);
-    return out;
-}
-RTG_DEV Q qmul_norm_tab(Q a, Q b, const UnitEnt *tab) { return qnormalize_tab(qmul(a, b), tab); }
 
 // ----------------------------------------------------------------------------
 // Lane-group kinematics (round 6): a frame's joints spread over a GROUP of lanes, F frames per wave (F = 16: four
@@ -348,7 +312,7 @@ RTG_DEV void fk_group_tile(const TopoView &T, const float *__restrict__ local_ro
     const float r = root_t[f0 * 3 + (lane < 3 * nfr ? lane : 0)];
     group_sched_fill(T, Grp<F>::L, sch);
     UnitEnt *utab = reinterpret_cast<UnitEnt *>(lds + group_core_floats(J, F, T.gsteps));
-    if (RTG_FK_UNIT_TAB) unit_tab_fill(utab);
+    if (RTG_FK_UNIT_TAB) unit_tab_fill(utab, (int)threadIdx.x);
     rows.to_lds(rot, nrec);
     if (lane < 3 * nfr) {
         const int fr = lane / 3;
@@ -394,7 +358,7 @@ RTG_DEV void lrot_group_tile(const TopoView &T, const float *__restrict__ g_rot,
         v[k] = src[rec < nrec ? rec : 0];
     }
     UnitEnt *utab = reinterpret_cast<UnitEnt *>(lds + lrot_core_floats(J, F));
-    if (RTG_FK_UNIT_TAB) unit_tab_fill(utab);
+    if (RTG_FK_UNIT_TAB) unit_tab_fill(utab, (int)threadIdx.x);
     for (int j = lane; j < J; j += 64) {
         par[j] = ld_const(T.parents + j);
         if (STATE) {   // skeleton3d.py:470-478: quat_normalize(quat_conjugate(tree quat)), once per joint
@@ -512,7 +476,7 @@ __global__ __launch_bounds__(64, 4) void k_dof_fk_group(TopoView T, DofView D, c
     const float rt = root_t[f0 * 3 + (lane < 3 * nfr ? lane : 0)];
     group_sched_fill(T, G::L, sch);
     UnitEnt *utab = reinterpret_cast<UnitEnt *>(fk_lds + group_core_floats(J, F, T.gsteps));
-    if (kUnitTab) unit_tab_fill(utab);
+    if (kUnitTab) unit_tab_fill(utab, (int)threadIdx.x);
     for (int j = 1 + lane; j < J; j += 64) {
         const int ax = ld_const(D.axis + (j - 1));
         ntab[j] = f4v{__int_as_float(ax), CLIP ? ld_const(D.lower + (j - 1)) : 0.0f,

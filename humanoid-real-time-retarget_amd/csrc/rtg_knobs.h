@@ -107,6 +107,9 @@
 #ifndef RTG_DOF_UNIT_TAB
 #define RTG_DOF_UNIT_TAB 1   // HuForwardModel: joint rotations normalised through the near-1.0f (n, 1/n) table
 #endif
+#ifndef RTG_VEL_UNIT_TAB
+#define RTG_VEL_UNIT_TAB 1   // angular velocity: the quaternion product's normalisation through the near-1.0f table
+#endif
 #ifndef RTG_VEL_ANG_NB
 #define RTG_VEL_ANG_NB 2   // angular velocity tile: raw elements per thread per load batch (1-4 measured alike, ~110 us)
 #endif

@@ -580,6 +580,59 @@ RTG_DEV void qfrom_angle_unit_axis_n(const float (&angle)[N], const V (&axis)[N]
     qnormalize_n<N>(q, out);
 }
 
+// ------------------------------------------------ near-unit normalisation (round 6)
+// Most quaternions the kinematics normalise are products of unit quaternions, or {e_ax sin, cos} from a correctly
+// rounded pair: |q|^2 lands within a few f32 codes of 1.0f.  sqrt_clamp_rcp's (n, 1/n) for the 2K + 1 codes around
+// 1.0f are a table, filled by the kernel with sqrt_clamp_rcp_exact itself (unit_tab_fill: one code per lane, while
+// its loads are in flight), so a lookup returns exactly that function's values; a |q|^2 outside the table (a
+// non-unit input row, NaN) takes the ordinary path.
+constexpr int kUnitTabK = 16;
+struct UnitEnt {
+    double r;
+    float n, pad;
+};
+RTG_DEV void unit_tab_fill(UnitEnt *tab, int t)   // t: the filling thread's index (2K + 1 of them fill)
+{
+    if (t <= 2 * kUnitTabK) {
+        const NormRcp e = sqrt_clamp_rcp_exact(__int_as_float(0x3F800000 - kUnitTabK + t), 1e-9f);
+        tab[t] = UnitEnt{e.r.r, e.n, 0.0f};
+    }
+}
+RTG_DEV bool unit_tab_index(float s, uint32_t &idx)
+{
+    idx = (uint32_t)(__float_as_int(s) - (0x3F800000 - kUnitTabK));
+    const bool in = idx <= 2u * kUnitTabK;
+    idx = in ? idx : 0u;
+    return in;
+}
+// qnormalize for N quaternions through the table: the same sign flip, sum, products and subnormal test, element by
+// element; the ones off the table (or with a subnormal product) take qnormalize, one rare-case branch per group
+template <int N>
+RTG_DEV void qnormalize_tab_n(const Q (&q0)[N], const UnitEnt *tab, Q (&out)[N])
+{
+    bool ok[N], all = true;
+#pragma unroll
+    for (int i = 0; i < N; ++i) {
+        const float f = 1.0f - 2.0f * (q0[i].w < 0.0f ? 1.0f : 0.0f);
+        const Q q{f * q0[i].x, f * q0[i].y, f * q0[i].z, f * q0[i].w};
+        uint32_t idx;
+        const bool in = unit_tab_index(((q.x * q.x + q.y * q.y) + q.z * q.z) + q.w * q.w, idx);
+        const double r = tab[idx].r;
+        const double p[4] = {(double)q.x * r, (double)q.y * r, (double)q.z * r, (double)q.w * r};
+        bool sub = false;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) sub |= (__builtin_fabs(p[k]) < 0x1p-126) & (p[k] != 0.0);
+        out[i] = Q{(float)p[0], (float)p[1], (float)p[2], (float)p[3]};
+        ok[i] = in & !sub;
+        all &= ok[i];
+    }
+    if (__builtin_expect(!all, 0)) {
+#pragma unroll
+        for (int i = 0; i < N; ++i)
+            if (!ok[i]) out[i] = qnormalize(q0[i]);
+    }
+}
+
 RTG_DEV Q qfrom_rotmat(const float m[9])  // :146-193 (the four overlapping branches, in order)
 {
     const float d0 = m[0], d1 = m[4], d2 = m[8];
