@@ -150,9 +150,7 @@ constexpr size_t kUnitTabFloats = kUnitTab ? 4 * (2 * kUnitTabK + 1) : 0;
 RTG_DEV Q qmul_norm_tab(Q a, Q b, const UnitEnt *tab)
 {
     if (!RTG_FK_UNIT_TAB) return qmul_norm(a, b);
-    Q q[1] = {qmul(a, b)}, o[1];
-    qnormalize_tab_n<1>(q, tab, o);
-    return o[0];
+    return qnormalize_t(qmul(a, b), tab);
 }
 
 // ----------------------------------------------------------------------------

@@ -101,6 +101,12 @@
 #ifndef RTG_DOF_NWAY
 #define RTG_DOF_NWAY 4   // HuForwardModel lane groups: joint rotations per N-way group (one rare-case branch each)
 #endif
+#ifndef RTG_SIDES_UNIT_TAB
+#define RTG_SIDES_UNIT_TAB 7   // k_solve_sides FULL_BODY_POS, SoA: near-1.0f table normalisation at (1 fits | 2 arm maps | 4 Euler split)
+#endif
+#ifndef RTG_SIDES_UNIT_TAB_AOS
+#define RTG_SIDES_UNIT_TAB_AOS 1   // the same for AoS: the fits only (the arm maps push it to 138-141 VGPRs, 3 waves/SIMD)
+#endif
 #ifndef RTG_FK_UNIT_TAB
 #define RTG_FK_UNIT_TAB 1   // lane-group FK / inverse FK / HuForwardModel compose: qmul_norm through the near-1.0f table
 #endif

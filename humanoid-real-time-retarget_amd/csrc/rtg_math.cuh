@@ -566,20 +566,6 @@ RTG_DEV void qnormalize_n(const Q (&q0)[N], Q (&out)[N])   // qnormalize
     sqrt_clamp_rcp_n<N>(s, 1e-9f, r);
     mulr_q_n<N>(q, r, out);
 }
-template <int N>
-RTG_DEV void qfrom_angle_unit_axis_n(const float (&angle)[N], const V (&axis)[N], Q (&out)[N])
-{
-    double th[N];
-#pragma unroll
-    for (int i = 0; i < N; ++i) th[i] = (double)(angle[i] / 2.0f);
-    SC t[N];
-    cr_sincos_n<N>(th, t);
-    Q q[N];
-#pragma unroll
-    for (int i = 0; i < N; ++i) q[i] = Q{axis[i].x * t[i].s, axis[i].y * t[i].s, axis[i].z * t[i].s, t[i].c};
-    qnormalize_n<N>(q, out);
-}
-
 // ------------------------------------------------ near-unit normalisation (round 6)
 // Most quaternions the kinematics normalise are products of unit quaternions, or {e_ax sin, cos} from a correctly
 // rounded pair: |q|^2 lands within a few f32 codes of 1.0f.  sqrt_clamp_rcp's (n, 1/n) for the 2K + 1 codes around
@@ -632,8 +618,43 @@ RTG_DEV void qnormalize_tab_n(const Q (&q0)[N], const UnitEnt *tab, Q (&out)[N])
             if (!ok[i]) out[i] = qnormalize(q0[i]);
     }
 }
+// compile-time choice of the normalisation: NoTab = qnormalize itself, a table pointer = the table
+struct NoTab {};
+template <int N>
+RTG_DEV void qnormalize_n_t(const Q (&q)[N], Q (&out)[N], NoTab) { qnormalize_n<N>(q, out); }
+template <int N>
+RTG_DEV void qnormalize_n_t(const Q (&q)[N], Q (&out)[N], const UnitEnt *tab) { qnormalize_tab_n<N>(q, tab, out); }
+RTG_DEV Q qnormalize_t(Q q, NoTab) { return qnormalize(q); }
+template <bool ON> struct TabSel {   // a table pointer where ON, NoTab elsewhere
+    static RTG_DEV const UnitEnt *get(const UnitEnt *t) { return t; }
+};
+template <> struct TabSel<false> {
+    static RTG_DEV NoTab get(const UnitEnt *) { return NoTab{}; }
+};
+RTG_DEV Q qnormalize_t(Q q, const UnitEnt *tab)
+{
+    const Q a[1] = {q};
+    Q o[1];
+    qnormalize_tab_n<1>(a, tab, o);
+    return o[0];
+}
 
-RTG_DEV Q qfrom_rotmat(const float m[9])  // :146-193 (the four overlapping branches, in order)
+template <int N, typename Tab = NoTab>
+RTG_DEV void qfrom_angle_unit_axis_n(const float (&angle)[N], const V (&axis)[N], Q (&out)[N], Tab tab = Tab{})
+{
+    double th[N];
+#pragma unroll
+    for (int i = 0; i < N; ++i) th[i] = (double)(angle[i] / 2.0f);
+    SC t[N];
+    cr_sincos_n<N>(th, t);
+    Q q[N];
+#pragma unroll
+    for (int i = 0; i < N; ++i) q[i] = Q{axis[i].x * t[i].s, axis[i].y * t[i].s, axis[i].z * t[i].s, t[i].c};
+    qnormalize_n_t<N>(q, out, tab);
+}
+
+template <typename Tab = NoTab>
+RTG_DEV Q qfrom_rotmat(const float m[9], Tab tab = Tab{})  // :146-193 (the four overlapping branches, in order)
 {
     const float d0 = m[0], d1 = m[4], d2 = m[8];
     float w = cr_sqrt(clamp_lo((((d0 + d1) + d2) + 1.0f) / 4.0f, 0.0f));
@@ -660,7 +681,7 @@ RTG_DEV Q qfrom_rotmat(const float m[9])  // :146-193 (the four overlapping bran
         x *= tsign(m[6] + m[2]);
         y *= tsign(m[7] + m[5]);
     }
-    return qnormalize(Q{x, y, z, w});
+    return qnormalize_t(Q{x, y, z, w}, tab);
 }
 
 // quat_to_angle_axis + angle_axis_to_exp_map (:587-627), returns the 3 exp-map components
@@ -1422,8 +1443,8 @@ RTG_DEV void kabsch_rot(const float A[9], float R[9], const Hook &hook = Hook{})
 // `svd_nan` is set when A has a NaN entry: torch.linalg.svd refuses such a matrix (LAPACK sgesdd returns info = -4
 // on a NaN norm and torch raises "linalg.svd: ... contained non-finite values", transform3d.py:40), so the reference
 // frame raises there (an inf entry alone does not raise).
-template <int N, typename Hook = NoHook>
-RTG_DEV Q cal_joint_quat(const V (&Z)[N], const V (&M)[N], bool &svd_nan, const Hook &hook = Hook{})
+template <int N, typename Hook = NoHook, typename Tab = NoTab>
+RTG_DEV Q cal_joint_quat(const V (&Z)[N], const V (&M)[N], bool &svd_nan, const Hook &hook = Hook{}, Tab tab = Tab{})
 {
     float A[9];
 #pragma unroll
@@ -1448,7 +1469,7 @@ RTG_DEV Q cal_joint_quat(const V (&Z)[N], const V (&M)[N], bool &svd_nan, const 
     float R[9];
     kabsch_rot(A, R, hook);
     hook(1);
-    return qfrom_rotmat(R);
+    return qfrom_rotmat(R, tab);
 }
 template <int N, typename Hook = NoHook>
 RTG_DEV Q cal_joint_quat(const V (&Z)[N], const V (&M)[N], const Hook &hook = Hook{})
@@ -1663,9 +1684,9 @@ RTG_DEV float radians_between(V v1, V v2, V n)  // :77-100
 
 // shoulder_pr (SHOULDER) / elbow_py of NA arms at once, on the N-way leaf math: per arm the same operations on the
 // same operands as the scalar forms above (vunit(v1p) serves both angles, as CSE made it there), so the same bits
-template <bool SHOULDER, int NA>
+template <bool SHOULDER, int NA, typename Tab = NoTab>
 RTG_DEV void arm_pair_n(const V (&v1)[NA], const ArmZero (&z0)[NA], const Q (&parent)[NA], Q (&first)[NA],
-                        Q (&second)[NA])
+                        Q (&second)[NA], Tab tab = Tab{})
 {
     const V ex{1.f, 0.f, 0.f}, ey{0.f, 1.f, 0.f}, ez{0.f, 0.f, 1.f};
     const V pn = SHOULDER ? ey : ez;   // the plane of the first angle
@@ -1698,7 +1719,7 @@ RTG_DEV void arm_pair_n(const V (&v1)[NA], const ArmZero (&z0)[NA], const Q (&pa
         ax[2 * a + 1] = SHOULDER ? ex : ey;
     }
     Q q[2 * NA];
-    qfrom_angle_unit_axis_n<2 * NA>(ang, ax, q);
+    qfrom_angle_unit_axis_n<2 * NA>(ang, ax, q, tab);
 #pragma unroll
     for (int a = 0; a < NA; ++a) {
         first[a] = q[2 * a];

@@ -278,12 +278,12 @@ constexpr int kSideThreads = 128 * kSideTiles;
 constexpr int kSideFrames = 64 * kSideTiles;       // frames per block
 
 // torso fit R10 (full_body_pos_retargeter.py:69-70 / retarget_solver.py:49-50)
-template <typename View, typename Hook = NoHook>
-RTG_DEV Q fbp_torso(const SolverConsts &C, const View &b, bool &svd_nan, const Hook &hook = Hook{})
+template <typename View, typename Hook = NoHook, typename Tab = NoTab>
+RTG_DEV Q fbp_torso(const SolverConsts &C, const View &b, bool &svd_nan, const Hook &hook = Hook{}, Tab tab = Tab{})
 {
     const V b10 = b.p3(10);
     const V Mt[3] = {vsub(b.p3(17), b10), vsub(b.p3(13), b10), vsub(b.p3(11), b10)};
-    return cal_joint_quat<3>(C.Zt, Mt, svd_nan, hook);
+    return cal_joint_quat<3>(C.Zt, Mt, svd_nan, hook, tab);
 }
 RTG_DEV Q upper_pt_sign(V v) { return Q{v.x * -1.0f, v.y * -1.0f, v.z * 1.0f, 0.0f}; }   // coord_transform :41
 template <typename View>
@@ -298,12 +298,12 @@ RTG_DEV Q upper_torso(const SolverConsts &C, const View &x, bool &svd_nan)
     return cal_joint_quat<3>(C.Zt, Mt, svd_nan);
 }
 // wrist fit W (full_body_pos_retargeter.py:137-140 left, :160-163 right)
-template <int SIDE, typename View, typename Hook = NoHook>
-RTG_DEV Q fbp_wrist_fit(const SolverConsts &C, const View &H, bool &svd_nan, const Hook &hook = Hook{})
+template <int SIDE, typename View, typename Hook = NoHook, typename Tab = NoTab>
+RTG_DEV Q fbp_wrist_fit(const SolverConsts &C, const View &H, bool &svd_nan, const Hook &hook = Hook{}, Tab tab = Tab{})
 {
     const V h0 = H.p3(0);
     const V M[5] = {vsub(H.p3(2), h0), vsub(H.p3(6), h0), vsub(H.p3(10), h0), vsub(H.p3(14), h0), vsub(H.p3(17), h0)};
-    return cal_joint_quat<5>(SIDE ? C.Zr : C.Zl, M, svd_nan, hook);
+    return cal_joint_quat<5>(SIDE ? C.Zr : C.Zl, M, svd_nan, hook, tab);
 }
 
 // A side's body points (shoulder, elbow, wrist), loaded at kernel start with the torso / wrist-fit loads of the
@@ -330,21 +330,22 @@ RTG_DEV Q fbp_arm(const SolverConsts &C, const ArmPts &ap, Q R10, const Emit &E)
 }
 // Both arms' chains at once (round 6): solve_arm for the left and the right arm on the N-way leaf math, so the two
 // independent chains interleave in one instruction stream (the same values: arm_pair_n).  Returns the chains.
+template <typename Tab = NoTab>
 RTG_DEV void fbp_arms2(const SolverConsts &C, const ArmPts &apL, const ArmPts &apR, Q R10, const Emit &E, Q &chL,
-                       Q &chR)
+                       Q &chR, Tab tab = Tab{})
 {
     const V up[2] = {vsub(apL.el, apL.sh), vsub(apR.el, apR.sh)};
     const V fo[2] = {vsub(apL.wr, apL.el), vsub(apR.wr, apR.el)};
     const ArmZero zs[2] = {C.lsh, C.rsh}, ze[2] = {C.lel, C.rel};
     const Q par[2] = {R10, R10};
     Q p[2], r[2], y[2], e[2];
-    arm_pair_n<true, 2>(up, zs, par, p, r);
+    arm_pair_n<true, 2>(up, zs, par, p, r, tab);
     E.link<12>(p[0]);
     E.link<13>(r[0]);
     E.link<21>(p[1]);
     E.link<22>(r[1]);
     const Q par2[2] = {qmul(qmul(R10, p[0]), r[0]), qmul(qmul(R10, p[1]), r[1])};
-    arm_pair_n<false, 2>(fo, ze, par2, y, e);
+    arm_pair_n<false, 2>(fo, ze, par2, y, e, tab);
     E.link<14>(y[0]);
     E.link<15>(e[0]);
     E.link<23>(y[1]);
@@ -382,12 +383,12 @@ RTG_DEV void fbp_body_rows(float *__restrict__ brow, Q R10, Q W, bool const_rows
 }
 // the Euler split of the wrist (:128-136), the gripper (:142-158 / :165-175) and the body_rot rows; true where
 // scipy refuses the wrist's local quaternion
-template <bool PRECISE, int SIDE>
+template <bool PRECISE, int SIDE, typename Tab = NoTab>
 RTG_DEV bool fbp_side_after_arm(const SolverConsts &C, const TipPts &tp, Q R10, Q chain, Q W, const Emit &E,
-                                float *__restrict__ brow)
+                                float *__restrict__ brow, Tab tab = Tab{})
 {
     constexpr int E0 = SIDE ? 25 : 16, D0 = SIDE ? 27 : 18;
-    const bool refused = emit_euler_xyz<E0>(E, qmul_norm(qconj(qmul_norm(R10, chain)), W));
+    const bool refused = emit_euler_xyz<E0>(E, qnormalize_t(qmul(qconj(qnormalize_t(qmul(R10, chain), tab)), W), tab));
     fbp_gripper<PRECISE>(C, hand_x_mean(qconj(W), tp.h0, tp.t), E.row + D0);
     if (brow) fbp_body_rows<SIDE>(brow, R10, W);
     return refused;
@@ -532,6 +533,14 @@ __global__ __launch_bounds__(kSideThreads, RTG_SIDES_WAVES) void k_solve_sides(S
         // waves out, and the second one to finish stores the tile's DOF rows while the first exits.
         __shared__ int sflag[kSideTiles][4];   // per tile: [0] R10 ready, [1] left chain ready, [2] waves done, [3] right chain ready
         if (threadIdx.x < 4 * kSideTiles) (&sflag[0][0])[threadIdx.x] = 0;
+        // the near-unit normalisation table (rtg_math.cuh), per site: 1 the fits' quaternions, 2 the arm maps'
+        // angle-axis quaternions, 4 the Euler split's products (RTG_SIDES_UNIT_TAB for SoA, _AOS for AoS)
+        constexpr int kTab = SOA ? RTG_SIDES_UNIT_TAB : RTG_SIDES_UNIT_TAB_AOS;
+        __shared__ UnitEnt sut[2 * kUnitTabK + 1];
+        if constexpr (kTab != 0) unit_tab_fill(sut, (int)threadIdx.x);
+        const auto tabF = TabSel<(kTab & 1) != 0>::get(sut);
+        const auto tabA = TabSel<(kTab & 2) != 0>::get(sut);
+        const auto tabE = TabSel<(kTab & 4) != 0>::get(sut);
         __syncthreads();
         int *const fl = sflag[w >> 1];
         auto hook1 = [&](int k) { if (k < 2) TS(1 + k); };    // 1: first fit's A formed (its points loaded), 2: its SVD + R done
@@ -547,14 +556,14 @@ __global__ __launch_bounds__(kSideThreads, RTG_SIDES_WAVES) void k_solve_sides(S
         if (live) {
             bool nan = false;
             if (!side) {
-                R10 = fbp_torso(C, b, nan, hook1);
+                R10 = fbp_torso(C, b, nan, hook1, tabF);
                 storso[r] = make_float4(R10.x, R10.y, R10.z, R10.w);
                 fit1_nan = nan;
             } else {
                 apL = load_arm<0>(b);
                 apR = load_arm<1>(b);
                 if (kPreTips) tpre = load_tips(view(in2, 60));
-                W = fbp_wrist_fit<1>(C, view(in2, 60), nan, hook1);
+                W = fbp_wrist_fit<1>(C, view(in2, 60), nan, hook1, tabF);
                 fit1_nan = nan;
             }
         }
@@ -575,7 +584,7 @@ __global__ __launch_bounds__(kSideThreads, RTG_SIDES_WAVES) void k_solve_sides(S
                 const float4 t = storso[r];   // read R10 before the same lane overwrites the slot with the chain
                 R10 = Q{t.x, t.y, t.z, t.w};
                 Q cl;
-                fbp_arms2(C, apL, apR, R10, E, cl, chain);
+                fbp_arms2(C, apL, apR, R10, E, cl, chain, tabA);
                 storso[r] = make_float4(cl.x, cl.y, cl.z, cl.w);
             }
             if (wds) Emit::wait_words();   // the left chain's table words (slots 0-3) have landed in LDS
@@ -596,7 +605,7 @@ __global__ __launch_bounds__(kSideThreads, RTG_SIDES_WAVES) void k_solve_sides(S
             emit_fixed_links(E);
             bool nan = false;
             if (kPreTips) tpre = load_tips(view(in1, 60));
-            W = fbp_wrist_fit<0>(C, view(in1, 60), nan, hook2);
+            W = fbp_wrist_fit<0>(C, view(in1, 60), nan, hook2, tabF);
             fit2_nan = nan;
         }
         TS(5);
@@ -606,10 +615,10 @@ __global__ __launch_bounds__(kSideThreads, RTG_SIDES_WAVES) void k_solve_sides(S
             float *brow = body_rot ? body_rot + f * 236 : nullptr;
             const TipPts tp = kPreTips ? tpre : load_tips(view(side ? in2 : in1, 60));
             if (side) {
-                euler_refused = fbp_side_after_arm<PRECISE, 1>(C, tp, R10, chain, W, E, brow);
+                euler_refused = fbp_side_after_arm<PRECISE, 1>(C, tp, R10, chain, W, E, brow, tabE);
             } else {
                 const float4 c = storso[r];
-                euler_refused = fbp_side_after_arm<PRECISE, 0>(C, tp, R10, Q{c.x, c.y, c.z, c.w}, W, E, brow);
+                euler_refused = fbp_side_after_arm<PRECISE, 0>(C, tp, R10, Q{c.x, c.y, c.z, c.w}, W, E, brow, tabE);
             }
         }
         TS(7);
