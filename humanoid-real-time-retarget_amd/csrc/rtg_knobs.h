@@ -107,6 +107,14 @@
 #ifndef RTG_SIDES_UNIT_TAB_AOS
 #define RTG_SIDES_UNIT_TAB_AOS 1   // the same for AoS: the fits only (the arm maps push it to 138-141 VGPRs, 3 waves/SIMD)
 #endif
+#ifndef RTG_FRAME1_UNIT_TAB
+#define RTG_FRAME1_UNIT_TAB 6   // k_fbp_frame1 / k_frame_server (B = 1): the near-1.0f table at (1 fits | 6 arm maps + Euler
+                                // split); 6: 12.65-12.80 vs 12.88-13.10 us (profiles/r06/unit_tab/latency/)
+#endif
+#ifndef RTG_LAT_UNIT_TAB
+#define RTG_LAT_UNIT_TAB 0   // A/B knob (same values), k_fbp_quad / k_fbp_latency5: the near-1.0f table at (1 fits | 6 arm maps + Euler split);
+                             // all sites: B = 1 12.7-13.0 vs 12.9-13.2 us, config 2 17.2 vs 16.8 us (slower), profiles/r06/unit_tab/
+#endif
 #ifndef RTG_FK_UNIT_TAB
 #define RTG_FK_UNIT_TAB 1   // lane-group FK / inverse FK / HuForwardModel compose: qmul_norm through the near-1.0f table
 #endif

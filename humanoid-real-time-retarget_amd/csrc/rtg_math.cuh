@@ -577,9 +577,9 @@ struct UnitEnt {
     double r;
     float n, pad;
 };
-RTG_DEV void unit_tab_fill(UnitEnt *tab, int t)   // t: the filling thread's index (2K + 1 of them fill)
+RTG_DEV void unit_tab_fill(UnitEnt *tab, int t)   // t: the filling thread's index (t = 0 .. 2K fill)
 {
-    if (t <= 2 * kUnitTabK) {
+    if ((unsigned)t <= 2u * kUnitTabK) {
         const NormRcp e = sqrt_clamp_rcp_exact(__int_as_float(0x3F800000 - kUnitTabK + t), 1e-9f);
         tab[t] = UnitEnt{e.r.r, e.n, 0.0f};
     }
@@ -625,6 +625,13 @@ RTG_DEV void qnormalize_n_t(const Q (&q)[N], Q (&out)[N], NoTab) { qnormalize_n<
 template <int N>
 RTG_DEV void qnormalize_n_t(const Q (&q)[N], Q (&out)[N], const UnitEnt *tab) { qnormalize_tab_n<N>(q, tab, out); }
 RTG_DEV Q qnormalize_t(Q q, NoTab) { return qnormalize(q); }
+template <typename Tab>
+RTG_DEV Q qfrom_angle_unit_axis_t(float angle, V axis, Tab tab)   // qfrom_angle_unit_axis, normalised per Tab
+{
+    const float theta = angle / 2.0f;
+    const SC t = cr_sincos((double)theta);
+    return qnormalize_t(Q{axis.x * t.s, axis.y * t.s, axis.z * t.s, t.c}, tab);
+}
 template <bool ON> struct TabSel {   // a table pointer where ON, NoTab elsewhere
     static RTG_DEV const UnitEnt *get(const UnitEnt *t) { return t; }
 };

@@ -152,8 +152,8 @@ RTG_DEV void report_device_error(uint32_t *err, uint32_t code)
 // returns quat_mul_four of the four link rotations (the wrist parent chain, :128-136)
 // (round 6: on arm_pair_n, the two angles of each map in one instruction stream with shared rare-case branches; the
 // same values as shoulder_pr / elbow_py)
-template <int L0>
-RTG_DEV Q solve_arm(const Emit &E, V upper, V fore, ArmZero zs, ArmZero ze, Q parent)
+template <int L0, typename Tab = NoTab>
+RTG_DEV Q solve_arm(const Emit &E, V upper, V fore, ArmZero zs, ArmZero ze, Q parent, Tab tab = Tab{})
 {
     Q p, r, y, e;
     {
@@ -161,7 +161,7 @@ RTG_DEV Q solve_arm(const Emit &E, V upper, V fore, ArmZero zs, ArmZero ze, Q pa
         const ArmZero z[1] = {zs};
         const Q par[1] = {parent};
         Q a[1], b[1];
-        arm_pair_n<true, 1>(v, z, par, a, b);
+        arm_pair_n<true, 1>(v, z, par, a, b, tab);
         p = a[0];
         r = b[0];
     }
@@ -172,7 +172,7 @@ RTG_DEV Q solve_arm(const Emit &E, V upper, V fore, ArmZero zs, ArmZero ze, Q pa
         const ArmZero z[1] = {ze};
         const Q par[1] = {qmul(qmul(parent, p), r)};
         Q a[1], b[1];
-        arm_pair_n<false, 1>(v, z, par, a, b);
+        arm_pair_n<false, 1>(v, z, par, a, b, tab);
         y = a[0];
         e = b[0];
     }
@@ -749,10 +749,14 @@ RTG_DEV void fbp_latency5_tile(const SolverConsts &C, const float *__restrict__ 
     __shared__ float2 sst[14 * kLatFrames];
     __shared__ int sflag[3];                   // R10 ready, left arm ready, right arm ready
     __shared__ uint8_t sstat[3][kLatFrames];   // status bits of the torso wave and the two wrist waves
+    __shared__ UnitEnt sut[2 * kUnitTabK + 1];   // the near-unit normalisation table (RTG_LAT_UNIT_TAB)
     const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int64_t f = f0 + lane;
     const bool live = f < B;
     if (threadIdx.x < 3) sflag[threadIdx.x] = 0;
+    if (RTG_LAT_UNIT_TAB) unit_tab_fill(sut, (int)threadIdx.x - 256);   // wave 4 (the arm wave with the least to do)
+    const auto tabF = TabSel<(RTG_LAT_UNIT_TAB & 1) != 0>::get(sut);
+    const auto tab = TabSel<(RTG_LAT_UNIT_TAB & 6) != 0>::get(sut);
     __syncthreads();
 #if RTG_EXP_TIMESTAMPS
     float *const tsb = body_rot;
@@ -777,7 +781,7 @@ RTG_DEV void fbp_latency5_tile(const SolverConsts &C, const float *__restrict__ 
     if (w == 0) {
         if (live) {
             bool nan = false;
-            const Q q = fbp_torso(C, b, nan, hook);
+            const Q q = fbp_torso(C, b, nan, hook, tabF);
             sfit[lane] = make_float4(q.x, q.y, q.z, q.w);
             fit_nan = nan;
         }
@@ -796,7 +800,8 @@ RTG_DEV void fbp_latency5_tile(const SolverConsts &C, const float *__restrict__ 
             const float4 t = sfit[lane];
             const Q R10{t.x, t.y, t.z, t.w};
             const V up = vsub(ap.el, ap.sh), fo = vsub(ap.wr, ap.el);
-            const Q ch = side ? solve_arm<21>(E, up, fo, C.rsh, C.rel, R10) : solve_arm<12>(E, up, fo, C.lsh, C.lel, R10);
+            const Q ch = side ? solve_arm<21>(E, up, fo, C.rsh, C.rel, R10, tab)
+                              : solve_arm<12>(E, up, fo, C.lsh, C.lel, R10, tab);
             schain[side][lane] = make_float4(ch.x, ch.y, ch.z, ch.w);
         }
         lds_signal(&sflag[1 + side]);
@@ -810,7 +815,7 @@ RTG_DEV void fbp_latency5_tile(const SolverConsts &C, const float *__restrict__ 
         TipPts tp{};
         if (live) {
             bool nan = false;
-            W = side ? fbp_wrist_fit<1>(C, H, nan, hook) : fbp_wrist_fit<0>(C, H, nan, hook);
+            W = side ? fbp_wrist_fit<1>(C, H, nan, hook, tabF) : fbp_wrist_fit<0>(C, H, nan, hook, tabF);
             fit_nan = nan;
             tp = load_tips(H);
         }
@@ -825,7 +830,7 @@ RTG_DEV void fbp_latency5_tile(const SolverConsts &C, const float *__restrict__ 
             const Q R10{t.x, t.y, t.z, t.w}, chain{c.x, c.y, c.z, c.w};
             float *brow = body_rot ? body_rot + f * 236 : nullptr;
             fbp_gripper<PRECISE>(C, a, E.row + (side ? 27 : 18));
-            const Q loc = qmul_norm(qconj(qmul_norm(R10, chain)), W);
+            const Q loc = qnormalize_t(qmul(qconj(qnormalize_t(qmul(R10, chain), tab)), W), tab);
             euler_refused = side ? emit_euler_xyz<25>(E, loc) : emit_euler_xyz<16>(E, loc);
             if (brow) {
                 if (side) fbp_body_rows<1>(brow, R10, W);
@@ -907,8 +912,8 @@ template <int G>
 RTG_DEV int sublane() { return (int)(threadIdx.x & (G - 1)); }
 
 // shoulder_pr (SHOULDER) / elbow_py of the frame: sub-lane 0 the first angle's quaternion, sub-lane 1 the second's
-template <bool SHOULDER, int G = 64, typename Hook = NoHook>
-RTG_DEV void arm_pair_lanes(V v1, ArmZero z0, Q parent, Q &first, Q &second, const Hook &hook = Hook{})
+template <bool SHOULDER, int G = 64, typename Hook = NoHook, typename Tab = NoTab>
+RTG_DEV void arm_pair_lanes(V v1, ArmZero z0, Q parent, Q &first, Q &second, const Hook &hook = Hook{}, Tab tab = Tab{})
 {
     const int sub = sublane<G>();
     Q q = qident();
@@ -927,7 +932,7 @@ RTG_DEV void arm_pair_lanes(V v1, ArmZero z0, Q parent, Q &first, Q &second, con
         const float ang = radians_between(a, b, n);
         hook(2);
         const V ax = l0 ? pn : (SHOULDER ? ex : ey);
-        q = qfrom_angle_unit_axis(ang - (l0 ? z0.th0 : z0.ph0), ax);
+        q = qfrom_angle_unit_axis_t(ang - (l0 ? z0.th0 : z0.ph0), ax, tab);
         hook(3);
     }
     first = gbc<G, 0>(q);
@@ -940,14 +945,15 @@ RTG_DEV void link_rt(const Emit &E, int link, Q q)
     E.st[(link <= 18 ? link - 12 : link - 14) * E.sst] = make_float2(q.w, k == 0 ? q.x : (k == 1 ? q.y : q.z));
     if (E.lr) st4(E.lr + 4 * link, q);
 }
-template <int L0, int G = 64, typename Hook = NoHook>
-RTG_DEV Q solve_arm_lanes(const Emit &E, V upper, V fore, ArmZero zs, ArmZero ze, Q parent, const Hook &hook = Hook{})
+template <int L0, int G = 64, typename Hook = NoHook, typename Tab = NoTab>
+RTG_DEV Q solve_arm_lanes(const Emit &E, V upper, V fore, ArmZero zs, ArmZero ze, Q parent, const Hook &hook = Hook{},
+                          Tab tab = Tab{})
 {
     const bool w0 = sublane<G>() == 0;
     Q p, r, y, e;
-    arm_pair_lanes<true, G>(upper, zs, parent, p, r, [&](int k) { hook(k); });
+    arm_pair_lanes<true, G>(upper, zs, parent, p, r, [&](int k) { hook(k); }, tab);
     if (w0) { E.link<L0>(p); E.link<L0 + 1>(r); }
-    arm_pair_lanes<false, G>(fore, ze, qmul(qmul(parent, p), r), y, e, [&](int k) { hook(4 + k); });
+    arm_pair_lanes<false, G>(fore, ze, qmul(qmul(parent, p), r), y, e, [&](int k) { hook(4 + k); }, tab);
     if (w0) { E.link<L0 + 2>(y); E.link<L0 + 3>(e); }
     return qmul(qmul(qmul(p, r), y), e);
 }
@@ -1028,9 +1034,11 @@ RTG_DEV void finalize_lanes(const Emit &E, int s0, int n)
 // const_rows false (the frame server, once its output buffers hold them): the rows that are the same for every
 // frame -- the 17 fixed links of local_rot and the 56 identity rows of body_rot -- are not rewritten; they are still
 // in the server's own pinned output rows from an earlier frame.  Returns the frame's status bits (block-uniform).
-template <bool PRECISE>
+// tab: the near-unit normalisation table, filled and made visible by the caller (or NoTab)
+template <bool PRECISE, typename Tab = NoTab, typename TabF = NoTab>
 RTG_DEV uint32_t fbp_frame1_tile(const SolverConsts &C, const float *rows, float *__restrict__ dof,
-                                 float *__restrict__ local_rot, float *__restrict__ body_rot, bool const_rows = true)
+                                 float *__restrict__ local_rot, float *__restrict__ body_rot, bool const_rows = true,
+                                 Tab tab = Tab{}, TabF tabF = TabF{})
 {
     __shared__ float sdof[kDofStride];
     __shared__ float4 sfit, schain[2];
@@ -1068,7 +1076,7 @@ RTG_DEV uint32_t fbp_frame1_tile(const SolverConsts &C, const float *rows, float
     if (w == 0) {
         if (w0) {
             bool nan = false;
-            const Q q = fbp_torso(C, b, nan, hook);
+            const Q q = fbp_torso(C, b, nan, hook, tabF);
             sfit = make_float4(q.x, q.y, q.z, q.w);
             st = nan ? kStTorsoSvd : 0u;
         }
@@ -1088,8 +1096,8 @@ RTG_DEV uint32_t fbp_frame1_tile(const SolverConsts &C, const float *rows, float
             if (k < 4) TS(8 + k);
             else if (k == 7) TS(12);
         };
-        const Q ch = side ? solve_arm_lanes<21>(E, up, fo, C.rsh, C.rel, R10, ahook)
-                          : solve_arm_lanes<12>(E, up, fo, C.lsh, C.lel, R10, ahook);
+        const Q ch = side ? solve_arm_lanes<21>(E, up, fo, C.rsh, C.rel, R10, ahook, tab)
+                          : solve_arm_lanes<12>(E, up, fo, C.lsh, C.lel, R10, ahook, tab);
         if (w0) schain[side] = make_float4(ch.x, ch.y, ch.z, ch.w);
         lds_signal(&sflag[1 + side]);
         TS(7);
@@ -1102,7 +1110,7 @@ RTG_DEV uint32_t fbp_frame1_tile(const SolverConsts &C, const float *rows, float
         float a = 0.0f;
         if (w0) {
             bool nan = false;
-            W = side ? fbp_wrist_fit<1>(C, H, nan, hook) : fbp_wrist_fit<0>(C, H, nan, hook);
+            W = side ? fbp_wrist_fit<1>(C, H, nan, hook, tabF) : fbp_wrist_fit<0>(C, H, nan, hook, tabF);
             st = nan ? (side ? kStRightSvd : kStLeftSvd) : 0u;
             const TipPts tp = load_tips(H);
             a = hand_x_mean(qconj(W), tp.h0, tp.t);   // the gripper needs only W (:142-158 / :165-175)
@@ -1120,7 +1128,7 @@ RTG_DEV uint32_t fbp_frame1_tile(const SolverConsts &C, const float *rows, float
                 else fbp_body_rows<0>(body_rot, R10, W, const_rows);
             }
         }
-        const Q loc = qmul_norm(qconj(qmul_norm(R10, chain)), W);
+        const Q loc = qnormalize_t(qmul(qconj(qnormalize_t(qmul(R10, chain), tab)), W), tab);
         const bool refused = side ? emit_euler_xyz_lanes<25>(E, loc) : emit_euler_xyz_lanes<16>(E, loc);
         st |= refused ? (side ? kStRightEuler : kStLeftEuler) : 0u;
         TS(7);
@@ -1148,12 +1156,15 @@ __global__ __launch_bounds__(320) void k_fbp_frame1(SolverConsts C, const float 
                                                     float *__restrict__ body_rot)
 {
     __shared__ float rows[184];
+    __shared__ UnitEnt sut[2 * kUnitTabK + 1];   // the near-unit normalisation table (RTG_FRAME1_UNIT_TAB)
     if (threadIdx.x < 183) {
         const int e = threadIdx.x;
         rows[e] = e < 63 ? in0[e] : (e < 123 ? in1[e - 63] : in2[e - 123]);
     }
+    if (RTG_FRAME1_UNIT_TAB) unit_tab_fill(sut, (int)threadIdx.x - 256);   // wave 4, while the rows are in flight
     __syncthreads();
-    fbp_frame1_tile<PRECISE>(C, rows, dof, local_rot, body_rot);
+    fbp_frame1_tile<PRECISE>(C, rows, dof, local_rot, body_rot, true, TabSel<(RTG_FRAME1_UNIT_TAB & 6) != 0>::get(sut),
+                             TabSel<(RTG_FRAME1_UNIT_TAB & 1) != 0>::get(sut));
 }
 
 // ----------------------------------------------------------------------------
@@ -1184,6 +1195,9 @@ __global__ __launch_bounds__(320) void k_fbp_quad(SolverConsts C, const float *_
     __shared__ float2 sst[kQuadFrames * 14];
     __shared__ int sflag[3];                     // R10 ready, left arm ready, right arm ready
     __shared__ uint8_t sstat[3][kQuadFrames];    // status bits of the torso wave and the two wrist waves
+    __shared__ UnitEnt sut[2 * kUnitTabK + 1];   // the near-unit normalisation table (RTG_LAT_UNIT_TAB)
+    const auto tabF = TabSel<(RTG_LAT_UNIT_TAB & 1) != 0>::get(sut);
+    const auto tab = TabSel<(RTG_LAT_UNIT_TAB & 6) != 0>::get(sut);
     const int64_t f0 = (int64_t)blockIdx.x * kQuadFrames;
     const int nf = (int)((B - f0) < kQuadFrames ? (B - f0) : kQuadFrames);
     // the tile's rows into LDS, all loads in flight together; a frame slot past B repeats the last frame (every lane
@@ -1202,6 +1216,7 @@ __global__ __launch_bounds__(320) void k_fbp_quad(SolverConsts C, const float *_
         }
     }
     if (threadIdx.x < 3) sflag[threadIdx.x] = 0;
+    if (RTG_LAT_UNIT_TAB) unit_tab_fill(sut, (int)threadIdx.x - 256);   // wave 4, while the rows are in flight
     __syncthreads();
     // with 8 frames per block a wave's upper 8 quads repeat the lower 8 (same rows, same values, never stored)
     const int w = threadIdx.x >> 6, lane = threadIdx.x & 63, qq = lane >> 2, q = qq & (kQuadFrames - 1), sub = lane & 3;
@@ -1213,7 +1228,7 @@ __global__ __launch_bounds__(320) void k_fbp_quad(SolverConsts C, const float *_
     if (w == 0) {
         if (sub == 0) {
             bool nan = false;
-            const Q t = fbp_torso(C, b, nan);
+            const Q t = fbp_torso(C, b, nan, NoHook{}, tabF);
             sfit[q] = make_float4(t.x, t.y, t.z, t.w);
             st = nan ? kStTorsoSvd : 0u;
         }
@@ -1226,8 +1241,8 @@ __global__ __launch_bounds__(320) void k_fbp_quad(SolverConsts C, const float *_
         const float4 t = sfit[q];
         const Q R10{t.x, t.y, t.z, t.w};
         const V up = vsub(ap.el, ap.sh), fo = vsub(ap.wr, ap.el);
-        const Q ch = side ? solve_arm_lanes<21, 4>(E, up, fo, C.rsh, C.rel, R10)
-                          : solve_arm_lanes<12, 4>(E, up, fo, C.lsh, C.lel, R10);
+        const Q ch = side ? solve_arm_lanes<21, 4>(E, up, fo, C.rsh, C.rel, R10, NoHook{}, tab)
+                          : solve_arm_lanes<12, 4>(E, up, fo, C.lsh, C.lel, R10, NoHook{}, tab);
         if (sub == 0) schain[side][q] = make_float4(ch.x, ch.y, ch.z, ch.w);
         lds_signal(&sflag[1 + side]);
         finalize_lanes<4>(E, side ? 7 : 0, 4);
@@ -1238,7 +1253,7 @@ __global__ __launch_bounds__(320) void k_fbp_quad(SolverConsts C, const float *_
         float a = 0.0f;
         if (sub == 0) {
             bool nan = false;
-            W = side ? fbp_wrist_fit<1>(C, H, nan) : fbp_wrist_fit<0>(C, H, nan);
+            W = side ? fbp_wrist_fit<1>(C, H, nan, NoHook{}, tabF) : fbp_wrist_fit<0>(C, H, nan, NoHook{}, tabF);
             st = nan ? (side ? kStRightSvd : kStLeftSvd) : 0u;
             const TipPts tp = load_tips(H);
             a = hand_x_mean(qconj(W), tp.h0, tp.t);   // the gripper needs only W (:142-158 / :165-175)
@@ -1255,7 +1270,7 @@ __global__ __launch_bounds__(320) void k_fbp_quad(SolverConsts C, const float *_
                 else fbp_body_rows<0>(brow, R10, W);
             }
         }
-        const Q loc = qmul_norm(qconj(qmul_norm(R10, chain)), W);
+        const Q loc = qnormalize_t(qmul(qconj(qnormalize_t(qmul(R10, chain), tab)), W), tab);
         const bool refused = side ? emit_euler_xyz_lanes<25, 4>(E, loc) : emit_euler_xyz_lanes<16, 4>(E, loc);
         st |= refused ? (side ? kStRightEuler : kStLeftEuler) : 0u;
         finalize_lanes<4>(E, side ? 11 : 4, 3);
@@ -1287,6 +1302,8 @@ __global__ __launch_bounds__(320) void k_frame_server(SolverConsts C, const floa
 {
     __shared__ uint32_t scmd;
     __shared__ float sframe[184];
+    __shared__ UnitEnt sut[2 * kUnitTabK + 1];   // the near-unit normalisation table (RTG_FRAME1_UNIT_TAB), filled once
+    if (RTG_FRAME1_UNIT_TAB) unit_tab_fill(sut, (int)threadIdx.x - 256);   // visible after the loop's first barrier
     uint32_t last = 0;
     bool const_ok = false;   // the output rows that never change are in place (written by an unpoisoned frame)
     if (threadIdx.x == 0) last = __hip_atomic_load(ctl + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
@@ -1314,7 +1331,9 @@ __global__ __launch_bounds__(320) void k_frame_server(SolverConsts C, const floa
         // loads (tips after the wrist fit, arm points after R10) then read LDS instead of host memory
         if (threadIdx.x < 183) sframe[threadIdx.x] = in[threadIdx.x];
         __syncthreads();
-        const uint32_t bits = fbp_frame1_tile<PRECISE>(C, sframe, dof, local_rot, body_rot, !const_ok);
+        const uint32_t bits =
+            fbp_frame1_tile<PRECISE>(C, sframe, dof, local_rot, body_rot, !const_ok,
+                                     TabSel<(RTG_FRAME1_UNIT_TAB & 6) != 0>::get(sut), TabSel<(RTG_FRAME1_UNIT_TAB & 1) != 0>::get(sut));
         const_ok = bits == 0u;   // a poisoned frame overwrote every row with NaN: the next one rewrites them
         __syncthreads();   // every lane of every wave has issued its output stores (a convergent point) ...
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");   // ... so this wave's release covers all of them
