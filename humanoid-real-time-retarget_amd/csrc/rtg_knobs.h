@@ -105,7 +105,8 @@
 #define RTG_SIDES_UNIT_TAB 7   // k_solve_sides FULL_BODY_POS, SoA: near-1.0f table normalisation at (1 fits | 2 arm maps | 4 Euler split)
 #endif
 #ifndef RTG_SIDES_UNIT_TAB_AOS
-#define RTG_SIDES_UNIT_TAB_AOS 1   // the same for AoS: the fits only (the arm maps push it to 138-141 VGPRs, 3 waves/SIMD)
+#define RTG_SIDES_UNIT_TAB_AOS 1   // the same for AoS: the fits only (the arm maps push it to 138-141 VGPRs, 3 waves/SIMD;
+                                  // without the tip preload all sites fit in 120 but measured slower, profiles/r06/unit_tab/)
 #endif
 #ifndef RTG_FRAME1_UNIT_TAB
 #define RTG_FRAME1_UNIT_TAB 6   // k_fbp_frame1 / k_frame_server (B = 1): the near-1.0f table at (1 fits | 6 arm maps + Euler
