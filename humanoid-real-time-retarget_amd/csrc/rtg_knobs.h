@@ -108,6 +108,16 @@
 #define RTG_SIDES_UNIT_TAB_AOS 1   // the same for AoS: the fits only (the arm maps push it to 138-141 VGPRs, 3 waves/SIMD;
                                   // without the tip preload all sites fit in 120 but measured slower, profiles/r06/unit_tab/)
 #endif
+#ifndef RTG_FRAME1_SHARED_CODE
+#define RTG_FRAME1_SHARED_CODE 1   // k_fbp_frame1 / k_frame_server: 1 the two wrist (arm) waves run one copy of their code
+                                   // (120 -> 81 KB; B = 1 12.61-12.83 -> 12.32-12.42 us); 2 also the three fits one
+                                   // out-of-line SVD (kabsch_quat_call, 60 KB) measured slower, 12.64-12.89 us
+                                   // (profiles/r06/shared_code/)
+#endif
+#ifndef RTG_QUAD_SHARED_CODE
+#define RTG_QUAD_SHARED_CODE 1   // k_fbp_quad: the same code sharing (config 2: 16.71-16.75 -> 16.54-16.57 us; level 2
+                                 // 16.94-16.99)
+#endif
 #ifndef RTG_FRAME1_UNIT_TAB
 #define RTG_FRAME1_UNIT_TAB 6   // k_fbp_frame1 / k_frame_server (B = 1): the near-1.0f table at (1 fits | 6 arm maps + Euler
                                 // split); 6: 12.65-12.80 vs 12.88-13.10 us (profiles/r06/unit_tab/latency/)

@@ -20,6 +20,8 @@
 #pragma once
 #include "rtg_device.cuh"
 
+#include <type_traits>
+
 namespace rtg {
 
 // ----------------------------------------------------------------------------
@@ -304,6 +306,36 @@ RTG_DEV Q fbp_wrist_fit(const SolverConsts &C, const View &H, bool &svd_nan, con
     const V h0 = H.p3(0);
     const V M[5] = {vsub(H.p3(2), h0), vsub(H.p3(6), h0), vsub(H.p3(10), h0), vsub(H.p3(14), h0), vsub(H.p3(17), h0)};
     return cal_joint_quat<5>(SIDE ? C.Zr : C.Zl, M, svd_nan, hook, tab);
+}
+// the fits go through kabsch_quat_call (RTG_FRAME1_SHARED_CODE >= 2) unless they carry stage hooks (timestamp builds)
+// or the normalisation table
+template <typename Hook, typename Tab, int LEVEL = RTG_FRAME1_SHARED_CODE>
+constexpr bool kFitCall = LEVEL >= 2 && !RTG_EXP_TIMESTAMPS && std::is_same<Tab, NoTab>::value;
+// fbp_wrist_fit with a run-time side (the B = 1 kernel: both wrist waves run ONE copy of the fit's code, not two
+// template instances -- the I-cache then holds one; RTG_FRAME1_SHARED_CODE).  Z is C.Zl or C.Zr itself: the same bits.
+template <int LEVEL = RTG_FRAME1_SHARED_CODE, typename View, typename Hook = NoHook, typename Tab = NoTab>
+RTG_DEV Q fbp_wrist_fit_rt(const SolverConsts &C, const View &H, int side, bool &svd_nan, const Hook &hook = Hook{},
+                           Tab tab = Tab{})
+{
+    const V h0 = H.p3(0);
+    const V M[5] = {vsub(H.p3(2), h0), vsub(H.p3(6), h0), vsub(H.p3(10), h0), vsub(H.p3(14), h0), vsub(H.p3(17), h0)};
+    V Z[5];
+#pragma unroll
+    for (int k = 0; k < 5; ++k) Z[k] = side ? C.Zr[k] : C.Zl[k];
+    if constexpr (kFitCall<Hook, Tab, LEVEL>) return cal_joint_quat_call<5>(Z, M, svd_nan);
+    else return cal_joint_quat<5>(Z, M, svd_nan, hook, tab);
+}
+// the B = 1 kernel's torso fit, through the shared out-of-line SVD when the wrists' take it
+template <int LEVEL = RTG_FRAME1_SHARED_CODE, typename View, typename Hook = NoHook, typename Tab = NoTab>
+RTG_DEV Q fbp_torso_rt(const SolverConsts &C, const View &b, bool &svd_nan, const Hook &hook = Hook{}, Tab tab = Tab{})
+{
+    if constexpr (kFitCall<Hook, Tab, LEVEL>) {
+        const V b10 = b.p3(10);
+        const V Mt[3] = {vsub(b.p3(17), b10), vsub(b.p3(13), b10), vsub(b.p3(11), b10)};
+        return cal_joint_quat_call<3>(C.Zt, Mt, svd_nan);
+    } else {
+        return fbp_torso(C, b, svd_nan, hook, tab);
+    }
 }
 
 // A side's body points (shoulder, elbow, wrist), loaded at kernel start with the torso / wrist-fit loads of the
@@ -957,11 +989,25 @@ RTG_DEV Q solve_arm_lanes(const Emit &E, V upper, V fore, ArmZero zs, ArmZero ze
     if (w0) { E.link<L0 + 2>(y); E.link<L0 + 3>(e); }
     return qmul(qmul(qmul(p, r), y), e);
 }
+// solve_arm_lanes with a run-time first link (both arm waves of the B = 1 kernel run one copy; link_rt writes what
+// Emit::link writes when the wave has no early table words, as there)
+template <int G = 64, typename Hook = NoHook, typename Tab = NoTab>
+RTG_DEV Q solve_arm_lanes_rt(const Emit &E, int L0, V upper, V fore, ArmZero zs, ArmZero ze, Q parent,
+                             const Hook &hook = Hook{}, Tab tab = Tab{})
+{
+    const bool w0 = sublane<G>() == 0;
+    Q p, r, y, e;
+    arm_pair_lanes<true, G>(upper, zs, parent, p, r, [&](int k) { hook(k); }, tab);
+    if (w0) { link_rt(E, L0, p); link_rt(E, L0 + 1, r); }
+    arm_pair_lanes<false, G>(fore, ze, qmul(qmul(parent, p), r), y, e, [&](int k) { hook(4 + k); }, tab);
+    if (w0) { link_rt(E, L0 + 2, y); link_rt(E, L0 + 3, e); }
+    return qmul(qmul(qmul(p, r), y), e);
+}
 // emit_euler_xyz (quat_in_xyz_axis 'XYZ', scipy_as_euler's arithmetic) with the three atan2 on sub-lanes 0-2 and one
 // elementary quaternion per sub-lane; every lane of the group holds the same qf, so every lane returns the same
 // refusal flag
-template <int L0, int G = 64>
-RTG_DEV bool emit_euler_xyz_lanes(const Emit &E, Q qf)
+template <int G = 64>
+RTG_DEV bool emit_euler_xyz_lanes_rt(const Emit &E, int L0, Q qf)
 {
     const int sub = sublane<G>();
     {   // round 5: the atan2-free split (quat_in_xyz_fast, same values) on every lane -- qf is the same on all lanes
@@ -1013,6 +1059,11 @@ RTG_DEV bool emit_euler_xyz_lanes(const Emit &E, Q qf)
     }
     if (sub < 3) link_rt(E, L0 + sub, elementary_quat(sub, sub == 0 ? ang[0] : (sub == 1 ? ang[1] : ang[2])));
     return refused;
+}
+template <int L0, int G = 64>
+RTG_DEV bool emit_euler_xyz_lanes(const Emit &E, Q qf)
+{
+    return emit_euler_xyz_lanes_rt<G>(E, L0, qf);
 }
 // Emit::finalize with one slot per sub-lane (slots s0 .. s0 + n - 1, n <= G)
 template <int G = 64>
@@ -1076,7 +1127,7 @@ RTG_DEV uint32_t fbp_frame1_tile(const SolverConsts &C, const float *rows, float
     if (w == 0) {
         if (w0) {
             bool nan = false;
-            const Q q = fbp_torso(C, b, nan, hook, tabF);
+            const Q q = fbp_torso_rt(C, b, nan, hook, tabF);
             sfit = make_float4(q.x, q.y, q.z, q.w);
             st = nan ? kStTorsoSvd : 0u;
         }
@@ -1096,8 +1147,13 @@ RTG_DEV uint32_t fbp_frame1_tile(const SolverConsts &C, const float *rows, float
             if (k < 4) TS(8 + k);
             else if (k == 7) TS(12);
         };
+#if RTG_FRAME1_SHARED_CODE
+        const Q ch = solve_arm_lanes_rt(E, side ? 21 : 12, up, fo, side ? C.rsh : C.lsh, side ? C.rel : C.lel, R10, ahook,
+                                        tab);
+#else
         const Q ch = side ? solve_arm_lanes<21>(E, up, fo, C.rsh, C.rel, R10, ahook, tab)
                           : solve_arm_lanes<12>(E, up, fo, C.lsh, C.lel, R10, ahook, tab);
+#endif
         if (w0) schain[side] = make_float4(ch.x, ch.y, ch.z, ch.w);
         lds_signal(&sflag[1 + side]);
         TS(7);
@@ -1110,7 +1166,11 @@ RTG_DEV uint32_t fbp_frame1_tile(const SolverConsts &C, const float *rows, float
         float a = 0.0f;
         if (w0) {
             bool nan = false;
+#if RTG_FRAME1_SHARED_CODE
+            W = fbp_wrist_fit_rt(C, H, side, nan, hook, tabF);
+#else
             W = side ? fbp_wrist_fit<1>(C, H, nan, hook, tabF) : fbp_wrist_fit<0>(C, H, nan, hook, tabF);
+#endif
             st = nan ? (side ? kStRightSvd : kStLeftSvd) : 0u;
             const TipPts tp = load_tips(H);
             a = hand_x_mean(qconj(W), tp.h0, tp.t);   // the gripper needs only W (:142-158 / :165-175)
@@ -1129,7 +1189,11 @@ RTG_DEV uint32_t fbp_frame1_tile(const SolverConsts &C, const float *rows, float
             }
         }
         const Q loc = qnormalize_t(qmul(qconj(qnormalize_t(qmul(R10, chain), tab)), W), tab);
+#if RTG_FRAME1_SHARED_CODE
+        const bool refused = emit_euler_xyz_lanes_rt(E, side ? 25 : 16, loc);
+#else
         const bool refused = side ? emit_euler_xyz_lanes<25>(E, loc) : emit_euler_xyz_lanes<16>(E, loc);
+#endif
         st |= refused ? (side ? kStRightEuler : kStLeftEuler) : 0u;
         TS(7);
         finalize_lanes(E, side ? 11 : 4, 3);
@@ -1228,7 +1292,7 @@ __global__ __launch_bounds__(320) void k_fbp_quad(SolverConsts C, const float *_
     if (w == 0) {
         if (sub == 0) {
             bool nan = false;
-            const Q t = fbp_torso(C, b, nan, NoHook{}, tabF);
+            const Q t = fbp_torso_rt<RTG_QUAD_SHARED_CODE>(C, b, nan, NoHook{}, tabF);
             sfit[q] = make_float4(t.x, t.y, t.z, t.w);
             st = nan ? kStTorsoSvd : 0u;
         }
@@ -1241,8 +1305,13 @@ __global__ __launch_bounds__(320) void k_fbp_quad(SolverConsts C, const float *_
         const float4 t = sfit[q];
         const Q R10{t.x, t.y, t.z, t.w};
         const V up = vsub(ap.el, ap.sh), fo = vsub(ap.wr, ap.el);
+#if RTG_QUAD_SHARED_CODE
+        const Q ch = solve_arm_lanes_rt<4>(E, side ? 21 : 12, up, fo, side ? C.rsh : C.lsh, side ? C.rel : C.lel, R10,
+                                           NoHook{}, tab);
+#else
         const Q ch = side ? solve_arm_lanes<21, 4>(E, up, fo, C.rsh, C.rel, R10, NoHook{}, tab)
                           : solve_arm_lanes<12, 4>(E, up, fo, C.lsh, C.lel, R10, NoHook{}, tab);
+#endif
         if (sub == 0) schain[side][q] = make_float4(ch.x, ch.y, ch.z, ch.w);
         lds_signal(&sflag[1 + side]);
         finalize_lanes<4>(E, side ? 7 : 0, 4);
@@ -1253,7 +1322,11 @@ __global__ __launch_bounds__(320) void k_fbp_quad(SolverConsts C, const float *_
         float a = 0.0f;
         if (sub == 0) {
             bool nan = false;
+#if RTG_QUAD_SHARED_CODE
+            W = fbp_wrist_fit_rt<RTG_QUAD_SHARED_CODE>(C, H, side, nan, NoHook{}, tabF);
+#else
             W = side ? fbp_wrist_fit<1>(C, H, nan, NoHook{}, tabF) : fbp_wrist_fit<0>(C, H, nan, NoHook{}, tabF);
+#endif
             st = nan ? (side ? kStRightSvd : kStLeftSvd) : 0u;
             const TipPts tp = load_tips(H);
             a = hand_x_mean(qconj(W), tp.h0, tp.t);   // the gripper needs only W (:142-158 / :165-175)
@@ -1271,7 +1344,11 @@ __global__ __launch_bounds__(320) void k_fbp_quad(SolverConsts C, const float *_
             }
         }
         const Q loc = qnormalize_t(qmul(qconj(qnormalize_t(qmul(R10, chain), tab)), W), tab);
+#if RTG_QUAD_SHARED_CODE
+        const bool refused = emit_euler_xyz_lanes_rt<4>(E, side ? 25 : 16, loc);
+#else
         const bool refused = side ? emit_euler_xyz_lanes<25, 4>(E, loc) : emit_euler_xyz_lanes<16, 4>(E, loc);
+#endif
         st |= refused ? (side ? kStRightEuler : kStLeftEuler) : 0u;
         finalize_lanes<4>(E, side ? 11 : 4, 3);
     }
