@@ -109,9 +109,10 @@
                                   // without the tip preload all sites fit in 120 but measured slower, profiles/r06/unit_tab/)
 #endif
 #ifndef RTG_FRAME1_SHARED_CODE
-#define RTG_FRAME1_SHARED_CODE 1   // k_fbp_frame1 / k_frame_server: 1 the two wrist (arm) waves run one copy of their code
+#define RTG_FRAME1_SHARED_CODE 3   // k_fbp_frame1 / k_frame_server: 1 the two wrist (arm) waves run one copy of their code
                                    // (120 -> 81 KB; B = 1 12.61-12.83 -> 12.32-12.42 us); 2 also the three fits one
-                                   // out-of-line SVD (kabsch_quat_call, 60 KB) measured slower, 12.64-12.89 us
+                                   // out-of-line SVD (kabsch_quat_call, 60 KB) measured slower, 12.64-12.89 us; 3 the
+                                   // three fits one INLINED SVD copy after a per-wave A (60 KB): 12.13-12.38 us
                                    // (profiles/r06/shared_code/)
 #endif
 #ifndef RTG_QUAD_SHARED_CODE

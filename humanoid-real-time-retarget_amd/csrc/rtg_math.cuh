@@ -1450,10 +1450,10 @@ RTG_DEV void kabsch_rot(const float A[9], float R[9], const Hook &hook = Hook{})
 // `svd_nan` is set when A has a NaN entry: torch.linalg.svd refuses such a matrix (LAPACK sgesdd returns info = -4
 // on a NaN norm and torch raises "linalg.svd: ... contained non-finite values", transform3d.py:40), so the reference
 // frame raises there (an inf entry alone does not raise).
-template <int N, typename Hook = NoHook, typename Tab = NoTab>
-RTG_DEV Q cal_joint_quat(const V (&Z)[N], const V (&M)[N], bool &svd_nan, const Hook &hook = Hook{}, Tab tab = Tab{})
+// A = M^T Z (torch.matmul's summation order, measured) and whether it holds a NaN
+template <int N>
+RTG_DEV bool form_joint_A(const V (&Z)[N], const V (&M)[N], float (&A)[9])
 {
-    float A[9];
 #pragma unroll
     for (int i = 0; i < 3; ++i)
 #pragma unroll
@@ -1471,12 +1471,24 @@ RTG_DEV Q cal_joint_quat(const V (&Z)[N], const V (&M)[N], bool &svd_nan, const 
     bool nan = false;
 #pragma unroll
     for (int i = 0; i < 9; ++i) nan |= A[i] != A[i];
-    svd_nan = nan;
+    return nan;
+}
+// the rotation of a formed A: Kabsch then quat_from_rotation_matrix
+template <typename Hook = NoHook, typename Tab = NoTab>
+RTG_DEV Q joint_quat_of_A(const float (&A)[9], const Hook &hook = Hook{}, Tab tab = Tab{})
+{
     hook(0);
     float R[9];
     kabsch_rot(A, R, hook);
     hook(1);
     return qfrom_rotmat(R, tab);
+}
+template <int N, typename Hook = NoHook, typename Tab = NoTab>
+RTG_DEV Q cal_joint_quat(const V (&Z)[N], const V (&M)[N], bool &svd_nan, const Hook &hook = Hook{}, Tab tab = Tab{})
+{
+    float A[9];
+    svd_nan = form_joint_A<N>(Z, M, A);
+    return joint_quat_of_A(A, hook, tab);
 }
 // kabsch_rot + qfrom_rotmat out of line (the B = 1 kernel: its three fits -- torso and both wrists, on three waves at
 // once -- then run one copy of the SVD's code instead of three inlined ones; RTG_FRAME1_SHARED_CODE >= 2).  A passes

@@ -1124,10 +1124,39 @@ RTG_DEV uint32_t fbp_frame1_tile(const SolverConsts &C, const float *rows, float
     const Emit E{sdof, local_rot, C.ang_tab, sst, 1};
     const FV<false> b{rows};
     uint32_t st = 0;
+#if RTG_FRAME1_SHARED_CODE >= 3
+    // the three fits (torso on wave 0, the wrists on waves 1 / 2) form their A per wave and then run ONE inlined copy of
+    // the SVD's code (the same operations on the same A as cal_joint_quat)
+    Q fitq = qident();
+    bool fit_nan = false;
+    if (w < 3 && w0) {
+        float A[9];
+        if (w == 0) {
+            const V b10 = b.p3(10);
+            const V Mt[3] = {vsub(b.p3(17), b10), vsub(b.p3(13), b10), vsub(b.p3(11), b10)};
+            fit_nan = form_joint_A<3>(C.Zt, Mt, A);
+        } else {
+            const FV<false> H{rows + (w == 2 ? 123 : 63)};
+            const V h0 = H.p3(0);
+            const V M[5] = {vsub(H.p3(2), h0), vsub(H.p3(6), h0), vsub(H.p3(10), h0), vsub(H.p3(14), h0),
+                            vsub(H.p3(17), h0)};
+            V Z[5];
+#pragma unroll
+            for (int k = 0; k < 5; ++k) Z[k] = w == 2 ? C.Zr[k] : C.Zl[k];
+            fit_nan = form_joint_A<5>(Z, M, A);
+        }
+        fitq = joint_quat_of_A(A, hook, tabF);
+    }
+#endif
     if (w == 0) {
         if (w0) {
+#if RTG_FRAME1_SHARED_CODE >= 3
+            const Q q = fitq;
+            const bool nan = fit_nan;
+#else
             bool nan = false;
             const Q q = fbp_torso_rt(C, b, nan, hook, tabF);
+#endif
             sfit = make_float4(q.x, q.y, q.z, q.w);
             st = nan ? kStTorsoSvd : 0u;
         }
@@ -1166,7 +1195,10 @@ RTG_DEV uint32_t fbp_frame1_tile(const SolverConsts &C, const float *rows, float
         float a = 0.0f;
         if (w0) {
             bool nan = false;
-#if RTG_FRAME1_SHARED_CODE
+#if RTG_FRAME1_SHARED_CODE >= 3
+            W = fitq;
+            nan = fit_nan;
+#elif RTG_FRAME1_SHARED_CODE
             W = fbp_wrist_fit_rt(C, H, side, nan, hook, tabF);
 #else
             W = side ? fbp_wrist_fit<1>(C, H, nan, hook, tabF) : fbp_wrist_fit<0>(C, H, nan, hook, tabF);
