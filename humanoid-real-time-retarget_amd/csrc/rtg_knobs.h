@@ -116,8 +116,8 @@
                                    // (profiles/r06/shared_code/)
 #endif
 #ifndef RTG_QUAD_SHARED_CODE
-#define RTG_QUAD_SHARED_CODE 1   // k_fbp_quad: the same code sharing (config 2: 16.71-16.75 -> 16.54-16.57 us; level 2
-                                 // 16.94-16.99)
+#define RTG_QUAD_SHARED_CODE 3   // k_fbp_quad: the same code sharing (config 2: level 0 16.71-16.75, 1 16.54-16.57, 2
+                                 // 16.94-16.99, 3 16.32-16.35 us vs 16.48-16.50 for level 1 in its own A/B)
 #endif
 #ifndef RTG_FRAME1_UNIT_TAB
 #define RTG_FRAME1_UNIT_TAB 6   // k_fbp_frame1 / k_frame_server (B = 1): the near-1.0f table at (1 fits | 6 arm maps + Euler

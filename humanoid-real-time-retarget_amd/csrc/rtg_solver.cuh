@@ -1321,10 +1321,38 @@ __global__ __launch_bounds__(320) void k_fbp_quad(SolverConsts C, const float *_
     const Emit E{sdof + q * kDofStride, live && local_rot ? local_rot + f * 124 : nullptr, C.ang_tab, sst + q * 14, 1};
     const FV<false> b{rows + q * RP};
     uint32_t st = 0;
+#if RTG_QUAD_SHARED_CODE >= 3
+    // the three fits share one inlined copy of the SVD's code (k_fbp_frame1's level 3)
+    Q fitq = qident();
+    bool fit_nan = false;
+    if (w < 3 && sub == 0) {
+        float A[9];
+        if (w == 0) {
+            const V b10 = b.p3(10);
+            const V Mt[3] = {vsub(b.p3(17), b10), vsub(b.p3(13), b10), vsub(b.p3(11), b10)};
+            fit_nan = form_joint_A<3>(C.Zt, Mt, A);
+        } else {
+            const FV<false> H{rows + q * RP + (w == 2 ? 123 : 63)};
+            const V h0 = H.p3(0);
+            const V M[5] = {vsub(H.p3(2), h0), vsub(H.p3(6), h0), vsub(H.p3(10), h0), vsub(H.p3(14), h0),
+                            vsub(H.p3(17), h0)};
+            V Z[5];
+#pragma unroll
+            for (int k = 0; k < 5; ++k) Z[k] = w == 2 ? C.Zr[k] : C.Zl[k];
+            fit_nan = form_joint_A<5>(Z, M, A);
+        }
+        fitq = joint_quat_of_A(A, NoHook{}, tabF);
+    }
+#endif
     if (w == 0) {
         if (sub == 0) {
+#if RTG_QUAD_SHARED_CODE >= 3
+            const bool nan = fit_nan;
+            const Q t = fitq;
+#else
             bool nan = false;
             const Q t = fbp_torso_rt<RTG_QUAD_SHARED_CODE>(C, b, nan, NoHook{}, tabF);
+#endif
             sfit[q] = make_float4(t.x, t.y, t.z, t.w);
             st = nan ? kStTorsoSvd : 0u;
         }
@@ -1354,7 +1382,10 @@ __global__ __launch_bounds__(320) void k_fbp_quad(SolverConsts C, const float *_
         float a = 0.0f;
         if (sub == 0) {
             bool nan = false;
-#if RTG_QUAD_SHARED_CODE
+#if RTG_QUAD_SHARED_CODE >= 3
+            W = fitq;
+            nan = fit_nan;
+#elif RTG_QUAD_SHARED_CODE
             W = fbp_wrist_fit_rt<RTG_QUAD_SHARED_CODE>(C, H, side, nan, NoHook{}, tabF);
 #else
             W = side ? fbp_wrist_fit<1>(C, H, nan, NoHook{}, tabF) : fbp_wrist_fit<0>(C, H, nan, NoHook{}, tabF);
