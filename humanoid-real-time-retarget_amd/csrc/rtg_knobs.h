@@ -114,14 +114,14 @@
 #endif
 #ifndef RTG_FRAME1_SHARED_CODE
 #define RTG_FRAME1_SHARED_CODE 3   // k_fbp_frame1 / k_frame_server: 1 the two wrist (arm) waves run one copy of their code
-                                   // (120 -> 81 KB; B = 1 12.61-12.83 -> 12.32-12.42 us); 2 also the three fits one
-                                   // out-of-line SVD (kabsch_quat_call, 60 KB) measured slower, 12.64-12.89 us; 3 the
-                                   // three fits one INLINED SVD copy after a per-wave A (60 KB): 12.13-12.38 us
-                                   // (profiles/r06/shared_code/)
+                                   // (120 -> 81 KB; B = 1 12.61-12.83 -> 12.32-12.42 us); 3 also the three fits one
+                                   // INLINED SVD copy after a per-wave A (60 KB): 12.13-12.38 us.  (2, an out-of-line
+                                   // shared SVD, measured slower -- 12.64-12.89 us, call overhead -- and was removed;
+                                   // profiles/r06/shared_code/)
 #endif
 #ifndef RTG_QUAD_SHARED_CODE
-#define RTG_QUAD_SHARED_CODE 3   // k_fbp_quad: the same code sharing (config 2: level 0 16.71-16.75, 1 16.54-16.57, 2
-                                 // 16.94-16.99, 3 16.32-16.35 us vs 16.48-16.50 for level 1 in its own A/B)
+#define RTG_QUAD_SHARED_CODE 3   // k_fbp_quad: the same code sharing, levels 1 / 3 (config 2: level 0 16.71-16.75, 1
+                                 // 16.54-16.57, 3 16.32-16.35 us vs 16.48-16.50 for level 1 in its own A/B)
 #endif
 #ifndef RTG_FRAME1_UNIT_TAB
 #define RTG_FRAME1_UNIT_TAB 6   // k_fbp_frame1 / k_frame_server (B = 1): the near-1.0f table at (1 fits | 6 arm maps + Euler

@@ -1490,42 +1490,6 @@ RTG_DEV Q cal_joint_quat(const V (&Z)[N], const V (&M)[N], bool &svd_nan, const 
     svd_nan = form_joint_A<N>(Z, M, A);
     return joint_quat_of_A(A, hook, tab);
 }
-// kabsch_rot + qfrom_rotmat out of line (the B = 1 kernel: its three fits -- torso and both wrists, on three waves at
-// once -- then run one copy of the SVD's code instead of three inlined ones; RTG_FRAME1_SHARED_CODE >= 2).  A passes
-// in registers (nine scalars).
-__device__ __attribute__((noinline)) Q kabsch_quat_call(float a0, float a1, float a2, float a3, float a4, float a5,
-                                                        float a6, float a7, float a8)
-{
-    const float A[9] = {a0, a1, a2, a3, a4, a5, a6, a7, a8};
-    float R[9];
-    kabsch_rot(A, R);
-    return qfrom_rotmat(R);
-}
-// cal_joint_quat through kabsch_quat_call: the same A, the same nan flag, the same rotation
-template <int N>
-RTG_DEV Q cal_joint_quat_call(const V (&Z)[N], const V (&M)[N], bool &svd_nan)
-{
-    float A[9];
-#pragma unroll
-    for (int i = 0; i < 3; ++i)
-#pragma unroll
-        for (int k = 0; k < 3; ++k) {
-            float acc = 0.0f;
-#pragma unroll
-            for (int j = 0; j < N; ++j) {
-                const float mi = i == 0 ? M[j].x : (i == 1 ? M[j].y : M[j].z);
-                const float zk = k == 0 ? Z[j].x : (k == 1 ? Z[j].y : Z[j].z);
-                const float pr = mi * zk;
-                acc = j == 0 ? pr : acc + pr;
-            }
-            A[i * 3 + k] = acc;
-        }
-    bool nan = false;
-#pragma unroll
-    for (int i = 0; i < 9; ++i) nan |= A[i] != A[i];
-    svd_nan = nan;
-    return kabsch_quat_call(A[0], A[1], A[2], A[3], A[4], A[5], A[6], A[7], A[8]);
-}
 template <int N, typename Hook = NoHook>
 RTG_DEV Q cal_joint_quat(const V (&Z)[N], const V (&M)[N], const Hook &hook = Hook{})
 {

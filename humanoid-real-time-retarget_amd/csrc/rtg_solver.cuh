@@ -307,13 +307,9 @@ RTG_DEV Q fbp_wrist_fit(const SolverConsts &C, const View &H, bool &svd_nan, con
     const V M[5] = {vsub(H.p3(2), h0), vsub(H.p3(6), h0), vsub(H.p3(10), h0), vsub(H.p3(14), h0), vsub(H.p3(17), h0)};
     return cal_joint_quat<5>(SIDE ? C.Zr : C.Zl, M, svd_nan, hook, tab);
 }
-// the fits go through kabsch_quat_call (RTG_FRAME1_SHARED_CODE >= 2) unless they carry stage hooks (timestamp builds)
-// or the normalisation table
-template <typename Hook, typename Tab, int LEVEL = RTG_FRAME1_SHARED_CODE>
-constexpr bool kFitCall = LEVEL >= 2 && !RTG_EXP_TIMESTAMPS && std::is_same<Tab, NoTab>::value;
 // fbp_wrist_fit with a run-time side (the B = 1 kernel: both wrist waves run ONE copy of the fit's code, not two
 // template instances -- the I-cache then holds one; RTG_FRAME1_SHARED_CODE).  Z is C.Zl or C.Zr itself: the same bits.
-template <int LEVEL = RTG_FRAME1_SHARED_CODE, typename View, typename Hook = NoHook, typename Tab = NoTab>
+template <typename View, typename Hook = NoHook, typename Tab = NoTab>
 RTG_DEV Q fbp_wrist_fit_rt(const SolverConsts &C, const View &H, int side, bool &svd_nan, const Hook &hook = Hook{},
                            Tab tab = Tab{})
 {
@@ -322,22 +318,8 @@ RTG_DEV Q fbp_wrist_fit_rt(const SolverConsts &C, const View &H, int side, bool 
     V Z[5];
 #pragma unroll
     for (int k = 0; k < 5; ++k) Z[k] = side ? C.Zr[k] : C.Zl[k];
-    if constexpr (kFitCall<Hook, Tab, LEVEL>) return cal_joint_quat_call<5>(Z, M, svd_nan);
-    else return cal_joint_quat<5>(Z, M, svd_nan, hook, tab);
+    return cal_joint_quat<5>(Z, M, svd_nan, hook, tab);
 }
-// the B = 1 kernel's torso fit, through the shared out-of-line SVD when the wrists' take it
-template <int LEVEL = RTG_FRAME1_SHARED_CODE, typename View, typename Hook = NoHook, typename Tab = NoTab>
-RTG_DEV Q fbp_torso_rt(const SolverConsts &C, const View &b, bool &svd_nan, const Hook &hook = Hook{}, Tab tab = Tab{})
-{
-    if constexpr (kFitCall<Hook, Tab, LEVEL>) {
-        const V b10 = b.p3(10);
-        const V Mt[3] = {vsub(b.p3(17), b10), vsub(b.p3(13), b10), vsub(b.p3(11), b10)};
-        return cal_joint_quat_call<3>(C.Zt, Mt, svd_nan);
-    } else {
-        return fbp_torso(C, b, svd_nan, hook, tab);
-    }
-}
-
 // A side's body points (shoulder, elbow, wrist), loaded at kernel start with the torso / wrist-fit loads of the
 // same rows (measured -4 %: DESIGN.md §5), and its hand points for the gripper (0 and the tips 4,8,12,16,19).
 struct ArmPts { V sh, el, wr; };
@@ -1182,7 +1164,7 @@ RTG_DEV uint32_t fbp_frame1_tile(const SolverConsts &C, const float *rows, float
             const bool nan = fit_nan;
 #else
             bool nan = false;
-            const Q q = fbp_torso_rt(C, b, nan, hook, tabF);
+            const Q q = fbp_torso(C, b, nan, hook, tabF);
 #endif
             sfit = make_float4(q.x, q.y, q.z, q.w);
             st = nan ? kStTorsoSvd : 0u;
@@ -1378,7 +1360,7 @@ __global__ __launch_bounds__(320) void k_fbp_quad(SolverConsts C, const float *_
             const Q t = fitq;
 #else
             bool nan = false;
-            const Q t = fbp_torso_rt<RTG_QUAD_SHARED_CODE>(C, b, nan, NoHook{}, tabF);
+            const Q t = fbp_torso(C, b, nan, NoHook{}, tabF);
 #endif
             sfit[q] = make_float4(t.x, t.y, t.z, t.w);
             st = nan ? kStTorsoSvd : 0u;
@@ -1413,7 +1395,7 @@ __global__ __launch_bounds__(320) void k_fbp_quad(SolverConsts C, const float *_
             W = fitq;
             nan = fit_nan;
 #elif RTG_QUAD_SHARED_CODE
-            W = fbp_wrist_fit_rt<RTG_QUAD_SHARED_CODE>(C, H, side, nan, NoHook{}, tabF);
+            W = fbp_wrist_fit_rt(C, H, side, nan, NoHook{}, tabF);
 #else
             W = side ? fbp_wrist_fit<1>(C, H, nan, NoHook{}, tabF) : fbp_wrist_fit<0>(C, H, nan, NoHook{}, tabF);
 #endif
