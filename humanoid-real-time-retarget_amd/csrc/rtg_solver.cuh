@@ -567,46 +567,47 @@ __global__ __launch_bounds__(kSideThreads, RTG_SIDES_WAVES) void k_solve_sides(S
         // are in the L2 -- loaded after the arm chains they come back from the MALL or HBM (AoS fetch 1.57x the rows)
         constexpr bool kPreTips = RTG_AOS_PRELOAD_TIPS && !SOA;
         TipPts tpre{};
+        // RTG_SIDES_SHARED_FIT: each wave's first fit (left: torso, right: right wrist) forms its A, then both run ONE
+        // inlined copy of the SVD's code (the same operations on the same A as cal_joint_quat)
+        constexpr bool kSharedFit = RTG_SIDES_SHARED_FIT >= (SOA ? 1 : 2);
         if (live) {
-#if RTG_SIDES_SHARED_FIT
-            // each wave's first fit (left: torso, right: right wrist) forms its A, then both run ONE inlined copy of the
-            // SVD's code (the same operations on the same A as cal_joint_quat)
-            float A[9];
-            if (!side) {
-                const V b10 = b.p3(10);
-                const V Mt[3] = {vsub(b.p3(17), b10), vsub(b.p3(13), b10), vsub(b.p3(11), b10)};
-                fit1_nan = form_joint_A<3>(C.Zt, Mt, A);
+            if constexpr (kSharedFit) {
+                float A[9];
+                if (!side) {
+                    const V b10 = b.p3(10);
+                    const V Mt[3] = {vsub(b.p3(17), b10), vsub(b.p3(13), b10), vsub(b.p3(11), b10)};
+                    fit1_nan = form_joint_A<3>(C.Zt, Mt, A);
+                } else {
+                    apL = load_arm<0>(b);
+                    apR = load_arm<1>(b);
+                    const auto H = view(in2, 60);
+                    if (kPreTips) tpre = load_tips(H);
+                    const V h0 = H.p3(0);
+                    const V M[5] = {vsub(H.p3(2), h0), vsub(H.p3(6), h0), vsub(H.p3(10), h0), vsub(H.p3(14), h0),
+                                    vsub(H.p3(17), h0)};
+                    fit1_nan = form_joint_A<5>(C.Zr, M, A);
+                }
+                const Q q = joint_quat_of_A(A, hook1, tabF);
+                if (!side) {
+                    R10 = q;
+                    storso[r] = make_float4(R10.x, R10.y, R10.z, R10.w);
+                } else {
+                    W = q;
+                }
             } else {
-                apL = load_arm<0>(b);
-                apR = load_arm<1>(b);
-                const auto H = view(in2, 60);
-                if (kPreTips) tpre = load_tips(H);
-                const V h0 = H.p3(0);
-                const V M[5] = {vsub(H.p3(2), h0), vsub(H.p3(6), h0), vsub(H.p3(10), h0), vsub(H.p3(14), h0),
-                                vsub(H.p3(17), h0)};
-                fit1_nan = form_joint_A<5>(C.Zr, M, A);
+                bool nan = false;
+                if (!side) {
+                    R10 = fbp_torso(C, b, nan, hook1, tabF);
+                    storso[r] = make_float4(R10.x, R10.y, R10.z, R10.w);
+                    fit1_nan = nan;
+                } else {
+                    apL = load_arm<0>(b);
+                    apR = load_arm<1>(b);
+                    if (kPreTips) tpre = load_tips(view(in2, 60));
+                    W = fbp_wrist_fit<1>(C, view(in2, 60), nan, hook1, tabF);
+                    fit1_nan = nan;
+                }
             }
-            const Q q = joint_quat_of_A(A, hook1, tabF);
-            if (!side) {
-                R10 = q;
-                storso[r] = make_float4(R10.x, R10.y, R10.z, R10.w);
-            } else {
-                W = q;
-            }
-#else
-            bool nan = false;
-            if (!side) {
-                R10 = fbp_torso(C, b, nan, hook1, tabF);
-                storso[r] = make_float4(R10.x, R10.y, R10.z, R10.w);
-                fit1_nan = nan;
-            } else {
-                apL = load_arm<0>(b);
-                apR = load_arm<1>(b);
-                if (kPreTips) tpre = load_tips(view(in2, 60));
-                W = fbp_wrist_fit<1>(C, view(in2, 60), nan, hook1, tabF);
-                fit1_nan = nan;
-            }
-#endif
         }
         TS(3);
         if (!side) {
