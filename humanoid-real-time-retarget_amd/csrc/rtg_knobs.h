@@ -124,6 +124,10 @@
 #define RTG_QUAD_SHARED_CODE 3   // k_fbp_quad: the same code sharing, levels 1 / 3 (config 2: level 0 16.71-16.75, 1
                                  // 16.54-16.57, 3 16.32-16.35 us vs 16.48-16.50 for level 1 in its own A/B)
 #endif
+#ifndef RTG_LAT5_SHARED_CODE
+#define RTG_LAT5_SHARED_CODE 0   // A/B knob (same values), k_fbp_latency5: the frame1 / quad code sharing; measured mixed
+                                 // (24576-32768 frames +3 %, 49152 -2 %; profiles/r06/shared_code/latency5/), off
+#endif
 #ifndef RTG_FRAME1_UNIT_TAB
 #define RTG_FRAME1_UNIT_TAB 6   // k_fbp_frame1 / k_frame_server (B = 1): the near-1.0f table at (1 fits | 6 arm maps + Euler
                                 // split); 6: 12.65-12.80 vs 12.88-13.10 us (profiles/r06/unit_tab/latency/)

@@ -183,6 +183,51 @@ RTG_DEV Q solve_arm(const Emit &E, V upper, V fore, ArmZero zs, ArmZero ze, Q pa
     return qmul(qmul(qmul(p, r), y), e);
 }
 
+// Emit::link with a run-time link index (lane-parallel writers; a wave without early table words, Emit::wd null)
+RTG_DEV void link_rt(const Emit &E, int link, Q q)
+{
+    const int k = kHuDofAxis[link - 1];
+    E.st[(link <= 18 ? link - 12 : link - 14) * E.sst] = make_float2(q.w, k == 0 ? q.x : (k == 1 ? q.y : q.z));
+    if (E.lr) st4(E.lr + 4 * link, q);
+}
+// solve_arm / emit_euler_xyz with a run-time first link: two waves of a side pair run one copy of the code
+template <typename Tab = NoTab>
+RTG_DEV Q solve_arm_rt(const Emit &E, int L0, V upper, V fore, ArmZero zs, ArmZero ze, Q parent, Tab tab = Tab{})
+{
+    Q p, r, y, e;
+    {
+        const V v[1] = {upper};
+        const ArmZero z[1] = {zs};
+        const Q par[1] = {parent};
+        Q a[1], b[1];
+        arm_pair_n<true, 1>(v, z, par, a, b, tab);
+        p = a[0];
+        r = b[0];
+    }
+    link_rt(E, L0, p);
+    link_rt(E, L0 + 1, r);
+    {
+        const V v[1] = {fore};
+        const ArmZero z[1] = {ze};
+        const Q par[1] = {qmul(qmul(parent, p), r)};
+        Q a[1], b[1];
+        arm_pair_n<false, 1>(v, z, par, a, b, tab);
+        y = a[0];
+        e = b[0];
+    }
+    link_rt(E, L0 + 2, y);
+    link_rt(E, L0 + 3, e);
+    return qmul(qmul(qmul(p, r), y), e);
+}
+RTG_DEV bool emit_euler_xyz_rt(const Emit &E, int L0, Q local)
+{
+    Q eul[3];
+    const bool refused = quat_in_xyz_intrinsic(local, eul);
+    link_rt(E, L0, eul[0]);
+    link_rt(E, L0 + 1, eul[1]);
+    link_rt(E, L0 + 2, eul[2]);
+    return refused;
+}
 // quat_in_xyz_axis(q, 'XYZ') -> links L0..L0+2; true where scipy refuses q (transform3d.py:53)
 template <int L0>
 RTG_DEV bool emit_euler_xyz(const Emit &E, Q local)
@@ -820,12 +865,34 @@ RTG_DEV void fbp_latency5_tile(const SolverConsts &C, const float *__restrict__ 
     auto view = [&](const float *base, int row_floats) { return frame_view<SOA>(base, f, row_floats, B); };
     const auto b = view(in0, 63);
     bool fit_nan = false, euler_refused = false;   // this wave's raise points (lane masks, not a VGPR)
+    // RTG_LAT5_SHARED_CODE: the three fits form their A per wave and run ONE inlined copy of the SVD; the two waves
+    // of each side pair run one copy of their code (run-time side); the same operations on the same operands
+    constexpr bool kShared = RTG_LAT5_SHARED_CODE != 0;
+    Q fitq = qident();
+    if (kShared && w < 3 && live) {
+        float A[9];
+        if (w == 0) {
+            const V b10 = b.p3(10);
+            const V Mt[3] = {vsub(b.p3(17), b10), vsub(b.p3(13), b10), vsub(b.p3(11), b10)};
+            fit_nan = form_joint_A<3>(C.Zt, Mt, A);
+        } else {
+            const auto H = view(w == 2 ? in2 : in1, 60);
+            const V h0 = H.p3(0);
+            const V M[5] = {vsub(H.p3(2), h0), vsub(H.p3(6), h0), vsub(H.p3(10), h0), vsub(H.p3(14), h0),
+                            vsub(H.p3(17), h0)};
+            V Z[5];
+#pragma unroll
+            for (int k = 0; k < 5; ++k) Z[k] = w == 2 ? C.Zr[k] : C.Zl[k];
+            fit_nan = form_joint_A<5>(Z, M, A);
+        }
+        fitq = joint_quat_of_A(A, hook, tabF);
+    }
     if (w == 0) {
         if (live) {
             bool nan = false;
-            const Q q = fbp_torso(C, b, nan, hook, tabF);
+            const Q q = kShared ? fitq : fbp_torso(C, b, nan, hook, tabF);
             sfit[lane] = make_float4(q.x, q.y, q.z, q.w);
-            fit_nan = nan;
+            if (!kShared) fit_nan = nan;
         }
         lds_signal(&sflag[0]);
         TS(1);
@@ -842,8 +909,9 @@ RTG_DEV void fbp_latency5_tile(const SolverConsts &C, const float *__restrict__ 
             const float4 t = sfit[lane];
             const Q R10{t.x, t.y, t.z, t.w};
             const V up = vsub(ap.el, ap.sh), fo = vsub(ap.wr, ap.el);
-            const Q ch = side ? solve_arm<21>(E, up, fo, C.rsh, C.rel, R10, tab)
-                              : solve_arm<12>(E, up, fo, C.lsh, C.lel, R10, tab);
+            const Q ch = kShared ? solve_arm_rt(E, side ? 21 : 12, up, fo, side ? C.rsh : C.lsh, side ? C.rel : C.lel, R10, tab)
+                         : side ? solve_arm<21>(E, up, fo, C.rsh, C.rel, R10, tab)
+                                : solve_arm<12>(E, up, fo, C.lsh, C.lel, R10, tab);
             schain[side][lane] = make_float4(ch.x, ch.y, ch.z, ch.w);
         }
         lds_signal(&sflag[1 + side]);
@@ -856,9 +924,13 @@ RTG_DEV void fbp_latency5_tile(const SolverConsts &C, const float *__restrict__ 
         Q W = qident();
         TipPts tp{};
         if (live) {
-            bool nan = false;
-            W = side ? fbp_wrist_fit<1>(C, H, nan, hook, tabF) : fbp_wrist_fit<0>(C, H, nan, hook, tabF);
-            fit_nan = nan;
+            if (kShared) {
+                W = fitq;
+            } else {
+                bool nan = false;
+                W = side ? fbp_wrist_fit<1>(C, H, nan, hook, tabF) : fbp_wrist_fit<0>(C, H, nan, hook, tabF);
+                fit_nan = nan;
+            }
             tp = load_tips(H);
         }
         TS(1);
@@ -873,7 +945,8 @@ RTG_DEV void fbp_latency5_tile(const SolverConsts &C, const float *__restrict__ 
             float *brow = body_rot ? body_rot + f * 236 : nullptr;
             fbp_gripper<PRECISE>(C, a, E.row + (side ? 27 : 18));
             const Q loc = qnormalize_t(qmul(qconj(qnormalize_t(qmul(R10, chain), tab)), W), tab);
-            euler_refused = side ? emit_euler_xyz<25>(E, loc) : emit_euler_xyz<16>(E, loc);
+            euler_refused = kShared ? emit_euler_xyz_rt(E, side ? 25 : 16, loc)
+                                    : side ? emit_euler_xyz<25>(E, loc) : emit_euler_xyz<16>(E, loc);
             if (brow) {
                 if (side) fbp_body_rows<1>(brow, R10, W);
                 else fbp_body_rows<0>(brow, R10, W);
@@ -979,13 +1052,6 @@ RTG_DEV void arm_pair_lanes(V v1, ArmZero z0, Q parent, Q &first, Q &second, con
     }
     first = gbc<G, 0>(q);
     second = gbc<G, 1>(q);
-}
-// Emit::link with a run-time link index (lane-parallel writers)
-RTG_DEV void link_rt(const Emit &E, int link, Q q)
-{
-    const int k = kHuDofAxis[link - 1];
-    E.st[(link <= 18 ? link - 12 : link - 14) * E.sst] = make_float2(q.w, k == 0 ? q.x : (k == 1 ? q.y : q.z));
-    if (E.lr) st4(E.lr + 4 * link, q);
 }
 template <int L0, int G = 64, typename Hook = NoHook, typename Tab = NoTab>
 RTG_DEV Q solve_arm_lanes(const Emit &E, V upper, V fore, ArmZero zs, ArmZero ze, Q parent, const Hook &hook = Hook{},
