@@ -101,6 +101,10 @@
 #ifndef RTG_DOF_NWAY
 #define RTG_DOF_NWAY 4   // HuForwardModel lane groups: joint rotations per N-way group (one rare-case branch each)
 #endif
+#ifndef RTG_UNIT_TAB_K
+#define RTG_UNIT_TAB_K 16   // the near-unit normalisation table: the 2K + 1 f32 codes around 1.0f (32: no faster,
+                            // profiles/r06/unit_tab/ab_k32*)
+#endif
 #ifndef RTG_SIDES_SHARED_FIT
 #define RTG_SIDES_SHARED_FIT 1   // k_solve_sides FULL_BODY_POS: both waves' first fits run one inlined copy of the SVD
                                  // (134.6 -> 112.3 KB; SoA median 99.2 -> 97.9 us; AoS within noise and +1.4 % VALU, so

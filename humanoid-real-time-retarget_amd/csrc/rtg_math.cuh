@@ -572,16 +572,16 @@ RTG_DEV void qnormalize_n(const Q (&q0)[N], Q (&out)[N])   // qnormalize
 // 1.0f are a table, filled by the kernel with sqrt_clamp_rcp_exact itself (unit_tab_fill: one code per lane, while
 // its loads are in flight), so a lookup returns exactly that function's values; a |q|^2 outside the table (a
 // non-unit input row, NaN) takes the ordinary path.
-constexpr int kUnitTabK = 16;
+constexpr int kUnitTabK = RTG_UNIT_TAB_K;
 struct UnitEnt {
     double r;
     float n, pad;
 };
-RTG_DEV void unit_tab_fill(UnitEnt *tab, int t)   // t: the filling thread's index (t = 0 .. 2K fill)
+RTG_DEV void unit_tab_fill(UnitEnt *tab, int t)   // t: the filling thread's index in a wave (0 .. 63)
 {
-    if ((unsigned)t <= 2u * kUnitTabK) {
-        const NormRcp e = sqrt_clamp_rcp_exact(__int_as_float(0x3F800000 - kUnitTabK + t), 1e-9f);
-        tab[t] = UnitEnt{e.r.r, e.n, 0.0f};
+    for (int e = t; e >= 0 && e <= 2 * kUnitTabK; e += 64) {
+        const NormRcp n = sqrt_clamp_rcp_exact(__int_as_float(0x3F800000 - kUnitTabK + e), 1e-9f);
+        tab[e] = UnitEnt{n.r.r, n.n, 0.0f};
     }
 }
 RTG_DEV bool unit_tab_index(float s, uint32_t &idx)
