@@ -20,8 +20,6 @@
 #pragma once
 #include "rtg_device.cuh"
 
-#include <type_traits>
-
 namespace rtg {
 
 // ----------------------------------------------------------------------------
