@@ -110,6 +110,9 @@
                                  // (134.6 -> 112.3 KB; SoA median 99.2 -> 97.9 us; AoS within noise and +1.4 % VALU, so
                                  // 1 = SoA only, 2 = AoS too; profiles/r06/shared_code/)
 #endif
+#ifndef RTG_UPPER_UNIT_TAB
+#define RTG_UPPER_UNIT_TAB 1   // k_solve_sides UPPER_BODY: the arm maps normalise through the near-1.0f table
+#endif
 #ifndef RTG_SIDES_UNIT_TAB
 #define RTG_SIDES_UNIT_TAB 7   // k_solve_sides FULL_BODY_POS, SoA: near-1.0f table normalisation at (1 fits | 2 arm maps | 4 Euler split)
 #endif

@@ -452,8 +452,8 @@ RTG_DEV bool fbp_side_after_arm(const SolverConsts &C, const TipPts &tp, Q R10, 
 }
 
 // HuUpperBodyFromMocapRetarget (retarget_solver.py:40-99), one side: one arm given the torso fit; wrists untouched
-template <int SIDE, typename View>
-RTG_DEV void solve_upper_side(const SolverConsts &C, const View &x, Q R10, const Emit &E)
+template <int SIDE, typename View, typename Tab = NoTab>
+RTG_DEV void solve_upper_side(const SolverConsts &C, const View &x, Q R10, const Emit &E, Tab tab = Tab{})
 {
     auto pt = [&](int j) {   // coord_transform(dir=[-1,-1,1]) :41
         const Q q = upper_pt_sign(x.p3(j));
@@ -462,7 +462,7 @@ RTG_DEV void solve_upper_side(const SolverConsts &C, const View &x, Q R10, const
     constexpr int L0 = SIDE ? 21 : 12, E0 = SIDE ? 25 : 16, D0 = SIDE ? 27 : 18;
     constexpr int SH = SIDE ? 14 : 18, EL = SIDE ? 15 : 19, WR = SIDE ? 16 : 20;
     const V sel = pt(EL);
-    solve_arm<L0>(E, vsub(sel, pt(SH)), vsub(pt(WR), sel), SIDE ? C.rsh : C.lsh, SIDE ? C.rel : C.lel, R10);
+    solve_arm<L0>(E, vsub(sel, pt(SH)), vsub(pt(WR), sel), SIDE ? C.rsh : C.lsh, SIDE ? C.rel : C.lel, R10, tab);
     E.identity<E0>(); E.identity<E0 + 1>(); E.identity<E0 + 2>();
     E.row[D0] = 0.0f; E.row[D0 + 1] = 0.0f;
 }
@@ -764,6 +764,11 @@ __global__ __launch_bounds__(kSideThreads, RTG_SIDES_WAVES) void k_solve_sides(S
             // LDS (nothing for the right wave to overlap with it here).
             const auto b = view(in0, 63);   // mocap points (B, 21, 3)
             Q R10 = qident();
+            // the near-unit normalisation table for the arm maps (RTG_UPPER_UNIT_TAB), filled by the right waves while
+            // the left ones fit the torso
+            __shared__ UnitEnt sut[2 * kUnitTabK + 1];
+            if (RTG_UPPER_UNIT_TAB && side) unit_tab_fill(sut, lane);
+            const auto tab = TabSel<RTG_UPPER_UNIT_TAB != 0>::get(sut);
             if (live && !side) {
                 bool nan = false;
                 R10 = upper_torso(C, b, nan);
@@ -775,10 +780,10 @@ __global__ __launch_bounds__(kSideThreads, RTG_SIDES_WAVES) void k_solve_sides(S
                 if (side) {
                     const float4 t = storso[r];
                     R10 = Q{t.x, t.y, t.z, t.w};
-                    solve_upper_side<1>(C, b, R10, E);
+                    solve_upper_side<1>(C, b, R10, E, tab);
                 } else {
                     emit_fixed_links(E);
-                    solve_upper_side<0>(C, b, R10, E);
+                    solve_upper_side<0>(C, b, R10, E, tab);
                 }
             }
         } else if (live) {
