@@ -113,6 +113,9 @@
 #ifndef RTG_UPPER_UNIT_TAB
 #define RTG_UPPER_UNIT_TAB 1   // k_solve_sides UPPER_BODY: the arm maps normalise through the near-1.0f table
 #endif
+#ifndef RTG_ROT_UNIT_TAB
+#define RTG_ROT_UNIT_TAB 1   // k_solve_sides FULL_BODY_ROT: the normalisations through the near-1.0f table
+#endif
 #ifndef RTG_SIDES_UNIT_TAB
 #define RTG_SIDES_UNIT_TAB 7   // k_solve_sides FULL_BODY_POS, SoA: near-1.0f table normalisation at (1 fits | 2 arm maps | 4 Euler split)
 #endif

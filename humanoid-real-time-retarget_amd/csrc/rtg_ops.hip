@@ -1064,7 +1064,7 @@ int probe_valu_iters() { return kProbeIters; }
 extern "C" const char *rtg_build_info(void)
 {
     return "{\"abi\":" RTG_STR(RTG_ABI_VERSION) ",\"arch\":\"gfx950\",\"knobs\":{"
-        RTG_KNOB(RTG_DOF_NWAY) RTG_KNOB(RTG_DOF_UNIT_TAB) RTG_KNOB(RTG_FK_UNIT_TAB) RTG_KNOB(RTG_UNIT_TAB_K) RTG_KNOB(RTG_SIDES_SHARED_FIT) RTG_KNOB(RTG_UPPER_UNIT_TAB) RTG_KNOB(RTG_SIDES_UNIT_TAB) RTG_KNOB(RTG_SIDES_UNIT_TAB_AOS) RTG_KNOB(RTG_LAT_UNIT_TAB) RTG_KNOB(RTG_FRAME1_UNIT_TAB) RTG_KNOB(RTG_FRAME1_SHARED_CODE) RTG_KNOB(RTG_QUAD_SHARED_CODE) RTG_KNOB(RTG_LAT5_SHARED_CODE) RTG_KNOB(RTG_VEL_UNIT_TAB) RTG_KNOB(RTG_SIDES_WAVES) RTG_KNOB(RTG_SIDES_TILES) RTG_KNOB(RTG_SIDES_SPLIT_READOUT) RTG_KNOB(RTG_SIDES_ARMS2) RTG_KNOB(RTG_SIDES_EARLY_WORDS) RTG_KNOB(RTG_AOS_PRELOAD_TIPS) RTG_KNOB(RTG_QUAD8_MAX_B) RTG_KNOB(RTG_QUAD_MAX_B) RTG_KNOB(RTG_LATENCY_MAX_B)
+        RTG_KNOB(RTG_DOF_NWAY) RTG_KNOB(RTG_DOF_UNIT_TAB) RTG_KNOB(RTG_FK_UNIT_TAB) RTG_KNOB(RTG_UNIT_TAB_K) RTG_KNOB(RTG_SIDES_SHARED_FIT) RTG_KNOB(RTG_UPPER_UNIT_TAB) RTG_KNOB(RTG_ROT_UNIT_TAB) RTG_KNOB(RTG_SIDES_UNIT_TAB) RTG_KNOB(RTG_SIDES_UNIT_TAB_AOS) RTG_KNOB(RTG_LAT_UNIT_TAB) RTG_KNOB(RTG_FRAME1_UNIT_TAB) RTG_KNOB(RTG_FRAME1_SHARED_CODE) RTG_KNOB(RTG_QUAD_SHARED_CODE) RTG_KNOB(RTG_LAT5_SHARED_CODE) RTG_KNOB(RTG_VEL_UNIT_TAB) RTG_KNOB(RTG_SIDES_WAVES) RTG_KNOB(RTG_SIDES_TILES) RTG_KNOB(RTG_SIDES_SPLIT_READOUT) RTG_KNOB(RTG_SIDES_ARMS2) RTG_KNOB(RTG_SIDES_EARLY_WORDS) RTG_KNOB(RTG_AOS_PRELOAD_TIPS) RTG_KNOB(RTG_QUAD8_MAX_B) RTG_KNOB(RTG_QUAD_MAX_B) RTG_KNOB(RTG_LATENCY_MAX_B)
         RTG_KNOB(RTG_EXP_TIMESTAMPS) RTG_KNOB(RTG_EXP_SKIP_SIGNAL) RTG_KNOB(RTG_EXP_STUB_SVD) RTG_KNOB(RTG_EXP_NO_TABLE) RTG_KNOB(RTG_EXP_MULR_NOBRANCH) RTG_KNOB(RTG_FK_F16_MAXJ) RTG_KNOB(RTG_FK_NT_OUT) RTG_KNOB(RTG_EXP_LARTG_RCP64) RTG_KNOB(RTG_EXP_SQRT64) RTG_KNOB(RTG_EXP_SQRT_CALL) RTG_KNOB(RTG_EXP_ACOS_LIBM) RTG_KNOB(RTG_EXP_EULER_SCIPY) RTG_KNOB(RTG_VEL_SEG) RTG_KNOB(RTG_VEL_LDS_MIN) RTG_KNOB(RTG_VEL_IEEE_DIV) RTG_KNOB(RTG_DOF_NT_STORE) RTG_KNOB(RTG_IN_NT_LOAD) RTG_KNOB(RTG_VEL_W) RTG_KNOB(RTG_VEL_ANG_NB) RTG_KNOB(RTG_VEL_ANG_NWAY) RTG_KNOB(RTG_EXP_NO_RARE)
         "\"RTG_EXP_HOT_INPUTS\":\"" RTG_STR(RTG_EXP_HOT_INPUTS) "\"},\"wrong_answer_knobs\":"
         RTG_STR(RTG_WRONG_ANSWER_KNOBS) "}";

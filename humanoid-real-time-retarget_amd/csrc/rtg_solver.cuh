@@ -468,18 +468,18 @@ RTG_DEV void solve_upper_side(const SolverConsts &C, const View &x, Q R10, const
 }
 
 // VtrdynFullBodyRetargeter (full_body_retargeter.py:19-177), one side; true where scipy refuses (:121 / :138)
-template <int SIDE, typename View>
+template <int SIDE, typename View, typename Tab = NoTab>
 RTG_DEV bool solve_full_body_rot_side(const SolverConsts &C, const View &q, const View &b, const View &H,
-                                      const Emit &E)
+                                      const Emit &E, Tab tab = Tab{})
 {
     constexpr int L0 = SIDE ? 21 : 12, E0 = SIDE ? 25 : 16, D0 = SIDE ? 27 : 18;
     constexpr int SH = SIDE ? 14 : 18, EL = SIDE ? 15 : 19, WR = SIDE ? 16 : 20, PAR = SIDE ? 13 : 17;
     const Q par = q.q4(PAR);
     const V bel = b.p3(EL);
     const Q chain = solve_arm<L0>(E, vsub(bel, b.p3(SH)), vsub(b.p3(WR), bel), SIDE ? C.rsh : C.lsh,
-                                  SIDE ? C.rel : C.lel, par);
+                                  SIDE ? C.rel : C.lel, par, tab);
     const Q w = q.q4(WR);
-    const bool refused = emit_euler_xyz<E0>(E, qmul_norm(qconj(qmul_norm(par, chain)), w));
+    const bool refused = emit_euler_xyz<E0>(E, qnormalize_t(qmul(qconj(qnormalize_t(qmul(par, chain), tab)), w), tab));
     constexpr int tips[5] = {3, 7, 11, 15, 19};   // :145-177 rotates by the wrist quaternion itself
     const bool closed = hand_x_mean(w, H, tips) / C.orig < 0.7f;
     E.row[D0] = closed ? 0.0f : 0.044f;
@@ -488,20 +488,20 @@ RTG_DEV bool solve_full_body_rot_side(const SolverConsts &C, const View &q, cons
 }
 
 // Mocap2HuBodyRetargeter (body_retargeter.py:34-81), one side; true where scipy refuses either split (:42-55)
-template <int SIDE, typename View>
-RTG_DEV bool solve_body_rot_side(const SolverConsts &C, const View &g, const Emit &E)
+template <int SIDE, typename View, typename Tab = NoTab>
+RTG_DEV bool solve_body_rot_side(const SolverConsts &C, const View &g, const Emit &E, Tab tab = Tab{})
 {
-    auto local = [&](int j, int p) { return qmul_norm(qconj(g.q4(p)), g.q4(j)); };
+    auto local = [&](int j, int p) { return qnormalize_t(qmul(qconj(g.q4(p)), g.q4(j)), tab); };
     constexpr int SH = SIDE ? 14 : 18, EL = SIDE ? 15 : 19, D0 = SIDE ? 27 : 18;
     Q s3[3], e3[3];
     bool refused = quat_in_xyz_axis(local(SH, C.par[SIDE ? 1 : 0]), 1, 0, 2, false, s3);   // 'YXZ'
     refused |= quat_in_xyz_axis(local(EL, C.par[SIDE ? 3 : 2]), 2, 1, 0, false, e3);       // 'ZYX'
     if (SIDE) {
-        E.link<21>(s3[0]); E.link<22>(s3[1]); E.link<23>(qmul_norm(e3[0], s3[2]));
+        E.link<21>(s3[0]); E.link<22>(s3[1]); E.link<23>(qnormalize_t(qmul(e3[0], s3[2]), tab));
         E.link<24>(e3[1]); E.link<25>(e3[2]);
         E.identity<26>(); E.identity<27>();
     } else {
-        E.link<12>(s3[0]); E.link<13>(s3[1]); E.link<14>(qmul_norm(e3[0], s3[2]));
+        E.link<12>(s3[0]); E.link<13>(s3[1]); E.link<14>(qnormalize_t(qmul(e3[0], s3[2]), tab));
         E.link<15>(e3[1]); E.link<16>(e3[2]);
         E.identity<17>(); E.identity<18>();
     }
@@ -786,16 +786,32 @@ __global__ __launch_bounds__(kSideThreads, RTG_SIDES_WAVES) void k_solve_sides(S
                     solve_upper_side<0>(C, b, R10, E, tab);
                 }
             }
-        } else if (live) {
-            if (!side) emit_fixed_links(E);
-            bool refused;
-            if constexpr (KIND == RTG_SOLVER_FULL_BODY_ROT) {
-                refused = side ? solve_full_body_rot_side<1>(C, view(in0, 84), view(in1, 63), view(in3, 60), E)
-                               : solve_full_body_rot_side<0>(C, view(in0, 84), view(in1, 63), view(in2, 60), E);
-            } else {
-                refused = side ? solve_body_rot_side<1>(C, view(in0, 84), E) : solve_body_rot_side<0>(C, view(in0, 84), E);
+        } else {
+            // the near-unit normalisation table (RTG_ROT_UNIT_TAB, FULL_BODY_ROT: 56.5-57.0 -> 53.9-54.8 us; BODY_ROT
+            // measured 2 % slower with it, off): one copy per wave, filled by ALL its lanes (live or not: a batch's last
+            // tile has idle lanes) and read by the wave itself (its LDS operations execute in order; the fences keep
+            // the compiler from reordering them)
+            constexpr bool kRotTab = RTG_ROT_UNIT_TAB && KIND == RTG_SOLVER_FULL_BODY_ROT;
+            __shared__ UnitEnt sutw[2 * kSideTiles][2 * kUnitTabK + 1];
+            if (kRotTab) {
+                unit_tab_fill(sutw[w], lane);
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+                __builtin_amdgcn_wave_barrier();
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
             }
-            st |= refused ? (side ? kStRightEuler : kStLeftEuler) : 0u;
+            const auto tab = TabSel<kRotTab>::get(sutw[w]);
+            if (live) {
+                if (!side) emit_fixed_links(E);
+                bool refused;
+                if constexpr (KIND == RTG_SOLVER_FULL_BODY_ROT) {
+                    refused = side ? solve_full_body_rot_side<1>(C, view(in0, 84), view(in1, 63), view(in3, 60), E, tab)
+                                   : solve_full_body_rot_side<0>(C, view(in0, 84), view(in1, 63), view(in2, 60), E, tab);
+                } else {
+                    refused = side ? solve_body_rot_side<1>(C, view(in0, 84), E, tab)
+                                   : solve_body_rot_side<0>(C, view(in0, 84), E, tab);
+                }
+                st |= refused ? (side ? kStRightEuler : kStLeftEuler) : 0u;
+            }
         }
         if (live) E.finalize(side ? 7 : 0, 7);   // each wave reads out its own side's slots
         sstat[side][r] = (uint8_t)st;
